@@ -1,0 +1,153 @@
+"""Generate the golden parity fixtures by running the REFERENCE itself (survey container only).
+
+Imports the reference model class `WhisperForConditionalGenerationWeightCE`
+(`/root/reference/models/whisper_medical.py`) and HF's `WhisperFeatureExtractor` (the A1 code the
+reference calls at `data_utils/data_loader.py:171`), feeds them the build's seeded bf16-rounded
+synthetic weights and synthetic clips, and stores SMALL slices / summaries of their outputs as
+`tests/golden/*.npz`. The fixtures are data (inputs are regenerated from seeds; expected outputs
+are slices), never reference source. The reference does not travel to the GPU box; only these
+fixtures do.
+
+Harness-side shim (no reference file is edited): `_tied_weights_keys` is a list in the reference
+(`models/whisper_medical.py:14`, 4.x convention) and transformers 5.x expects a dict
+(SURVEY.md §8(c)).
+
+Decode semantics follow `scripts/evaluation.py:173-180`: bare GenerationConfig(max_length, pad,
+eos, decoder_start, use_cache=False), no suppression, fp32, greedy.
+
+Run:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+REF = "/root/reference"
+
+from whisper_context_biasing_amd.config import get_dims  # noqa: E402
+from whisper_context_biasing_amd.weights import make_weights  # noqa: E402
+from whisper_context_biasing_amd.synth import synth_batch, synth_clip  # noqa: E402
+
+MEL_COLS = [slice(0, 48), slice(1476, 1524), slice(2952, 3000)]
+ENC_ROWS = [slice(0, 4), slice(748, 752), slice(1496, 1500)]
+VOCAB_PROBE = np.array([0, 1, 2, 13, 220, 1000, 5000, 12345, 25000, 40000, 50255, 50256, 50257,
+                        50258, 50300, 50363, 51000, 51863], dtype=np.int64)
+
+
+def ref_model(dims, sd, attn="sdpa"):
+    sys.path.insert(0, REF)
+    from transformers import WhisperConfig
+    from models.whisper_medical import WhisperForConditionalGenerationWeightCE as Ref
+    Ref._tied_weights_keys = {"proj_out.weight": "model.decoder.embed_tokens.weight"}  # shim
+    cfg = WhisperConfig(**dims.hf_config_kwargs())
+    cfg._attn_implementation = attn
+    torch.manual_seed(0)
+    m = Ref(cfg, bias_weight=10.0)
+    state = {k: torch.from_numpy(v) for k, v in sd.items()}
+    state["proj_out.weight"] = state["model.decoder.embed_tokens.weight"]
+    missing, unexpected = m.load_state_dict(state, strict=False)
+    assert not unexpected, unexpected
+    assert all(k == "proj_out.weight" for k in missing), missing
+    m.eval()
+    assert m.proj_out.weight.data_ptr() == m.model.decoder.embed_tokens.weight.data_ptr() or \
+        torch.equal(m.proj_out.weight, m.model.decoder.embed_tokens.weight)
+    return m
+
+
+def mel_fixture():
+    from transformers import WhisperFeatureExtractor
+    clips = [synth_clip(0), synth_clip(1), synth_clip(2, n_samples=5 * 16000),
+             (synth_clip(3) * 0.001).astype(np.float32)]
+    out = {}
+    for n_mel in (80, 128):
+        fe = WhisperFeatureExtractor(feature_size=n_mel)
+        out[f"filters_{n_mel}"] = fe.mel_filters.astype(np.float64)
+        for i, c in enumerate(clips):
+            # single-waveform call exactly like data_utils/data_loader.py:171-172
+            m = fe(c, sampling_rate=16000).input_features[0]
+            assert m.shape == (n_mel, 3000), m.shape
+            out[f"mel{n_mel}_clip{i}_slices"] = np.concatenate([m[:, s] for s in MEL_COLS], axis=1)
+            out[f"mel{n_mel}_clip{i}_stats"] = np.array(
+                [m.sum(dtype=np.float64), np.abs(m).sum(dtype=np.float64), m.max(), m.min()])
+    np.savez_compressed(os.path.join(HERE, "mel_golden.npz"), **out)
+    print("mel fixture written")
+
+
+def model_fixture(size, seed, recipe, B, n_tokens, tf_len, beams=True):
+    from transformers import GenerationConfig
+    dims = get_dims(size)
+    sd = make_weights(dims, seed=seed, recipe=recipe)
+    from transformers import WhisperFeatureExtractor
+    fe = WhisperFeatureExtractor(feature_size=dims.n_mel)
+    pcm = synth_batch(B)
+    mel = np.stack([fe(c, sampling_rate=16000).input_features[0] for c in pcm]).astype(np.float32)
+    out = {"mel_sum": mel.sum(dtype=np.float64)}
+    rng = np.random.default_rng(seed + 17)
+    dec_ids = np.concatenate([np.full((B, 1), dims.decoder_start_token_id),
+                              rng.integers(0, dims.eos_token_id, size=(B, tf_len - 1))], axis=1)
+    out["tf_decoder_input_ids"] = dec_ids
+    res = {}
+    for attn in ("sdpa", "eager"):
+        m = ref_model(dims, sd, attn)
+        with torch.no_grad():
+            x = torch.from_numpy(mel)
+            enc = m.model.encoder(x).last_hidden_state.numpy()
+            fw = m(input_features=x, decoder_input_ids=torch.from_numpy(dec_ids), return_dict=True)
+            logits = fw.logits.float().numpy()
+            gc = GenerationConfig(max_length=n_tokens, pad_token_id=dims.pad_token_id,
+                                  eos_token_id=dims.eos_token_id,
+                                  decoder_start_token_id=dims.decoder_start_token_id, use_cache=False)
+            # scripts/evaluation.py:173-182: the bare config replaces model.generation_config;
+            # Seq2SeqTrainer then calls generate(**inputs, max_length=...) ([tf] trainer_seq2seq.py:329)
+            m.generation_config = gc
+            m.config.use_cache = False
+            m.config.suppress_tokens = []
+            g = m.generate(input_features=x, max_length=n_tokens, return_dict_in_generate=True,
+                           output_scores=True)
+            ids = g.sequences.numpy()
+            scores = torch.stack(g.scores, 1).float().numpy()       # [B, steps, V]
+            plain = m.generate(input_features=x, max_length=n_tokens).numpy()
+            res[attn] = (enc, logits, ids, scores, plain)
+            if attn == "sdpa" and beams:
+                gcb = GenerationConfig(max_length=min(n_tokens, 24), pad_token_id=dims.pad_token_id,
+                                       eos_token_id=dims.eos_token_id, num_beams=5,
+                                       decoder_start_token_id=dims.decoder_start_token_id, use_cache=True)
+                out["beam5_ids"] = m.generate(input_features=x, generation_config=gcb).numpy()
+    enc, logits, ids, scores, plain = res["sdpa"]
+    out["enc_slices"] = np.concatenate([enc[:, s] for s in ENC_ROWS], axis=1)
+    out["enc_stats"] = np.array([enc.sum(dtype=np.float64), np.abs(enc).sum(dtype=np.float64)])
+    out["tf_logits_probe"] = logits[:, :, VOCAB_PROBE]
+    out["tf_logits_top5_idx"] = np.argsort(-logits, axis=-1, kind="stable")[:, :, :5]
+    out["tf_logits_top5_val"] = np.take_along_axis(logits, out["tf_logits_top5_idx"], -1)
+    lse = np.log(np.exp(logits - logits.max(-1, keepdims=True)).sum(-1)) + logits.max(-1)
+    out["tf_logits_lse"] = lse
+    out["greedy_sequences"] = ids                    # return_dict_in_generate: includes SOT
+    out["greedy_ids"] = plain                        # plain generate(): SOT stripped, pad-right
+    srt = np.sort(scores, axis=-1)
+    out["greedy_margin"] = srt[..., -1] - srt[..., -2]
+    out["greedy_top1"] = scores.argmax(-1)
+    out["greedy_step_max"] = srt[..., -1]
+    e_enc, e_logits, e_ids, _, _ = res["eager"]
+    out["eager_vs_sdpa_enc_maxdiff"] = np.abs(e_enc - enc).max()
+    out["eager_vs_sdpa_logits_maxdiff"] = np.abs(e_logits - logits).max()
+    out["eager_greedy_ids"] = e_ids
+    meta = dict(size=size, seed=seed, recipe=recipe, B=B, n_tokens=n_tokens)
+    out["meta"] = np.array([str(meta)])
+    name = f"model_{size}_{recipe}_s{seed}.npz"
+    np.savez_compressed(os.path.join(HERE, name), **out)
+    print(name, "greedy", plain.shape, "min margin", out["greedy_margin"].min(),
+          "eager/sdpa enc diff", out["eager_vs_sdpa_enc_maxdiff"])
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    mel_fixture()
+    model_fixture("micro", 0, "diverse", B=2, n_tokens=32, tf_len=8)
+    model_fixture("tiny.en", 0, "diverse", B=2, n_tokens=48, tf_len=6)
+    model_fixture("tiny.en", 1, "margin", B=2, n_tokens=48, tf_len=6, beams=False)
