@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Benchmark of the Whisper contextual-biasing hot path on MI355X (BASELINE.json metric).
+
+One "step" = the full inference path for one batch of synthetic 30 s / 16 kHz clips already
+resident in HBM: log-mel → encoder → greedy decode of exactly 64 new tokens (EOS masked,
+SURVEY.md §8(d) benchmark mode) with the fused bias-list boost (1000 phrases, lambda 2.0).
+Default workload = config C2: whisper-small, batch 32 per GPU, bf16 (random-init weights of that
+architecture; no checkpoint offline).
+
+Multi-GPU (`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`): one process
+per GPU, utterances sharded (weak scaling: 32 clips per GPU), weights generated on rank 0 and
+broadcast once over RCCL/xGMI (`dist.broadcast`), no collective in the timed region besides the
+barriers; time = max over ranks.
+
+Prints ONE JSON line (rank 0) with the driver's contract fields plus `roofline` (dominant kernel:
+the encoder MFMA GEMMs, timed with HIP events on the library's stream inside the timed region)
+and `cpu_baseline` (the numpy oracle timed on this host, rank 0 / N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
+PEAK_F16_TFLOPS = 2500.0
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(size: str, n_tokens: int, n_phr: int, boost: float, seed: int = 0):
+    """numpy oracle (test infrastructure) on a bounded sample: 1 clip, log-mel + encoder + KV-cached
+    greedy decode of n_tokens with the same bias list and boost. Returns audio-s/s."""
+    from oracle import whisper_np as W
+    from whisper_context_biasing_amd.config import get_dims
+    from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list
+    from whisper_context_biasing_amd.weights import make_weights
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    dims = get_dims(size)
+    om = W.OracleModel.from_dims(dims, make_weights(dims, seed=seed))
+    pcm = synth_batch(1)
+    phrases = synth_bias_list(n_phr, eot=dims.eos_token_id)
+    t0 = time.perf_counter()
+    mel = W.log_mel(pcm, dims.n_mel)
+    om.generate(mel, max_length=n_tokens, min_new_tokens=n_tokens, bias=phrases, bias_boost=boost)
+    dt = time.perf_counter() - t0
+    return {"value": round(30.0 / dt, 3), "unit": "audio-seconds/sec", "cores": int(threads), "kind": "port",
+            "sample": f"1 clip x 30 s, {size} fp32 numpy oracle (oracle/whisper_np.py): log-mel + encoder + "
+                      f"{n_tokens} KV-cached greedy tokens with {n_phr}-phrase boost; {dt:.2f} s wall"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="small")
+    ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
+    ap.add_argument("--new-tokens", type=int, default=64)
+    ap.add_argument("--bias-phrases", type=int, default=1000)
+    ap.add_argument("--boost", type=float, default=2.0)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from whisper_context_biasing_amd.config import get_dims
+    from whisper_context_biasing_amd.model import WhisperCB
+    from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list
+    from whisper_context_biasing_amd.weights import make_weights, param_shapes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    dims = get_dims(args.model)
+    # ---- weights: rank 0 generates, one RCCL broadcast of the packed bf16 blob over xGMI
+    names = [n for n, _ in param_shapes(dims)]
+    shapes = dict(param_shapes(dims))
+    numel = [int(np.prod(shapes[n])) for n in names]
+    if rank == 0:
+        sd = make_weights(dims, seed=0)
+        flat = torch.cat([torch.from_numpy(sd[n]).reshape(-1) for n in names]).to(torch.bfloat16).to(dev)
+        del sd
+    else:
+        flat = torch.empty(sum(numel), dtype=torch.bfloat16, device=dev)
+    if world > 1:
+        t0 = time.perf_counter()
+        dist.broadcast(flat, src=0)
+        torch.cuda.synchronize()
+        log(f"rank {rank}: weight broadcast {flat.numel() * 2 / 1e9:.3f} GB in {time.perf_counter() - t0:.3f} s")
+    host = flat.float().cpu().numpy()
+    sd, off = {}, 0
+    for n, k in zip(names, numel):
+        sd[n] = host[off:off + k].reshape(shapes[n])
+        off += k
+    model = WhisperCB.from_state_dict(dims, sd, dtype=args.dtype, device=local)
+    del sd, host, flat
+
+    B = args.batch
+    pcm = torch.from_numpy(synth_batch(B, start=rank * B)).to(dev)     # resident in HBM before timing
+    phrases = synth_bias_list(args.bias_phrases, eot=dims.eos_token_id)
+    bias = model.bias_list(phrases)
+    use_graph = not args.no_graph
+
+    def step():
+        mel = model.log_mel(pcm)
+        return model.generate(mel, max_length=args.new_tokens, min_new_tokens=args.new_tokens,
+                              bias_list=phrases, bias_boost=args.boost, use_graph=use_graph)
+
+    for i in range(args.warmup):
+        ids = step()
+        torch.cuda.synchronize()
+        log(f"warmup {i} done, ids {tuple(ids.shape)}")
+    assert ids.shape == (B, args.new_tokens)
+    if not args.no_profile:
+        model.profile_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    prof = model.profile_read() if not args.no_profile else {}
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * B * 30.0 / (elapsed / args.steps)
+
+    roof = None
+    if prof.get("enc_gemm"):
+        p = prof["enc_gemm"]
+        per_launch_flops = p["flops"] / p["launches"]
+        avg_ms = p["ms"] / p["launches"]
+        achieved = per_launch_flops / (avg_ms * 1e-3) / 1e12
+        peak = {"bf16": PEAK_BF16_TFLOPS, "f16": PEAK_F16_TFLOPS}.get(args.dtype, PEAK_F32_TFLOPS)
+        roof = {"bound": "mfma", "kernel": "gemm_tile_kernel (encoder conv/QKV/out/fc1/fc2)",
+                "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": None,
+                "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": per_launch_flops}
+    phases = {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "launches_per_step": v["launches"] / args.steps}
+              for k, v in prof.items()}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("timing the CPU oracle baseline ...")
+        cpu = cpu_baseline(args.model, args.new_tokens, args.bias_phrases, args.boost)
+
+    if rank == 0:
+        out = {
+            "metric": "audio-seconds/sec (RTF) + biased-WER, whisper-small 30s clips, batch32",
+            "value": round(value, 2), "unit": "audio-seconds/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (seeded 30 s/16 kHz clips, random-init weights of the named architecture)",
+            "config": {"workload": f"C2: whisper-{args.model}, {B} clips/GPU x 30 s, log-mel + encoder + "
+                                   f"{args.new_tokens}-token greedy decode, {args.bias_phrases}-phrase bias boost "
+                                   f"lambda={args.boost}", "global_batch": world * B, "parallelism": f"utterance-dp{world}",
+                       "hipgraph_decode": use_graph},
+            "rtf": round(1.0 / (value / world), 6),
+            "roofline": roof,
+            "phases": phases,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,116 @@
+/* libwcb — MI355X-native Whisper contextual-biasing inference path (C ABI).
+ *
+ * The reference exposes no native plugin API: its hot-path boundary is the Python class contract of
+ * `WhisperForConditionalGenerationWeightCE` (models/whisper_medical.py:12-172) driven by
+ * `scripts/evaluation.py:164-206` and the feature extractor call at data_utils/data_loader.py:171.
+ * Each entry point below replaces one piece of that surface; the Python mirror
+ * `whisper_context_biasing_amd.model.WhisperCB` binds them with ctypes.
+ *
+ * Conventions: return 0 on success, a negative wcb_status otherwise (message: wcb_last_error);
+ * no exception crosses the ABI. Activation buffers are caller-owned DEVICE memory; weights,
+ * workspaces and KV caches are library-owned. One handle per GPU; calls on one handle are
+ * serialised by the caller. `stream` is a hipStream_t (NULL = default stream).
+ */
+#ifndef WCB_H_
+#define WCB_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct wcb_handle wcb_handle;
+typedef struct wcb_bias wcb_bias;
+
+enum wcb_status {
+  WCB_OK = 0,
+  WCB_ERR_ARG = -1,       /* invalid argument / shape (ValueError in the reference) */
+  WCB_ERR_STATE = -2,     /* call out of order (e.g. weights not finalized) */
+  WCB_ERR_HIP = -3,       /* HIP runtime error */
+  WCB_ERR_UNSUPPORTED = -4
+};
+
+enum wcb_dtype { WCB_BF16 = 0, WCB_F16 = 1, WCB_F32 = 2 };
+
+/* Model dimensions (HF WhisperConfig fields; encoder and decoder depth are equal for every size). */
+typedef struct {
+  int d_model, n_layers, n_heads, ffn, vocab, n_mel;
+  int n_audio_ctx;   /* 1500 */
+  int n_text_ctx;    /* 448 */
+  int eos_token_id, pad_token_id, decoder_start_token_id;
+  int dtype;         /* wcb_dtype of weights and activations (f32 accumulation everywhere) */
+} wcb_model_desc;
+
+/* Decode configuration (replaces the GenerationConfig of scripts/evaluation.py:173-179). */
+typedef struct {
+  int max_new_tokens;   /* generate(max_length=N) of the reference → at most N new tokens */
+  int min_new_tokens;   /* EOS masked while fewer tokens were generated (benchmark mode) */
+  int num_beams;        /* 1 = greedy (the reference eval setting) */
+  float bias_boost;     /* lambda >= 0 of the bias-list boost; 0 = plain greedy bit-for-bit */
+  int use_graph;        /* replay the decode step as a captured hipGraph */
+} wcb_gen_cfg;
+
+/* replaces WhisperForConditionalGenerationWeightCE(config) (models/whisper_medical.py:16-22) */
+int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out);
+void wcb_destroy(wcb_handle* h);
+const char* wcb_last_error(const wcb_handle* h);
+
+/* replaces from_pretrained / load_state_dict: one HF state-dict tensor (host f32, C order).
+ * Names follow the reference's state dict (model.encoder.layers.{i}.self_attn.q_proj.weight, ...).
+ * proj_out.weight is tied to model.decoder.embed_tokens.weight (models/whisper_medical.py:14). */
+int wcb_set_weight(wcb_handle* h, const char* name, const float* data, const int64_t* shape, int ndim);
+/* repack every tensor into the device layout (fused QKV, q pre-scaled, im2col conv weights,
+ * all-layer cross-KV projection) and upload; host copies are released. */
+int wcb_finalize_weights(wcb_handle* h);
+
+/* replaces WhisperFeatureExtractor.__call__ (data_utils/data_loader.py:171-172):
+ * pcm f32 [B][pcm_stride] (first n_samples valid, zero-padded/trimmed to 480000)
+ * → mel_out f32 [B][n_mel][3000]. */
+int wcb_log_mel(wcb_handle* h, const float* pcm, int B, int n_samples, int64_t pcm_stride, float* mel_out,
+                void* stream);
+
+/* replaces WhisperEncoder.forward ([tf] modeling_whisper.py:592-646): mel f32 [B][n_mel][3000]
+ * → enc_out [B][1500][d] in the model dtype (may be NULL: result kept internally for decode). */
+int wcb_encode(wcb_handle* h, const float* mel, int B, void* enc_out, void* stream);
+
+/* replaces model.generate(input_features, max_length=...) as called by
+ * [tf] trainer_seq2seq.py:329: greedy from [decoder_start] (+ optional prefix), bias boost,
+ * out_ids int32 DEVICE [B][cfg->max_new_tokens] (finished rows padded with pad_token_id),
+ * *out_steps = number of generated columns (all rows finished or max_new_tokens). */
+int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg, const wcb_bias* bias,
+                 const int32_t* prefix, int prefix_len, int32_t* out_ids, int32_t* out_steps, void* stream);
+
+/* replaces forward(input_features, decoder_input_ids) (models/whisper_medical.py:45-111):
+ * dec_ids int32 DEVICE [B][T] → logits f32 DEVICE [B][T][vocab]; enc_out as in wcb_encode. */
+int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, int T, float* logits,
+                void* enc_out, void* stream);
+
+/* bias list: n_phrases token sequences, phrase i = tokens[offsets[i] .. offsets[i+1]) (host
+ * arrays). Built into an Aho-Corasick automaton on the device (boost semantics: k_select.hip). */
+int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets, int n_phrases,
+                    wcb_bias** out);
+void wcb_bias_destroy(wcb_bias* b);
+int wcb_bias_num_states(const wcb_bias* b);
+
+/* per-kernel time accounting for the benchmark's roofline (HIP events on the launch stream) */
+int wcb_profile_enable(wcb_handle* h, int enable);
+/* fills up to n entries: name, launches, total milliseconds, algorithmic flops, algorithmic bytes */
+int wcb_profile_read(wcb_handle* h, int n, char (*names)[32], int64_t* launches, double* ms,
+                     double* flops, double* bytes);
+
+/* ---- kernel-level entry points (parity tests and microbenchmarks) ---- */
+/* out[M][N] = act(A[M][K] · W[N][K]ᵀ + bias) (+ resid), row-major, dtype of A/W = dtype */
+int wcb_op_gemm(int dtype, const void* A, const void* W, int M, int N, int K, const float* bias, int act,
+                const float* resid, void* out, int out_f32, void* stream);
+/* y[M][d] (dtype) = LayerNorm(x f32 [M][d]) * w + b, eps 1e-5 */
+int wcb_op_layernorm(int dtype, const float* x, const float* w, const float* b, void* y, int M, int d,
+                     void* stream);
+/* o[B][Sq][H*64] = softmax(q kᵀ) v per head (q pre-scaled), k/v [B][Sk][H*64];
+ * flash=1 selects the MFMA kernel (16-bit dtypes). */
+int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H, int Sq,
+                     int Sk, int flash, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WCB_H_ */

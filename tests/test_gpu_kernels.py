@@ -1,0 +1,168 @@
+"""GPU: kernel-level parity of libwcb entry points (wcb_op_*, wcb_log_mel) against fp32/fp64
+references of the same op. Tolerances are written per test."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from whisper_context_biasing_amd import _lib  # noqa: E402
+
+DT = {"bf16": (torch.bfloat16, _lib.WCB_BF16), "f16": (torch.float16, _lib.WCB_F16), "f32": (torch.float32, _lib.WCB_F32)}
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _gemm(dt, A, W, bias=None, act=0, resid=None, out_f32=True):
+    lib = _lib.load()
+    M, K = A.shape
+    N = W.shape[0]
+    out = torch.empty(M, N, device="cuda", dtype=torch.float32 if out_f32 else A.dtype)
+    _lib.check(lib.wcb_op_gemm(DT[dt][1], A.data_ptr(), W.data_ptr(), M, N, K,
+                               bias.data_ptr() if bias is not None else None, act,
+                               resid.data_ptr() if resid is not None else None, out.data_ptr(),
+                               int(out_f32), _s()), None, "gemm")
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16", "f32"])
+@pytest.mark.parametrize("shape", [(256, 256, 256), (300, 192, 512), (16, 2304, 768), (40, 1000, 384),
+                                   (1500, 768, 768), (3, 51864, 384)])
+def test_gemm_matches_fp64(dt, shape):
+    M, N, K = shape
+    if dt == "f32" and K % 32:
+        pytest.skip()
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N)
+    A = torch.randn(M, K, generator=g).to(DT[dt][0]).cuda()
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(DT[dt][0]).cuda()
+    bias = torch.randn(N, generator=g).float().cuda()
+    out = _gemm(dt, A, W, bias=bias)
+    ref = A.double() @ W.double().T + bias.double()
+    scale = (A.double().abs() @ W.double().abs().T) + 1.0
+    # exact products, f32 accumulation: error bounded by ~K·2^-24 relative to Σ|a·b|
+    err = ((out.double() - ref).abs() / scale).max().item()
+    assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+def test_gemm_epilogues(dt):
+    M, N, K = 384, 256, 256
+    g = torch.Generator(device="cpu").manual_seed(3)
+    A = torch.randn(M, K, generator=g).to(DT[dt][0]).cuda()
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(DT[dt][0]).cuda()
+    bias = torch.randn(N, generator=g).float().cuda()
+    resid = torch.randn(M, N, generator=g).float().cuda()
+    ref = A.double() @ W.double().T + bias.double()
+    gel = torch.nn.functional.gelu(ref)
+    out = _gemm(dt, A, W, bias=bias, act=1)
+    assert (out.double() - gel).abs().max().item() < 1e-4
+    out = _gemm(dt, A, W, bias=bias, resid=resid.clone())
+    assert (out.double() - (ref + resid.double())).abs().max().item() < 1e-4
+    out = _gemm(dt, A, W, bias=bias, act=1, out_f32=False)
+    tol = 1e-5 if dt == "f32" else 8e-3
+    assert ((out.double() - gel).abs() / (gel.abs() + 1e-2)).max().item() < tol * 4
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+@pytest.mark.parametrize("d", [64, 384, 768, 1280])
+def test_layernorm(dt, d):
+    lib = _lib.load()
+    M = 77
+    x = (torch.randn(M, d) * 3 + 1).float().cuda()
+    w = torch.randn(d).float().cuda()
+    b = torch.randn(d).float().cuda()
+    y = torch.empty(M, d, dtype=DT[dt][0], device="cuda")
+    _lib.check(lib.wcb_op_layernorm(DT[dt][1], x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), M, d, _s()))
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.layer_norm(x.double(), (d,), w.double(), b.double(), eps=1e-5)
+    tol = 1e-5 if dt == "f32" else 1e-2
+    assert ((y.double() - ref).abs() / (ref.abs() + 1)).max().item() < tol
+
+
+def _attn(dt, q, k, v, flash):
+    lib = _lib.load()
+    B, Sq, D = q.shape
+    Sk = k.shape[1]
+    H = D // 64
+    o = torch.empty_like(q)
+    _lib.check(lib.wcb_op_attention(DT[dt][1], q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), B, H, Sq,
+                                    Sk, int(flash), _s()), None, "attention")
+    torch.cuda.synchronize()
+    return o
+
+
+def _attn_ref(q, k, v):
+    B, Sq, D = q.shape
+    H = D // 64
+    qh = q.double().view(B, Sq, H, 64).transpose(1, 2)
+    kh = k.double().view(B, -1, H, 64).transpose(1, 2)
+    vh = v.double().view(B, -1, H, 64).transpose(1, 2)
+    p = torch.softmax(qh @ kh.transpose(-1, -2), -1)
+    return (p @ vh).transpose(1, 2).reshape(B, Sq, D)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("S", [1500, 200, 64])
+def test_flash_attention(dt, S):
+    g = torch.Generator(device="cpu").manual_seed(S)
+    B, H = 2, 3
+    q = (torch.randn(B, S, H * 64, generator=g) * 0.3).to(DT[dt][0]).cuda()
+    k = torch.randn(B, S, H * 64, generator=g).to(DT[dt][0]).cuda()
+    v = torch.randn(B, S, H * 64, generator=g).to(DT[dt][0]).cuda()
+    o = _attn(dt, q, k, v, True)
+    ref = _attn_ref(q, k, v)
+    # P is rounded to the 16-bit type before P·V: |err| ≲ 2^-8 relative for bf16
+    tol = 1e-2 if dt == "bf16" else 2e-3
+    assert (o.double() - ref).abs().max().item() < tol
+
+
+def test_flash_attention_spike():
+    """Force the online-softmax rescale: one key dominates late in the sequence."""
+    B, H, S = 1, 1, 1500
+    g = torch.Generator(device="cpu").manual_seed(5)
+    q = torch.randn(B, S, 64, generator=g).bfloat16().cuda() * 0.2
+    k = torch.randn(B, S, 64, generator=g).bfloat16().cuda()
+    k[0, 1400] = q[0, 0] * 40
+    v = torch.randn(B, S, 64, generator=g).bfloat16().cuda()
+    o = _attn("bf16", q, k, v, True)
+    assert (o.double() - _attn_ref(q, k, v)).abs().max().item() < 1e-2
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+@pytest.mark.parametrize("Sq,Sk", [(1, 1500), (3, 700), (1, 1), (5, 33)])
+def test_decode_attention(dt, Sq, Sk):
+    g = torch.Generator(device="cpu").manual_seed(Sq * 1000 + Sk)
+    B, H = 3, 2
+    q = (torch.randn(B, Sq, H * 64, generator=g) * 0.3).to(DT[dt][0]).cuda()
+    k = torch.randn(B, Sk, H * 64, generator=g).to(DT[dt][0]).cuda()
+    v = torch.randn(B, Sk, H * 64, generator=g).to(DT[dt][0]).cuda()
+    o = _attn(dt, q, k, v, False)
+    tol = 1e-5 if dt == "f32" else 1e-2
+    assert (o.double() - _attn_ref(q, k, v)).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("n_mel", [80, 128])
+def test_log_mel_matches_oracle(n_mel):
+    from oracle.whisper_np import log_mel
+    from whisper_context_biasing_amd.config import get_dims
+    from whisper_context_biasing_amd.model import WhisperCB
+    from whisper_context_biasing_amd.synth import synth_batch, synth_clip
+    dims = get_dims("large-v3" if n_mel == 128 else "micro")
+    m = WhisperCB(dims, dtype="f32")
+    pcm = synth_batch(3)
+    pcm[2] *= 0.001                                  # quiet clip: exercises the max − 8 clamp
+    short = synth_clip(7, n_samples=5 * 16000)       # 5 s clip: zero-padded to 30 s
+    got = m.log_mel(torch.from_numpy(pcm)).cpu().numpy()
+    ref = log_mel(pcm, n_mel)
+    # exact-f32 DFT vs float64 FFT: HF quotes 1e-5 between its own CPU/GPU paths; near-silent
+    # bins carry f32 roundoff — tolerance 2e-4 max, 2e-6 mean
+    assert np.abs(got - ref).max() < 2e-4
+    assert np.abs(got - ref).mean() < 2e-6
+    got_s = m.log_mel(torch.from_numpy(short)[None]).cpu().numpy()
+    ref_s = log_mel(short[None], n_mel)
+    assert np.abs(got_s - ref_s).max() < 2e-4

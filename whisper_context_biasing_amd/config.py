@@ -61,7 +61,7 @@ _ML = dict(eos_token_id=50257, pad_token_id=50257, decoder_start_token_id=50258)
 
 MODELS = {
     # micro: the golden-fixture config of SURVEY.md §8(c) recipe (i)
-    "micro": WhisperDims("micro", 64, 2, 2, 256, 51865, 80, **_ML),
+    "micro": WhisperDims("micro", 64, 2, 1, 256, 51865, 80, **_ML),   # head_dim 64 like every release
     "tiny.en": WhisperDims("tiny.en", 384, 4, 6, 1536, 51864, 80, **_EN),
     "tiny": WhisperDims("tiny", 384, 4, 6, 1536, 51865, 80, **_ML),
     "base.en": WhisperDims("base.en", 512, 6, 8, 2048, 51864, 80, **_EN),

@@ -1,0 +1,118 @@
+// Shared device helpers for libwcb (gfx950 / CDNA4 only).
+//
+// Element types: bf16 (uint16 bits), f16 (_Float16), f32. Every kernel is templated on the
+// activation/weight type T and computes in f32. MFMA fragments use ONE lane layout for all three
+// types (lane l holds A[row l&15][k = 8*(l>>4) + j], j = 0..7, of a 16x16x32 step):
+//   bf16 / f16 : one v_mfma_f32_16x16x32_{bf16,f16}
+//   f32        : eight v_mfma_f32_16x16x4_f32 (exact f32 fma chains) — MFMA j consumes element j of
+//                every lane, i.e. k = 8g + j over the four lane groups g; summing j = 0..7 covers
+//                all 32 k, so A and B only have to share the permutation (they do).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+typedef _Float16 f16_t;
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+#define WCB_DEV __device__ __forceinline__
+
+WCB_DEV float bf16_to_f(bf16_t v) { return __uint_as_float(uint32_t(v) << 16); }
+WCB_DEV bf16_t f_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return bf16_t((u >> 16) | 0x40);  // keep NaN a NaN
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return bf16_t(u >> 16);
+}
+
+template <typename T> struct DT;
+template <> struct DT<bf16_t> {
+  using frag = s16x8;
+  static constexpr int kBytes = 2;
+  WCB_DEV static float tof(bf16_t v) { return bf16_to_f(v); }
+  WCB_DEV static bf16_t fromf(float f) { return f_to_bf16(f); }
+};
+template <> struct DT<f16_t> {
+  using frag = h16x8;
+  static constexpr int kBytes = 2;
+  WCB_DEV static float tof(f16_t v) { return float(v); }
+  WCB_DEV static f16_t fromf(float f) { return f16_t(f); }
+};
+template <> struct DT<float> {
+  using frag = f32x8;
+  static constexpr int kBytes = 4;
+  WCB_DEV static float tof(float v) { return v; }
+  WCB_DEV static float fromf(float f) { return f; }
+};
+
+WCB_DEV f32x4 mma16(const s16x8& a, const s16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+WCB_DEV f32x4 mma16(const h16x8& a, const h16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+WCB_DEV f32x4 mma16(const f32x8& a, const f32x8& b, f32x4 c) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], c, 0, 0, 0);
+  return c;
+}
+
+// Load one fragment (8 consecutive elements) from global or LDS memory.
+template <typename T>
+WCB_DEV typename DT<T>::frag load_frag(const T* p) {
+  return *reinterpret_cast<const typename DT<T>::frag*>(p);
+}
+
+WCB_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+WCB_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+WCB_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Store 8 consecutive f32 values as T.
+template <typename T> WCB_DEV void store8(T* dst, const float* v);
+template <> WCB_DEV void store8<bf16_t>(bf16_t* dst, const float* v) {
+  s16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (short)f_to_bf16(v[j]);
+  *reinterpret_cast<s16x8*>(dst) = o;
+}
+template <> WCB_DEV void store8<f16_t>(f16_t* dst, const float* v) {
+  h16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f16_t(v[j]);
+  *reinterpret_cast<h16x8*>(dst) = o;
+}
+template <> WCB_DEV void store8<float>(float* dst, const float* v) {
+  *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+template <typename T> WCB_DEV void load8f(const T* src, float* v) {
+  auto f = load_frag<T>(src);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if constexpr (sizeof(T) == 2) {
+      if constexpr (DT<T>::kBytes == 2 && __is_same(T, bf16_t)) v[j] = bf16_to_f((bf16_t)f[j]);
+      else v[j] = float(f[j]);
+    } else {
+      v[j] = f[j];
+    }
+  }
+}
+
+// Bijective XCD-aware remap of a 1-D workgroup id (cdna_hip_programming.md §5 "XCD swizzle").
+WCB_DEV int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}

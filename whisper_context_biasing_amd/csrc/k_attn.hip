@@ -1,0 +1,305 @@
+// Attention kernels (head_dim 64 for every Whisper size).
+//
+// attn_flash_kernel — encoder self-attention, non-causal, S = 1500 keys
+//   ([tf] modeling_whisper.py:284-356 with the SDPA backend; q is pre-scaled by head_dim^-0.5 —
+//   folded exactly into q_proj since 0.125 is a power of two). 16-bit T only.
+//   Workgroup = 4 waves × 32 query rows; K/V tiles of 64 keys double-buffered in LDS via
+//   global_load_lds with an XOR-swizzled source address. "Swapped" products keep the softmax
+//   lane-local: Sᵀ = K·Qᵀ puts one query per lane column, Oᵀ = Vᵀ·Pᵀ consumes the Sᵀ accumulator
+//   registers directly as the B operand (permuted k order, matched by the Vᵀ fragment), Vᵀ
+//   fragments come from ds_read_b64_tr_b16 transposed LDS reads. Online softmax in f32.
+//
+// attn_decode_kernel — one query row per workgroup (decoder self-attention over the KV cache,
+//   decoder cross-attention over the precomputed encoder K/V, and the f32 "exact" encoder path).
+//   8 lanes per key (16 B each), scores in LDS, exact two-pass softmax, P·V with per-lane
+//   partial rows reduced by shuffles and LDS. HBM-bound on the K/V read.
+#include "common.h"
+#include "kernels.h"
+
+namespace wcb {
+
+constexpr int kMaxKeys = 2048;
+
+template <typename T, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_decode_kernel(AttnArgs a) {
+  __shared__ float sc[kMaxKeys];
+  __shared__ float red[NW][64 + 1];
+  __shared__ float stat[2];
+  const int i = blockIdx.x, bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int seg = lane & 7, kg = lane >> 3;
+  const int nk = a.nkeys_dev ? (*a.nkeys_dev + a.nkeys_add) : a.nkeys;
+  const T* q = reinterpret_cast<const T*>(a.q) + ((long)b * a.q_Sb + i) * a.ldq + h * 64;
+  const T* kb = reinterpret_cast<const T*>(a.k) + (long)b * a.k_sb + (long)h * a.k_sh + seg * 8;
+  const T* vb = reinterpret_cast<const T*>(a.v) + (long)b * a.k_sb + (long)h * a.k_sh + seg * 8;
+  float qv[8];
+  load8f<T>(q + seg * 8, qv);
+
+  // pass 1: scores (8 keys per wave-instruction, 8 lanes per key)
+  float mx = -INFINITY;
+  constexpr int STEP = NW * 8;
+  for (int j0 = wave * 8; j0 < nk; j0 += STEP * 2) {
+    float kv0[8], kv1[8];
+    const int ja = j0 + kg, jb = j0 + STEP + kg;
+    load8f<T>(kb + (long)min(ja, nk - 1) * a.k_sk, kv0);
+    load8f<T>(kb + (long)min(jb, nk - 1) * a.k_sk, kv1);
+    float d0 = 0.f, d1 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { d0 = fmaf(qv[e], kv0[e], d0); d1 = fmaf(qv[e], kv1[e], d1); }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) { d0 += __shfl_xor(d0, o, 64); d1 += __shfl_xor(d1, o, 64); }
+    if (ja < nk) { if (seg == 0) sc[ja] = d0; mx = fmaxf(mx, d0); }
+    if (jb < nk) { if (seg == 0) sc[jb] = d1; mx = fmaxf(mx, d1); }
+  }
+  mx = wave_max(mx);
+  if (lane == 0) red[wave][0] = mx;
+  __syncthreads();
+  if (tid == 0) {
+    float m = red[0][0];
+    for (int w = 1; w < NW; ++w) m = fmaxf(m, red[w][0]);
+    stat[0] = m;
+  }
+  __syncthreads();
+  const float m = stat[0];
+  // pass 2: exponentials + denominator
+  float ssum = 0.f;
+  for (int j = tid; j < nk; j += NW * 64) {
+    const float p = __expf(sc[j] - m);
+    sc[j] = p;
+    ssum += p;
+  }
+  ssum = wave_sum(ssum);
+  __syncthreads();
+  if (lane == 0) red[wave][1] = ssum;
+  __syncthreads();
+  if (tid == 0) {
+    float s = 0.f;
+    for (int w = 0; w < NW; ++w) s += red[w][1];
+    stat[1] = s;
+  }
+  // pass 3: o = P·V
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int j0 = wave * 8; j0 < nk; j0 += STEP * 2) {
+    float v0[8], v1[8];
+    const int ja = j0 + kg, jb = j0 + STEP + kg;
+    load8f<T>(vb + (long)min(ja, nk - 1) * a.k_sk, v0);
+    load8f<T>(vb + (long)min(jb, nk - 1) * a.k_sk, v1);
+    const float pa = ja < nk ? sc[ja] : 0.f, pb = jb < nk ? sc[jb] : 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = fmaf(pa, v0[e], fmaf(pb, v1[e], o[e]));
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o[e] += __shfl_xor(o[e], 8, 64);
+    o[e] += __shfl_xor(o[e], 16, 64);
+    o[e] += __shfl_xor(o[e], 32, 64);
+  }
+  __syncthreads();
+  if (kg == 0)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[wave][seg * 8 + e] = o[e];
+  __syncthreads();
+  if (tid < 64) {
+    float acc = 0.f;
+    for (int w = 0; w < NW; ++w) acc += red[w][tid];
+    acc /= stat[1];
+    T* out = reinterpret_cast<T*>(a.o) + ((long)b * a.o_Sb + i) * a.ldo + h * 64;
+    out[tid] = DT<T>::fromf(acc);
+  }
+}
+
+void attention_decode(DType t, const AttnArgs& a, hipStream_t s) {
+  const dim3 grid(a.Sq, a.B * a.H);
+  switch (t) {
+    case kBF16: hipLaunchKernelGGL((attn_decode_kernel<bf16_t, 8>), grid, dim3(512), 0, s, a); break;
+    case kF16: hipLaunchKernelGGL((attn_decode_kernel<f16_t, 8>), grid, dim3(512), 0, s, a); break;
+    case kF32: hipLaunchKernelGGL((attn_decode_kernel<float, 8>), grid, dim3(512), 0, s, a); break;
+  }
+}
+
+// --------------------------------------------------------------------------------- flash (MFMA)
+WCB_DEV void glds16a(const void* gptr, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(gptr, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+WCB_DEV int swz(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+template <typename T>
+WCB_DEV typename DT<T>::frag tr_frag(const char* vt, int r0, int col_chunk2, int lane) {
+  // 16-bit transposed read: group h = lane>>4, lane 4q+p of the group supplies row r0+4h+q,
+  // columns 4p..4p+3 of the 16-column block (chunk pair col_chunk2, col_chunk2+1).
+  const int h = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int r1 = r0 + 4 * h + q, r2 = r1 + 16;
+  const int c = col_chunk2 + (p >> 1), byte = (p & 1) * 8;
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const s4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(vt + swz(r1, c) + byte));
+  const s4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(vt + swz(r2, c) + byte));
+  typename DT<T>::frag f;
+  if constexpr (__is_same(T, bf16_t)) {
+    f = s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+  } else {
+    const s16x8 t8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+    f = __builtin_bit_cast(h16x8, t8);
+  }
+  return f;
+}
+
+template <typename T>
+WCB_DEV typename DT<T>::frag pack_p(const f32x4& lo, const f32x4& hi) {
+  typename DT<T>::frag f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if constexpr (__is_same(T, bf16_t)) { f[e] = (short)f_to_bf16(lo[e]); f[e + 4] = (short)f_to_bf16(hi[e]); }
+    else { f[e] = f16_t(lo[e]); f[e + 4] = f16_t(hi[e]); }
+  }
+  return f;
+}
+
+template <typename T, int QW>
+__global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
+  using Frag = typename DT<T>::frag;
+  constexpr int QB = 4 * QW * 16;     // query rows per workgroup
+  __shared__ __attribute__((aligned(16))) char lds[2][2][64 * 128];   // [stage][K|V][64 keys x 128 B]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int S = a.nkeys;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int q0 = blockIdx.x * QB + wave * QW * 16;
+  const T* Q = reinterpret_cast<const T*>(a.q);
+  const T* K = reinterpret_cast<const T*>(a.k) + (long)b * a.k_sb + (long)h * a.k_sh;
+  const T* V = reinterpret_cast<const T*>(a.v) + (long)b * a.k_sb + (long)h * a.k_sh;
+
+  // Q as the B operand of Sᵀ = K·Qᵀ: lane holds Q[q0 + qi*16 + (lane&15)][ks*32 + 8(lane>>4) .. +7]
+  Frag qf[QW][2];
+#pragma unroll
+  for (int qi = 0; qi < QW; ++qi) {
+    const int qr = min(q0 + qi * 16 + (lane & 15), a.Sq - 1);
+    const T* qp = Q + ((long)b * a.q_Sb + qr) * a.ldq + h * 64 + 8 * (lane >> 4);
+    qf[qi][0] = load_frag<T>(qp);
+    qf[qi][1] = load_frag<T>(qp + 32);
+  }
+  // glds sources: each wave moves rows [wave*16, wave*16+16) of the K and V tiles (2 x 1 KiB each)
+  const int lr0 = wave * 16 + (lane >> 3), lc = lane & 7;
+  auto stage = [&](int st, int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = lr0 + i * 8;
+      const int key = min(kt * 64 + r, S - 1);
+      const int c = lc ^ ((r >> 1) & 7);
+      glds16a(K + (long)key * a.k_sk + c * 8, &lds[st][0][(wave * 16 + i * 8) * 128]);
+      glds16a(V + (long)key * a.k_sk + c * 8, &lds[st][1][(wave * 16 + i * 8) * 128]);
+    }
+  };
+
+  f32x4 o[QW][4];
+  float mrow[QW], lrow[QW];
+#pragma unroll
+  for (int qi = 0; qi < QW; ++qi) {
+    mrow[qi] = -INFINITY; lrow[qi] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[qi][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const float L2E = 1.4426950408889634f;
+  const int nt = (S + 63) / 64;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nt; ++kt) {
+    const int st = kt & 1;
+    if (kt + 1 < nt) stage(st ^ 1, kt + 1);
+    const char* kt_l = lds[st][0];
+    const char* vt_l = lds[st][1];
+    // K fragments (A operand of Sᵀ): rows = keys 16mf + (lane&15), k = dd
+    Frag kf[4][2];
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int r = mf * 16 + (lane & 15);
+        kf[mf][ks] = *reinterpret_cast<const Frag*>(kt_l + swz(r, ks * 4 + (lane >> 4)));
+      }
+    // Vᵀ fragments (A operand of Oᵀ): rows = dd 16mf' + (lane&15), k = keys (permuted)
+    Frag vf[4][2];
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) vf[mf][ks] = tr_frag<T>(vt_l, ks * 32, mf * 2, lane);
+    const bool tail = (kt + 1) * 64 > S;
+#pragma unroll
+    for (int qi = 0; qi < QW; ++qi) {
+      f32x4 s[4];
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf) {
+        s[mf] = f32x4{0.f, 0.f, 0.f, 0.f};
+        s[mf] = mma16(kf[mf][0], qf[qi][0], s[mf]);
+        s[mf] = mma16(kf[mf][1], qf[qi][1], s[mf]);
+      }
+      if (tail) {
+#pragma unroll
+        for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (kt * 64 + mf * 16 + 4 * (lane >> 4) + e >= S) s[mf][e] = -INFINITY;
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tmax = fmaxf(tmax, s[mf][e]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(mrow[qi], tmax);
+      const float alpha = exp2f((mrow[qi] - mnew) * L2E);
+      mrow[qi] = mnew;
+      const float mb = mnew * L2E;
+      float ls = 0.f;
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { s[mf][e] = exp2f(fmaf(s[mf][e], L2E, -mb)); ls += s[mf][e]; }
+      lrow[qi] = lrow[qi] * alpha + ls;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[qi][j] *= alpha;
+      const Frag p0 = pack_p<T>(s[0], s[1]), p1 = pack_p<T>(s[2], s[3]);
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf) {
+        o[qi][mf] = mma16(vf[mf][0], p0, o[qi][mf]);
+        o[qi][mf] = mma16(vf[mf][1], p1, o[qi][mf]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // epilogue: lane holds Oᵀ[dd = 16mf + 4(lane>>4) + e][q = lane&15]
+#pragma unroll
+  for (int qi = 0; qi < QW; ++qi) {
+    float l = lrow[qi];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.f / l;
+    const int qr = q0 + qi * 16 + (lane & 15);
+    if (qr >= a.Sq) continue;
+    T* op = reinterpret_cast<T*>(a.o) + ((long)b * a.o_Sb + qr) * a.ldo + h * 64 + 4 * (lane >> 4);
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf) {
+      typedef short s4 __attribute__((ext_vector_type(4)));
+      s4 w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const T tv = DT<T>::fromf(o[qi][mf][e] * inv);
+        w[e] = __builtin_bit_cast(short, tv);
+      }
+      *reinterpret_cast<s4*>(op + mf * 16) = w;
+    }
+  }
+}
+
+bool attention_flash(DType t, const AttnArgs& a, hipStream_t s) {
+  constexpr int QW = 2;
+  const dim3 grid((a.Sq + 4 * QW * 16 - 1) / (4 * QW * 16), a.B * a.H);
+  switch (t) {
+    case kBF16: hipLaunchKernelGGL((attn_flash_kernel<bf16_t, QW>), grid, dim3(256), 0, s, a); return true;
+    case kF16: hipLaunchKernelGGL((attn_flash_kernel<f16_t, QW>), grid, dim3(256), 0, s, a); return true;
+    default: return false;
+  }
+}
+
+}  // namespace wcb

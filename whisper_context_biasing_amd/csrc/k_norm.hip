@@ -1,0 +1,110 @@
+// LayerNorm, token+position embedding and small fills.
+//
+// LayerNorm restates nn.LayerNorm(d, eps=1e-5) as used by every Whisper block
+// ([tf] modeling_whisper.py:379-413, 448-505, final norms :642 / :790). One wave per row: the f32
+// residual-stream row is read once into registers (vectorised by VEC), mean and variance are
+// wave-shuffle reductions, the normalised row is written in the activation type T.
+// embed restates WhisperDecoder's `embed_tokens(ids) + embed_positions(position_ids)`
+// ([tf] modeling_whisper.py:737-762) for one decode step with the position read on device.
+#include "common.h"
+#include "kernels.h"
+
+namespace wcb {
+
+template <typename T, int VEC, int CH>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                        const float* __restrict__ b, T* __restrict__ y, int M, int d) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* xr = x + (long)row * d;
+  float v[CH][VEC];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int base = (c * 64 + lane) * VEC;
+    if (base < d) {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) v[c][e] = xr[base + e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) v[c][e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) s += v[c][e];
+  }
+  const float mean = wave_sum(s) / d;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int base = (c * 64 + lane) * VEC;
+    if (base < d)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) { const float t = v[c][e] - mean; q += t * t; }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / d + 1e-5f);
+  T* yr = y + (long)row * d;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int base = (c * 64 + lane) * VEC;
+    if (base < d)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e)
+        yr[base + e] = DT<T>::fromf((v[c][e] - mean) * rstd * w[base + e] + b[base + e]);
+  }
+}
+
+template <typename T>
+static void layernorm_t(const float* x, const float* w, const float* b, void* y, int M, int d, hipStream_t s) {
+  const dim3 grid((M + 3) / 4), blk(256);
+  T* yy = reinterpret_cast<T*>(y);
+  // every Whisper width is a multiple of 64: d/64 elements per lane, grouped VEC at a time
+  if (d % 256 == 0 && d <= 2048) {
+    if (d <= 1024) hipLaunchKernelGGL((layernorm_kernel<T, 4, 4>), grid, blk, 0, s, x, w, b, yy, M, d);
+    else hipLaunchKernelGGL((layernorm_kernel<T, 4, 8>), grid, blk, 0, s, x, w, b, yy, M, d);
+  } else if (d % 128 == 0 && d <= 1024) {
+    hipLaunchKernelGGL((layernorm_kernel<T, 2, 8>), grid, blk, 0, s, x, w, b, yy, M, d);
+  } else {
+    hipLaunchKernelGGL((layernorm_kernel<T, 1, 32>), grid, blk, 0, s, x, w, b, yy, M, d);
+  }
+}
+
+void layernorm(DType t, const float* x, const float* w, const float* b, void* y, int M, int d, hipStream_t s) {
+  switch (t) {
+    case kBF16: layernorm_t<bf16_t>(x, w, b, y, M, d, s); break;
+    case kF16: layernorm_t<f16_t>(x, w, b, y, M, d, s); break;
+    case kF32: layernorm_t<float>(x, w, b, y, M, d, s); break;
+  }
+}
+
+template <typename T>
+__global__ void embed_kernel(const T* __restrict__ emb, const T* __restrict__ pemb, const int* __restrict__ ids,
+                             const int* __restrict__ pos, float* __restrict__ x, int M, int d) {
+  const int row = blockIdx.x;
+  const int p = *pos;
+  const long id = ids[row];
+  for (int c = threadIdx.x; c < d; c += blockDim.x)
+    x[(long)row * d + c] = DT<T>::tof(emb[id * d + c]) + DT<T>::tof(pemb[(long)p * d + c]);
+}
+
+void embed(DType t, const void* emb, const void* pemb, const int* ids, const int* pos, float* x, int M, int d,
+           hipStream_t s) {
+  switch (t) {
+    case kBF16: hipLaunchKernelGGL(embed_kernel<bf16_t>, dim3(M), dim3(256), 0, s, (const bf16_t*)emb,
+                                   (const bf16_t*)pemb, ids, pos, x, M, d); break;
+    case kF16: hipLaunchKernelGGL(embed_kernel<f16_t>, dim3(M), dim3(256), 0, s, (const f16_t*)emb,
+                                  (const f16_t*)pemb, ids, pos, x, M, d); break;
+    case kF32: hipLaunchKernelGGL(embed_kernel<float>, dim3(M), dim3(256), 0, s, (const float*)emb,
+                                  (const float*)pemb, ids, pos, x, M, d); break;
+  }
+}
+
+__global__ void fill_i32_kernel(int* p, int v, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = v;
+}
+void fill_i32(int* p, int v, long n, hipStream_t s) {
+  const int grid = (int)min((n + 255) / 256, 1024L);
+  hipLaunchKernelGGL(fill_i32_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, p, v, n);
+}
+
+}  // namespace wcb

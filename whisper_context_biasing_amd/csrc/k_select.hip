@@ -1,0 +1,139 @@
+// Greedy token selection fused with the bias-list log-prob boost and the generate() bookkeeping.
+//
+// Semantics (restating the greedy step of [tf] generation/utils.py:2894-2936 plus the build-defined
+// A8 boost, oracle/bias_ref.py):
+//   score[v] = logit[v] + lam * boosted(s, v)        boosted <=> AC-automaton delta(s, v) != root
+//   score[eos] = -inf while step < min_new_tokens     (MinNewTokens semantics, benchmark mode)
+//   tok = argmax(score), lowest index on ties (torch.argmax); finished rows emit pad;
+//   finished |= tok == eos; s <- delta(s, tok).       lam == 0 → plain greedy, bit-identical.
+// boosted(s, v) = root_child[v] >= 0  OR  v in trans(s), where trans(s) lists every token whose
+// transition from s lands deeper than depth 1 (CSR: trans_off/trans_tok/trans_dst, sorted by
+// token). The vocabulary-wide pass reads the logits once (HBM-bound, 4·V bytes per row) applying
+// the root bitmap; the per-row finalize scans only trans(s) (a handful of tokens) — valid because
+// lam >= 0 (checked on the host) so an unboosted value never beats its own boosted value.
+#include "common.h"
+#include "kernels.h"
+
+namespace wcb {
+
+WCB_DEV bool better(float v, int i, float bv, int bi) { return v > bv || (v == bv && i < bi); }
+
+__global__ __launch_bounds__(256) void select_partial_kernel(SelectArgs a) {
+  const int m = blockIdx.y, c = blockIdx.x;
+  const int chunk = (a.V + a.nchunk - 1) / a.nchunk;
+  const int v0 = c * chunk, v1 = min(a.V, v0 + chunk);
+  const float* row = a.logits + (long)m * a.ld;
+  const bool mask_eos = *a.step < a.min_new;
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int v = v0 + threadIdx.x; v < v1; v += 256) {
+    float x = row[v];
+    if (a.lam != 0.f && ((a.root_bits[v >> 5] >> (v & 31)) & 1u)) x += a.lam;
+    if (mask_eos && v == a.eos) x = -INFINITY;
+    if (better(x, v, bv, bi)) { bv = x; bi = v; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+  }
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sv[w] = bv; si[w] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float best = sv[0];
+    int bidx = si[0];
+    for (int k = 1; k < 4; ++k)
+      if (better(sv[k], si[k], best, bidx)) { best = sv[k]; bidx = si[k]; }
+    a.part_val[m * a.nchunk + c] = best;
+    a.part_idx[m * a.nchunk + c] = bidx;
+  }
+}
+
+__global__ __launch_bounds__(256) void select_finalize_kernel(SelectArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int step = *a.step;
+  const bool mask_eos = step < a.min_new;
+  __shared__ int n_unfinished;
+  if (threadIdx.x == 0) n_unfinished = 0;
+  __syncthreads();
+  for (int m = wave; m < a.M; m += 4) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int c = lane; c < a.nchunk; c += 64) {
+      const float v = a.part_val[m * a.nchunk + c];
+      const int i = a.part_idx[m * a.nchunk + c];
+      if (better(v, i, bv, bi)) { bv = v; bi = i; }
+    }
+    const int s = a.state[m];
+    if (a.lam != 0.f) {
+      const float* row = a.logits + (long)m * a.ld;
+      for (int t = a.trans_off[s] + lane; t < a.trans_off[s + 1]; t += 64) {
+        const int v = a.trans_tok[t];
+        if (a.root_child[v] >= 0) continue;     // already boosted in the vocabulary pass
+        float x = row[v] + a.lam;
+        if (mask_eos && v == a.eos) x = -INFINITY;
+        if (better(x, v, bv, bi)) { bv = x; bi = v; }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    }
+    const bool fin = a.finished[m] != 0;
+    const int tok = fin ? a.pad : bi;
+    // AC transition: look tok up in trans(s) (sorted), else the root child, else root
+    int dst = -1;
+    for (int t = a.trans_off[s] + lane; t < a.trans_off[s + 1]; t += 64)
+      if (a.trans_tok[t] == tok) dst = a.trans_dst[t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dst = max(dst, __shfl_xor(dst, o, 64));
+    if (lane == 0) {
+      if (dst < 0) dst = (tok >= 0 && tok < a.V && a.root_child[tok] >= 0) ? a.root_child[tok] : 0;
+      a.state[m] = dst;
+      a.next_ids[m] = tok;
+      a.out_ids[(long)m * a.out_ld + step] = tok;
+      const bool nf = fin || tok == a.eos;
+      a.finished[m] = nf ? 1 : 0;
+      if (!nf) atomicAdd(&n_unfinished, 1);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *a.step = step + 1;
+    *a.pos = *a.pos + 1;
+    if (n_unfinished == 0 && *a.all_done == 0) *a.all_done = step + 1;
+  }
+}
+
+// Teacher forcing / prompt prefill: next_ids[b] = forced[b·ld + (*pos) + 1]; pos += 1.
+__global__ void advance_forced_kernel(int* next_ids, const int* forced, int M, int ld, int* pos) {
+  const int p = *pos;
+  __syncthreads();
+  for (int b = threadIdx.x; b < M; b += blockDim.x) next_ids[b] = forced[(long)b * ld + p + 1];
+  __syncthreads();
+  if (threadIdx.x == 0) *pos = p + 1;
+}
+void advance_forced(int* next_ids, const int* forced, int M, int ld, int* pos, hipStream_t s) {
+  hipLaunchKernelGGL(advance_forced_kernel, dim3(1), dim3(256), 0, s, next_ids, forced, M, ld, pos);
+}
+
+// next_ids[b] = src[b·ld + col]
+__global__ void gather_col_kernel(int* dst, const int* src, int M, int ld, int col) {
+  for (int b = threadIdx.x; b < M; b += blockDim.x) dst[b] = src[(long)b * ld + col];
+}
+void gather_col(int* dst, const int* src, int M, int ld, int col, hipStream_t s) {
+  hipLaunchKernelGGL(gather_col_kernel, dim3(1), dim3(256), 0, s, dst, src, M, ld, col);
+}
+
+void select_greedy(const SelectArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(select_partial_kernel, dim3(a.nchunk, a.M), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(select_finalize_kernel, dim3(1), dim3(256), 0, s, a);
+}
+
+}  // namespace wcb

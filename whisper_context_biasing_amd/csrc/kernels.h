@@ -1,0 +1,80 @@
+// Host-side launch interface of the libwcb device kernels (internal; the public C-ABI is include/wcb.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wcb {
+
+enum DType : int { kBF16 = 0, kF16 = 1, kF32 = 2 };
+
+// C[M,N] = epilogue(A[M,K] · W[N,K]ᵀ).  A row m lives at A + (m / a_Mb)·a_strideB + (m % a_Mb)·lda
+// (elements): one formula covers plain row-major operands, per-clip batched operands and the
+// overlapping im2col rows of the two conv-stem convolutions.
+struct GemmArgs {
+  const void* A = nullptr; long lda = 0; long a_Mb = 1L << 40; long a_strideB = 0;
+  const void* W = nullptr; long ldw = 0;
+  int M = 0, N = 0, K = 0;
+  const float* bias = nullptr;     // [N] f32
+  int act = 0;                     // 0 none, 1 gelu(erf)
+  const float* resid = nullptr;    // f32, same addressing as out (mode 0), may alias out
+  const float* addrow = nullptr;   // f32 [c_Mb][N] row table added after act (encoder positions)
+  void* out = nullptr; int out_f32 = 0;
+  int mode = 0;                    // 0 rows, 1 head-split, 2 decode qkv (q rows + kv-cache append)
+  long ldc = 0; long c_Mb = 1L << 40; long c_strideB = 0;
+  int hs_S = 0, hs_H = 0, hs_B = 0;        // mode 1: [g][B][H][S][64]; mode 2: rows of the cache
+  const int* pos = nullptr; int kv_T = 0;  // mode 2: cache position (device) and cache length
+  void* kv_out = nullptr; int n_split = 0; // mode 2: columns >= n_split go to the cache
+};
+
+void gemm(DType t, const GemmArgs& g, hipStream_t s);
+
+// LayerNorm over rows of f32 x[M][d] → T y[M][d] (w, b f32).
+void layernorm(DType t, const float* x, const float* w, const float* b, void* y, int M, int d,
+               hipStream_t s);
+
+// x[r][:] = emb[ids[r]][:] + pos_emb[*pos + r_pos][:] (f32 out), r_pos = r % rows_per_seq.
+void embed(DType t, const void* emb, const void* pos_emb, const int* ids, const int* pos, float* x,
+           int M, int d, hipStream_t s);
+
+// Attention over heads of 64. q row for (b, i): q + (b·q_Sb + i)·ldq + h·64.
+// key j of (b, h): k + b·k_sb + h·k_sh + j·k_sk (same strides for v).
+// nkeys: if nkeys_dev != null → *nkeys_dev + nkeys_add (self-attention), else nkeys.
+struct AttnArgs {
+  const void* q = nullptr; long ldq = 0; long q_Sb = 0; int Sq = 1;
+  const void* k = nullptr; const void* v = nullptr; long k_sb = 0, k_sh = 0, k_sk = 0;
+  void* o = nullptr; long ldo = 0; long o_Sb = 0;
+  int B = 0, H = 0;
+  int nkeys = 0; const int* nkeys_dev = nullptr; int nkeys_add = 0;
+};
+void attention_decode(DType t, const AttnArgs& a, hipStream_t s);   // VALU, any T, any Sq
+bool attention_flash(DType t, const AttnArgs& a, hipStream_t s);    // MFMA encoder (16-bit T)
+
+// log-mel front end
+void logmel_power_mel(const float* pcm, long pcm_stride, int n_samples, int B, const float* dft,
+                      const int* mel_lo, const int* mel_hi, const float* mel_w, int n_mel,
+                      float* mel_out, unsigned* clip_max, hipStream_t s);
+void logmel_normalize(float* mel, const unsigned* clip_max, int B, int n_mel, hipStream_t s);
+void mel_to_conv_input(DType t, const float* mel, int B, int n_mel, void* xt, long clip_stride,
+                       hipStream_t s);
+
+// greedy selection with bias-list boost (see csrc/k_select.hip for the semantics)
+struct SelectArgs {
+  const float* logits = nullptr; long ld = 0; int M = 0; int V = 0;
+  float lam = 0.f; const uint32_t* root_bits = nullptr;
+  const int* trans_off = nullptr; const int* trans_tok = nullptr; const int* trans_dst = nullptr;
+  const int* root_child = nullptr;
+  int* state = nullptr; int* finished = nullptr;
+  int eos = 0, pad = 0; int min_new = 0;
+  int* step = nullptr;               // device counter of generated tokens (read + incremented)
+  int* pos = nullptr;                // device decoder position (incremented)
+  int* next_ids = nullptr; int* out_ids = nullptr; int out_ld = 0;
+  float* part_val = nullptr; int* part_idx = nullptr; int nchunk = 0;
+  int* all_done = nullptr;
+};
+void select_greedy(const SelectArgs& a, hipStream_t s);
+void advance_forced(int* next_ids, const int* forced, int M, int ld, int* pos, hipStream_t s);
+void gather_col(int* dst, const int* src, int M, int ld, int col, hipStream_t s);
+
+void fill_i32(int* p, int v, long n, hipStream_t s);
+
+}  // namespace wcb

@@ -1,0 +1,964 @@
+// libwcb host runtime: C-ABI entry points (include/wcb.h), weight repacking, workspaces, the
+// encoder pipeline, the hipGraph-replayed greedy decode loop, the bias-list automaton builder and
+// per-kernel time accounting.
+//
+// Maps onto the reference as follows:
+//   wcb_log_mel   ↔ WhisperFeatureExtractor.__call__   (data_utils/data_loader.py:171-172)
+//   wcb_encode    ↔ WhisperEncoder.forward             ([tf] modeling_whisper.py:592-646)
+//   wcb_generate  ↔ model.generate(input_features, max_length) (scripts/evaluation.py:173-206,
+//                   [tf] trainer_seq2seq.py:329, [tf] generation/utils.py:2783-2944 greedy loop)
+//   wcb_forward   ↔ WhisperForConditionalGenerationWeightCE.forward (models/whisper_medical.py:45-111)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+#include <deque>
+
+#include "../../include/wcb.h"
+#include "kernels.h"
+
+using namespace wcb;
+
+namespace {
+
+struct WcbError : std::runtime_error {
+  int code;
+  WcbError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHK(x)                                                                              \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess)                                                                      \
+      throw WcbError(WCB_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_));             \
+  } while (0)
+#define REQUIRE(c, msg)                                       \
+  do {                                                        \
+    if (!(c)) throw WcbError(WCB_ERR_ARG, std::string(msg)); \
+  } while (0)
+
+constexpr int kFrames = 3000, kNCol = 416, kNSamp = 480000;
+
+int esize(int dt) { return dt == WCB_F32 ? 4 : 2; }
+
+// host f32 → device element bits
+void pack_elems(int dt, const float* src, size_t n, std::vector<uint8_t>& out) {
+  out.resize(n * esize(dt));
+  if (dt == WCB_F32) {
+    memcpy(out.data(), src, n * 4);
+  } else if (dt == WCB_BF16) {
+    uint16_t* o = reinterpret_cast<uint16_t*>(out.data());
+    for (size_t i = 0; i < n; ++i) {
+      uint32_t u;
+      memcpy(&u, src + i, 4);
+      if ((u & 0x7fffffffu) > 0x7f800000u) { o[i] = uint16_t((u >> 16) | 0x40); continue; }
+      u += 0x7FFFu + ((u >> 16) & 1u);
+      o[i] = uint16_t(u >> 16);
+    }
+  } else {
+    _Float16* o = reinterpret_cast<_Float16*>(out.data());
+    for (size_t i = 0; i < n; ++i) o[i] = (_Float16)src[i];
+  }
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t b) {
+    if (b <= bytes) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    HIPCHK(hipMalloc(&p, b));
+    HIPCHK(hipMemset(p, 0, b));
+    bytes = b;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <typename X> X* as() const { return reinterpret_cast<X*>(p); }
+};
+
+struct LayerW {
+  void* qkv_w = nullptr; float* qkv_b = nullptr;   // [3d][d] (q rows pre-scaled by 1/8), bias (k = 0)
+  void* o_w = nullptr; float* o_b = nullptr;
+  float *ln1_w = nullptr, *ln1_b = nullptr;
+  void* xq_w = nullptr; float* xq_b = nullptr;     // decoder cross-attention q (pre-scaled)
+  void* xo_w = nullptr; float* xo_b = nullptr;
+  float *lnx_w = nullptr, *lnx_b = nullptr;
+  void* fc1_w = nullptr; float* fc1_b = nullptr;
+  void* fc2_w = nullptr; float* fc2_b = nullptr;
+  float *ln2_w = nullptr, *ln2_b = nullptr;
+};
+
+struct ProfEntry {
+  std::string name;
+  int64_t launches = 0;
+  double ms = 0, flops = 0, bytes = 0;
+};
+
+}  // namespace
+
+struct wcb_bias {
+  int n_states = 1;
+  int vocab = 0;
+  DevBuf root_bits, root_child, trans_off, trans_tok, trans_dst;
+};
+
+struct wcb_handle {
+  wcb_model_desc d{};
+  DType dt = kBF16;
+  int device = 0;
+  std::string err;
+  hipStream_t hs = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  std::map<std::string, std::vector<float>> host_w;
+  std::vector<DevBuf> owned;
+  bool ready = false;
+  // weights
+  void *conv1_w = nullptr, *conv2_w = nullptr;
+  float *conv1_b = nullptr, *conv2_b = nullptr, *enc_pos = nullptr;
+  int k1pad = 0;
+  std::vector<LayerW> enc, dec;
+  float *enc_ln_w = nullptr, *enc_ln_b = nullptr, *dec_ln_w = nullptr, *dec_ln_b = nullptr;
+  void* xkv_w = nullptr; float* xkv_b = nullptr;
+  void *tok_emb = nullptr, *dec_pos = nullptr;
+  // mel tables
+  DevBuf dft, mel_lo, mel_hi, mel_w, clip_max;
+  // encoder workspace
+  int enc_B = 0;
+  DevBuf xt, hbuf, x, h, qkv, att, ffn, encout;
+  // decoder workspace
+  int dec_B = 0, dec_T = 0;
+  DevBuf xkv, kvself, dx, dh, dq, datt, dffn, logits, part_val, part_idx, ints, outbuf, forced;
+  int nchunk = 64;
+  // graph cache
+  hipGraphExec_t gexec = nullptr;
+  std::string gkey;
+  // default (empty) bias automaton
+  std::unique_ptr<wcb_bias> empty_bias;
+  // profiling
+  bool prof = false;
+  std::vector<ProfEntry> prof_e;
+  std::deque<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
+  std::vector<hipEvent_t> ev_pool;
+
+  int H() const { return d.n_heads; }
+  int S() const { return d.n_audio_ctx; }
+
+  void* upload(const void* src, size_t bytes) {
+    owned.emplace_back();
+    owned.back().ensure(bytes);
+    HIPCHK(hipMemcpy(owned.back().p, src, bytes, hipMemcpyHostToDevice));
+    return owned.back().p;
+  }
+  void* upload_t(const std::vector<float>& v) {
+    std::vector<uint8_t> b;
+    pack_elems(d.dtype, v.data(), v.size(), b);
+    return upload(b.data(), b.size());
+  }
+  float* upload_f(const std::vector<float>& v) { return reinterpret_cast<float*>(upload(v.data(), v.size() * 4)); }
+
+  std::vector<float>& W(const std::string& name, size_t expect) {
+    auto it = host_w.find(name);
+    if (it == host_w.end()) throw WcbError(WCB_ERR_STATE, "missing weight " + name);
+    if (it->second.size() != expect)
+      throw WcbError(WCB_ERR_ARG, "weight " + name + " has " + std::to_string(it->second.size()) +
+                                      " elements, expected " + std::to_string(expect));
+    return it->second;
+  }
+  std::vector<float> Wopt(const std::string& name, size_t n) {
+    auto it = host_w.find(name);
+    if (it == host_w.end()) return std::vector<float>(n, 0.f);
+    if (it->second.size() != n) throw WcbError(WCB_ERR_ARG, "bad size for " + name);
+    return it->second;
+  }
+
+  // ---------------------------------------------------------------- profiling helpers
+  int prof_id(const char* name) {
+    for (size_t i = 0; i < prof_e.size(); ++i)
+      if (prof_e[i].name == name) return (int)i;
+    prof_e.push_back(ProfEntry{name});
+    return (int)prof_e.size() - 1;
+  }
+  hipEvent_t get_ev() {
+    if (!ev_pool.empty()) { auto e = ev_pool.back(); ev_pool.pop_back(); return e; }
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    return e;
+  }
+  template <typename F>
+  void timed(const char* name, double flops, double bytes, F&& f) {
+    if (!prof) { f(); return; }
+    const int id = prof_id(name);
+    hipEvent_t a = get_ev(), b = get_ev();
+    HIPCHK(hipEventRecord(a, hs));
+    f();
+    HIPCHK(hipEventRecord(b, hs));
+    prof_e[id].launches += 1;
+    prof_e[id].flops += flops;
+    prof_e[id].bytes += bytes;
+    prof_pending.push_back({id, {a, b}});
+  }
+  void prof_collect() {
+    while (!prof_pending.empty()) {
+      auto& p = prof_pending.front();
+      HIPCHK(hipEventSynchronize(p.second.second));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, p.second.first, p.second.second));
+      prof_e[p.first].ms += ms;
+      ev_pool.push_back(p.second.first);
+      ev_pool.push_back(p.second.second);
+      prof_pending.pop_front();
+    }
+  }
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+template <typename F>
+int guarded(wcb_handle* h, F&& f) {
+  try {
+    f();
+    return WCB_OK;
+  } catch (const WcbError& e) {
+    (h ? h->err : g_err) = e.what();
+    return e.code;
+  } catch (const std::exception& e) {
+    (h ? h->err : g_err) = e.what();
+    return WCB_ERR_ARG;
+  }
+}
+
+// ---------------------------------------------------------------------------- mel tables
+double hz_to_mel(double f) { return f >= 1000.0 ? 15.0 + std::log(f / 1000.0) * (27.0 / std::log(6.4)) : 3.0 * f / 200.0; }
+double mel_to_hz(double m) { return m >= 15.0 ? 1000.0 * std::exp((std::log(6.4) / 27.0) * (m - 15.0)) : 200.0 * m / 3.0; }
+
+// Slaney filters [201][n_mel] as [tf] audio_utils.py:638-729 (norm="slaney", mel_scale="slaney")
+std::vector<double> mel_filters(int n_mel) {
+  const int nf = 201;
+  std::vector<double> mf(n_mel + 2), ff(n_mel + 2), fft(nf), out((size_t)nf * n_mel, 0.0);
+  const double mmin = hz_to_mel(0.0), mmax = hz_to_mel(8000.0);
+  for (int i = 0; i < n_mel + 2; ++i) {
+    // np.linspace: start + i*step, last point exactly stop
+    mf[i] = (i == n_mel + 1) ? mmax : mmin + i * ((mmax - mmin) / (n_mel + 1));
+    ff[i] = mel_to_hz(mf[i]);
+  }
+  for (int k = 0; k < nf; ++k) fft[k] = (k == nf - 1) ? 8000.0 : k * (8000.0 / (nf - 1));
+  for (int k = 0; k < nf; ++k)
+    for (int m = 0; m < n_mel; ++m) {
+      const double down = -(ff[m] - fft[k]) / (ff[m + 1] - ff[m]);
+      const double up = (ff[m + 2] - fft[k]) / (ff[m + 2] - ff[m + 1]);
+      const double v = std::max(0.0, std::min(down, up));
+      out[(size_t)k * n_mel + m] = v * (2.0 / (ff[m + 2] - ff[m]));
+    }
+  return out;
+}
+
+}  // namespace
+
+// ======================================================================================= C ABI
+extern "C" {
+
+const char* wcb_last_error(const wcb_handle* h) { return h ? h->err.c_str() : g_err.c_str(); }
+
+int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
+  return guarded(nullptr, [&] {
+    REQUIRE(desc && out, "null argument");
+    REQUIRE(desc->d_model % 64 == 0 && desc->d_model / desc->n_heads == 64, "head_dim must be 64");
+    REQUIRE(desc->dtype >= 0 && desc->dtype <= 2, "dtype");
+    REQUIRE(desc->n_mel == 80 || desc->n_mel == 128, "n_mel must be 80 or 128");
+    REQUIRE(desc->n_audio_ctx * 2 == kFrames, "n_audio_ctx must be 1500");
+    HIPCHK(hipSetDevice(device));
+    auto h = std::make_unique<wcb_handle>();
+    h->d = *desc;
+    h->dt = DType(desc->dtype);
+    h->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&h->hs, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
+    // DFT table [416 cols][416 k]: col 2b = win·cos(2πbk/400), col 2b+1 = −win·sin(2πbk/400)
+    std::vector<float> dft((size_t)kNCol * kNCol, 0.f);
+    for (int c = 0; c < 402; ++c) {
+      const int bin = c >> 1;
+      for (int k = 0; k < 400; ++k) {
+        const double win = 0.5 - 0.5 * std::cos(2.0 * M_PI * k / 400.0);
+        const double ang = 2.0 * M_PI * (double)((long)bin * k % 400) / 400.0;
+        dft[(size_t)c * kNCol + k] = (float)(win * ((c & 1) ? -std::sin(ang) : std::cos(ang)));
+      }
+    }
+    h->dft.ensure(dft.size() * 4);
+    HIPCHK(hipMemcpy(h->dft.p, dft.data(), dft.size() * 4, hipMemcpyHostToDevice));
+    const auto fb = mel_filters(desc->n_mel);
+    std::vector<int> lo(desc->n_mel), hi(desc->n_mel);
+    std::vector<float> w((size_t)desc->n_mel * 32, 0.f);
+    for (int m = 0; m < desc->n_mel; ++m) {
+      int a = -1, b = -1;
+      for (int k = 0; k < 201; ++k)
+        if ((float)fb[(size_t)k * desc->n_mel + m] != 0.f) { if (a < 0) a = k; b = k; }
+      if (a < 0) { a = 0; b = -1; }
+      REQUIRE(b - a + 1 <= 32, "mel filter wider than 32 bins");
+      lo[m] = a;
+      hi[m] = b + 1;
+      for (int k = a; k <= b; ++k) w[(size_t)m * 32 + (k - a)] = (float)fb[(size_t)k * desc->n_mel + m];
+    }
+    h->mel_lo.ensure(lo.size() * 4);
+    h->mel_hi.ensure(hi.size() * 4);
+    h->mel_w.ensure(w.size() * 4);
+    HIPCHK(hipMemcpy(h->mel_lo.p, lo.data(), lo.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->mel_hi.p, hi.data(), hi.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->mel_w.p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+    // empty automaton (root only) so greedy without a bias list uses the same kernels
+    auto eb = std::make_unique<wcb_bias>();
+    eb->vocab = desc->vocab;
+    const int nw = (desc->vocab + 31) / 32;
+    eb->root_bits.ensure((size_t)nw * 4);
+    eb->root_child.ensure((size_t)desc->vocab * 4);
+    HIPCHK(hipMemset(eb->root_child.p, 0xff, (size_t)desc->vocab * 4));
+    std::vector<int> off = {0, 0};
+    eb->trans_off.ensure(8);
+    HIPCHK(hipMemcpy(eb->trans_off.p, off.data(), 8, hipMemcpyHostToDevice));
+    eb->trans_tok.ensure(4);
+    eb->trans_dst.ensure(4);
+    h->empty_bias = std::move(eb);
+    *out = h.release();
+  });
+}
+
+void wcb_destroy(wcb_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+  for (auto& b : h->owned) b.release();
+  for (DevBuf* b : {&h->dft, &h->mel_lo, &h->mel_hi, &h->mel_w, &h->clip_max, &h->xt, &h->hbuf, &h->x, &h->h,
+                    &h->qkv, &h->att, &h->ffn, &h->encout, &h->xkv, &h->kvself, &h->dx, &h->dh, &h->dq,
+                    &h->datt, &h->dffn, &h->logits, &h->part_val, &h->part_idx, &h->ints, &h->outbuf, &h->forced})
+    b->release();
+  for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+  if (h->ev_in) (void)hipEventDestroy(h->ev_in);
+  if (h->ev_out) (void)hipEventDestroy(h->ev_out);
+  if (h->hs) (void)hipStreamDestroy(h->hs);
+  delete h;
+}
+
+int wcb_set_weight(wcb_handle* h, const char* name, const float* data, const int64_t* shape, int ndim) {
+  return guarded(h, [&] {
+    REQUIRE(h && name && data && shape && ndim >= 1, "null argument");
+    size_t n = 1;
+    for (int i = 0; i < ndim; ++i) n *= (size_t)shape[i];
+    h->host_w[name] = std::vector<float>(data, data + n);
+  });
+}
+
+int wcb_finalize_weights(wcb_handle* h) {
+  return guarded(h, [&] {
+    REQUIRE(h, "null handle");
+    HIPCHK(hipSetDevice(h->device));
+    const int d = h->d.d_model, L = h->d.n_layers, F = h->d.ffn, V = h->d.vocab, nm = h->d.n_mel;
+    const size_t dd = (size_t)d * d;
+    // conv1: W1[o][c][k] → [o][k·n_mel + c], K padded to a multiple of 64 with zeros
+    {
+      const auto& w1 = h->W("model.encoder.conv1.weight", (size_t)d * nm * 3);
+      h->k1pad = (3 * nm + 63) / 64 * 64;
+      std::vector<float> p((size_t)d * h->k1pad, 0.f);
+      for (int o = 0; o < d; ++o)
+        for (int c = 0; c < nm; ++c)
+          for (int k = 0; k < 3; ++k) p[(size_t)o * h->k1pad + k * nm + c] = w1[((size_t)o * nm + c) * 3 + k];
+      h->conv1_w = h->upload_t(p);
+      h->conv1_b = h->upload_f(h->W("model.encoder.conv1.bias", d));
+      const auto& w2 = h->W("model.encoder.conv2.weight", dd * 3);
+      std::vector<float> q((size_t)d * 3 * d);
+      for (int o = 0; o < d; ++o)
+        for (int c = 0; c < d; ++c)
+          for (int k = 0; k < 3; ++k) q[(size_t)o * 3 * d + k * d + c] = w2[((size_t)o * d + c) * 3 + k];
+      h->conv2_w = h->upload_t(q);
+      h->conv2_b = h->upload_f(h->W("model.encoder.conv2.bias", d));
+      h->enc_pos = h->upload_f(h->W("model.encoder.embed_positions.weight", (size_t)h->S() * d));
+    }
+    auto attn_qkv = [&](const std::string& p, LayerW& lw) {
+      std::vector<float> w(3 * dd), b(3 * d, 0.f);
+      const auto& wq = h->W(p + "q_proj.weight", dd);
+      const auto& wk = h->W(p + "k_proj.weight", dd);
+      const auto& wv = h->W(p + "v_proj.weight", dd);
+      const auto bq = h->W(p + "q_proj.bias", d);
+      const auto bv = h->W(p + "v_proj.bias", d);
+      // q scaling head_dim^-0.5 = 0.125 (exact power of two: folding it is bit-identical)
+      for (size_t i = 0; i < dd; ++i) { w[i] = wq[i] * 0.125f; w[dd + i] = wk[i]; w[2 * dd + i] = wv[i]; }
+      for (int i = 0; i < d; ++i) { b[i] = bq[i] * 0.125f; b[2 * d + i] = bv[i]; }
+      lw.qkv_w = h->upload_t(w);
+      lw.qkv_b = h->upload_f(b);
+      lw.o_w = h->upload_t(h->W(p + "out_proj.weight", dd));
+      lw.o_b = h->upload_f(h->W(p + "out_proj.bias", d));
+    };
+    auto mlp = [&](const std::string& p, LayerW& lw) {
+      lw.ln1_w = h->upload_f(h->W(p + "self_attn_layer_norm.weight", d));
+      lw.ln1_b = h->upload_f(h->W(p + "self_attn_layer_norm.bias", d));
+      lw.ln2_w = h->upload_f(h->W(p + "final_layer_norm.weight", d));
+      lw.ln2_b = h->upload_f(h->W(p + "final_layer_norm.bias", d));
+      lw.fc1_w = h->upload_t(h->W(p + "fc1.weight", (size_t)F * d));
+      lw.fc1_b = h->upload_f(h->W(p + "fc1.bias", F));
+      lw.fc2_w = h->upload_t(h->W(p + "fc2.weight", (size_t)d * F));
+      lw.fc2_b = h->upload_f(h->W(p + "fc2.bias", d));
+    };
+    h->enc.assign(L, LayerW{});
+    h->dec.assign(L, LayerW{});
+    std::vector<float> xkv_w((size_t)2 * L * dd), xkv_b((size_t)2 * L * d, 0.f);
+    for (int i = 0; i < L; ++i) {
+      const std::string pe = "model.encoder.layers." + std::to_string(i) + ".";
+      attn_qkv(pe + "self_attn.", h->enc[i]);
+      mlp(pe, h->enc[i]);
+      const std::string pd = "model.decoder.layers." + std::to_string(i) + ".";
+      attn_qkv(pd + "self_attn.", h->dec[i]);
+      mlp(pd, h->dec[i]);
+      LayerW& lw = h->dec[i];
+      std::vector<float> wq = h->W(pd + "encoder_attn.q_proj.weight", dd);
+      std::vector<float> bq = h->W(pd + "encoder_attn.q_proj.bias", d);
+      for (auto& v : wq) v *= 0.125f;
+      for (auto& v : bq) v *= 0.125f;
+      lw.xq_w = h->upload_t(wq);
+      lw.xq_b = h->upload_f(bq);
+      lw.xo_w = h->upload_t(h->W(pd + "encoder_attn.out_proj.weight", dd));
+      lw.xo_b = h->upload_f(h->W(pd + "encoder_attn.out_proj.bias", d));
+      lw.lnx_w = h->upload_f(h->W(pd + "encoder_attn_layer_norm.weight", d));
+      lw.lnx_b = h->upload_f(h->W(pd + "encoder_attn_layer_norm.bias", d));
+      // cross K/V projection of every layer fused into one [2·L·d][d] weight: rows (l, k|v, d)
+      const auto& wk = h->W(pd + "encoder_attn.k_proj.weight", dd);
+      const auto& wv = h->W(pd + "encoder_attn.v_proj.weight", dd);
+      const auto& bv = h->W(pd + "encoder_attn.v_proj.bias", d);
+      std::copy(wk.begin(), wk.end(), xkv_w.begin() + (size_t)(2 * i) * dd);
+      std::copy(wv.begin(), wv.end(), xkv_w.begin() + (size_t)(2 * i + 1) * dd);
+      std::copy(bv.begin(), bv.end(), xkv_b.begin() + (size_t)(2 * i + 1) * d);
+    }
+    h->xkv_w = h->upload_t(xkv_w);
+    h->xkv_b = h->upload_f(xkv_b);
+    h->enc_ln_w = h->upload_f(h->W("model.encoder.layer_norm.weight", d));
+    h->enc_ln_b = h->upload_f(h->W("model.encoder.layer_norm.bias", d));
+    h->dec_ln_w = h->upload_f(h->W("model.decoder.layer_norm.weight", d));
+    h->dec_ln_b = h->upload_f(h->W("model.decoder.layer_norm.bias", d));
+    h->tok_emb = h->upload_t(h->W("model.decoder.embed_tokens.weight", (size_t)V * d));
+    h->dec_pos = h->upload_t(h->W("model.decoder.embed_positions.weight", (size_t)h->d.n_text_ctx * d));
+    if (h->host_w.count("proj_out.weight")) {
+      const auto& po = h->host_w["proj_out.weight"];
+      const auto& te = h->host_w["model.decoder.embed_tokens.weight"];
+      REQUIRE(po == te, "proj_out.weight must be tied to model.decoder.embed_tokens.weight");
+    }
+    h->host_w.clear();
+    h->ready = true;
+  });
+}
+
+}  // extern "C"
+
+// ============================================================================== pipelines
+namespace {
+
+void sync_in(wcb_handle* h, void* stream) {
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipEventRecord(h->ev_in, (hipStream_t)stream));
+  HIPCHK(hipStreamWaitEvent(h->hs, h->ev_in, 0));
+}
+void sync_out(wcb_handle* h, void* stream) {
+  HIPCHK(hipEventRecord(h->ev_out, h->hs));
+  HIPCHK(hipStreamWaitEvent((hipStream_t)stream, h->ev_out, 0));
+  HIPCHK(hipGetLastError());
+}
+
+void ensure_enc_ws(wcb_handle* h, int B) {
+  if (B <= h->enc_B) return;
+  const size_t e = esize(h->d.dtype), d = h->d.d_model, S = h->S(), M = (size_t)B * S;
+  h->xt.ensure(((size_t)B * (kFrames + 2) * h->d.n_mel + 256) * e);
+  h->hbuf.ensure(((size_t)B * (kFrames + 1) * d + 256) * e);
+  h->x.ensure(M * d * 4);
+  h->h.ensure(M * d * e);
+  h->qkv.ensure(M * 3 * d * e);
+  h->att.ensure(M * d * e);
+  h->ffn.ensure(M * h->d.ffn * e);
+  h->encout.ensure(M * d * e);
+  h->clip_max.ensure((size_t)B * 4);
+  h->enc_B = B;
+}
+
+GemmArgs rowgemm(const void* A, long lda, const void* W, int M, int N, int K, void* out, long ldc) {
+  GemmArgs g;
+  g.A = A; g.lda = lda; g.W = W; g.ldw = K; g.M = M; g.N = N; g.K = K; g.out = out; g.ldc = ldc;
+  return g;
+}
+
+void run_gemm(wcb_handle* h, const char* cls, const GemmArgs& g) {
+  h->timed(cls, 2.0 * g.M * g.N * g.K, 0.0, [&] { gemm(h->dt, g, h->hs); });
+}
+
+// WhisperEncoder.forward ([tf] modeling_whisper.py:592-646) on mel f32 [B][n_mel][3000]
+void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
+  ensure_enc_ws(h, B);
+  const int d = h->d.d_model, S = h->S(), nm = h->d.n_mel, H = h->H();
+  const long M = (long)B * S;
+  const size_t e = esize(h->d.dtype);
+  const long xt_stride = (long)(kFrames + 2) * nm, hb_stride = (long)(kFrames + 1) * d;
+  h->timed("mel_to_conv_input", 0, 0, [&] { mel_to_conv_input(h->dt, mel, B, nm, h->xt.p, xt_stride, h->hs); });
+  {  // conv1 + GELU → hbuf rows 1..3000 of every clip (row 0 = conv2's zero padding)
+    GemmArgs g = rowgemm(h->xt.p, nm, h->conv1_w, B * kFrames, d, h->k1pad, (char*)h->hbuf.p + d * e, d);
+    g.a_Mb = kFrames; g.a_strideB = xt_stride;
+    g.c_Mb = kFrames; g.c_strideB = hb_stride;
+    g.bias = h->conv1_b; g.act = 1;
+    run_gemm(h, "enc_gemm", g);
+  }
+  {  // conv2 (stride 2) + GELU + positions → x (f32 residual stream)
+    GemmArgs g = rowgemm(h->hbuf.p, 2L * d, h->conv2_w, (int)M, d, 3 * d, h->x.p, d);
+    g.a_Mb = S; g.a_strideB = hb_stride;
+    g.c_Mb = S;
+    g.bias = h->conv2_b; g.act = 1; g.addrow = h->enc_pos; g.out_f32 = 1;
+    run_gemm(h, "enc_gemm", g);
+  }
+  for (int l = 0; l < h->d.n_layers; ++l) {
+    const LayerW& w = h->enc[l];
+    h->timed("layernorm", 0, M * d * (4.0 + e), [&] { layernorm(h->dt, h->x.as<float>(), w.ln1_w, w.ln1_b, h->h.p, (int)M, d, h->hs); });
+    GemmArgs q = rowgemm(h->h.p, d, w.qkv_w, (int)M, 3 * d, d, h->qkv.p, 3 * d);
+    q.bias = w.qkv_b;
+    run_gemm(h, "enc_gemm", q);
+    AttnArgs a;
+    a.q = h->qkv.p; a.ldq = 3 * d; a.q_Sb = S; a.Sq = S;
+    a.k = (char*)h->qkv.p + d * e; a.v = (char*)h->qkv.p + 2 * d * e;
+    a.k_sb = (long)S * 3 * d; a.k_sh = 64; a.k_sk = 3 * d;
+    a.o = h->att.p; a.ldo = d; a.o_Sb = S; a.B = B; a.H = H; a.nkeys = S;
+    h->timed("enc_attn", 4.0 * B * H * (double)S * S * 64, 0, [&] {
+      if (!attention_flash(h->dt, a, h->hs)) attention_decode(h->dt, a, h->hs);
+    });
+    GemmArgs o = rowgemm(h->att.p, d, w.o_w, (int)M, d, d, h->x.p, d);
+    o.bias = w.o_b; o.resid = h->x.as<float>(); o.out_f32 = 1;
+    run_gemm(h, "enc_gemm", o);
+    h->timed("layernorm", 0, M * d * (4.0 + e), [&] { layernorm(h->dt, h->x.as<float>(), w.ln2_w, w.ln2_b, h->h.p, (int)M, d, h->hs); });
+    GemmArgs f1 = rowgemm(h->h.p, d, w.fc1_w, (int)M, h->d.ffn, d, h->ffn.p, h->d.ffn);
+    f1.bias = w.fc1_b; f1.act = 1;
+    run_gemm(h, "enc_gemm", f1);
+    GemmArgs f2 = rowgemm(h->ffn.p, h->d.ffn, w.fc2_w, (int)M, d, h->d.ffn, h->x.p, d);
+    f2.bias = w.fc2_b; f2.resid = h->x.as<float>(); f2.out_f32 = 1;
+    run_gemm(h, "enc_gemm", f2);
+  }
+  void* dst = enc_out ? enc_out : h->encout.p;
+  h->timed("layernorm", 0, M * d * (4.0 + e), [&] { layernorm(h->dt, h->x.as<float>(), h->enc_ln_w, h->enc_ln_b, dst, (int)M, d, h->hs); });
+  if (enc_out && enc_out != h->encout.p)
+    HIPCHK(hipMemcpyAsync(h->encout.p, enc_out, M * d * e, hipMemcpyDeviceToDevice, h->hs));
+}
+
+enum { I_STEP = 0, I_POS = 1, I_DONE = 2, I_NEXT = 16 };
+
+void ensure_dec_ws(wcb_handle* h, int B, int T, int out_ld) {
+  const size_t e = esize(h->d.dtype), d = h->d.d_model, L = h->d.n_layers, S = h->S();
+  if (B > h->dec_B || T > h->dec_T) {
+    h->xkv.ensure(2 * L * (size_t)B * S * d * e);
+    h->kvself.ensure(2 * L * (size_t)B * T * d * e);
+    h->dec_B = std::max(h->dec_B, B);
+    h->dec_T = std::max(h->dec_T, T);
+    if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; h->gkey.clear(); }
+  }
+  const size_t before = h->dx.bytes + h->logits.bytes + h->ints.bytes + h->outbuf.bytes + h->dffn.bytes;
+  h->dx.ensure((size_t)B * d * 4);
+  h->dh.ensure((size_t)B * d * e);
+  h->dq.ensure((size_t)B * d * e);
+  h->datt.ensure((size_t)B * d * e);
+  h->dffn.ensure((size_t)B * h->d.ffn * e);
+  h->logits.ensure((size_t)B * h->d.vocab * 4);
+  h->part_val.ensure((size_t)B * h->nchunk * 4);
+  h->part_idx.ensure((size_t)B * h->nchunk * 4);
+  h->ints.ensure((size_t)(I_NEXT + 3 * B + 16) * 4);
+  h->outbuf.ensure((size_t)B * out_ld * 4);
+  const size_t after = h->dx.bytes + h->logits.bytes + h->ints.bytes + h->outbuf.bytes + h->dffn.bytes;
+  if (after != before && h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; h->gkey.clear(); }
+}
+
+// cross-attention K/V of every decoder layer from the encoder output (A4), once per clip:
+// one GEMM [B·1500, d] × [2·L·d, d]ᵀ written head-split as [L·2][B][H][1500][64]
+void cross_kv(wcb_handle* h, int B) {
+  const int d = h->d.d_model, S = h->S(), L = h->d.n_layers;
+  GemmArgs g = rowgemm(h->encout.p, d, h->xkv_w, B * S, 2 * L * d, d, h->xkv.p, 0);
+  g.bias = h->xkv_b; g.mode = 1; g.hs_S = S; g.hs_H = h->H(); g.hs_B = B;
+  run_gemm(h, "xkv_gemm", g);
+}
+
+struct StepCfg {
+  int B, T, out_ld;
+  bool lm_head, select;
+  float* logits_out; long logits_ld;   // LM head destination
+  const wcb_bias* bias; float lam; int min_new;
+  const int* forced; int forced_ld;    // advance_forced source when !select
+};
+
+// One decoder step for every row (WhisperDecoder.forward with a KV cache, [tf] modeling_whisper.py:690-795),
+// LM head and token selection. Every position-dependent quantity is read on the device, so the
+// same launch sequence replays as a hipGraph.
+void decode_step(wcb_handle* h, const StepCfg& c) {
+  const int d = h->d.d_model, S = h->S(), H = h->H(), L = h->d.n_layers, B = c.B, T = c.T;
+  const size_t e = esize(h->d.dtype);
+  int* ints = h->ints.as<int>();
+  int* pos = ints + I_POS;
+  int* next_ids = ints + I_NEXT;
+  float* x = h->dx.as<float>();
+  embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, x, B, d, h->hs);
+  const size_t cache_l = 2 * (size_t)B * H * T * 64;   // elements per layer (K then V)
+  const size_t xkv_l = 2 * (size_t)B * H * S * 64;
+  for (int l = 0; l < L; ++l) {
+    const LayerW& w = h->dec[l];
+    layernorm(h->dt, x, w.ln1_w, w.ln1_b, h->dh.p, B, d, h->hs);
+    char* cache = (char*)h->kvself.p + l * cache_l * e;
+    GemmArgs q = rowgemm(h->dh.p, d, w.qkv_w, B, 3 * d, d, h->dq.p, d);
+    q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
+    gemm(h->dt, q, h->hs);
+    AttnArgs a;
+    a.q = h->dq.p; a.ldq = d; a.q_Sb = 1; a.Sq = 1;
+    a.k = cache; a.v = cache + (size_t)B * H * T * 64 * e;
+    a.k_sb = (long)H * T * 64; a.k_sh = (long)T * 64; a.k_sk = 64;
+    a.o = h->datt.p; a.ldo = d; a.o_Sb = 1; a.B = B; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1;
+    attention_decode(h->dt, a, h->hs);
+    GemmArgs o = rowgemm(h->datt.p, d, w.o_w, B, d, d, x, d);
+    o.bias = w.o_b; o.resid = x; o.out_f32 = 1;
+    gemm(h->dt, o, h->hs);
+    // cross attention over the precomputed encoder K/V
+    layernorm(h->dt, x, w.lnx_w, w.lnx_b, h->dh.p, B, d, h->hs);
+    GemmArgs xq = rowgemm(h->dh.p, d, w.xq_w, B, d, d, h->dq.p, d);
+    xq.bias = w.xq_b;
+    gemm(h->dt, xq, h->hs);
+    AttnArgs xa;
+    const char* xkv = (const char*)h->xkv.p + l * xkv_l * e;
+    xa.q = h->dq.p; xa.ldq = d; xa.q_Sb = 1; xa.Sq = 1;
+    xa.k = xkv; xa.v = xkv + (size_t)B * H * S * 64 * e;
+    xa.k_sb = (long)H * S * 64; xa.k_sh = (long)S * 64; xa.k_sk = 64;
+    xa.o = h->datt.p; xa.ldo = d; xa.o_Sb = 1; xa.B = B; xa.H = H; xa.nkeys = S;
+    attention_decode(h->dt, xa, h->hs);
+    GemmArgs xo = rowgemm(h->datt.p, d, w.xo_w, B, d, d, x, d);
+    xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1;
+    gemm(h->dt, xo, h->hs);
+    // MLP
+    layernorm(h->dt, x, w.ln2_w, w.ln2_b, h->dh.p, B, d, h->hs);
+    GemmArgs f1 = rowgemm(h->dh.p, d, w.fc1_w, B, h->d.ffn, d, h->dffn.p, h->d.ffn);
+    f1.bias = w.fc1_b; f1.act = 1;
+    gemm(h->dt, f1, h->hs);
+    GemmArgs f2 = rowgemm(h->dffn.p, h->d.ffn, w.fc2_w, B, d, h->d.ffn, x, d);
+    f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1;
+    gemm(h->dt, f2, h->hs);
+  }
+  if (c.lm_head) {
+    layernorm(h->dt, x, h->dec_ln_w, h->dec_ln_b, h->dh.p, B, d, h->hs);
+    GemmArgs lm = rowgemm(h->dh.p, d, h->tok_emb, B, h->d.vocab, d, c.logits_out, c.logits_ld);
+    lm.out_f32 = 1;
+    gemm(h->dt, lm, h->hs);
+  }
+  if (c.select) {
+    SelectArgs s;
+    s.logits = c.logits_out; s.ld = c.logits_ld; s.M = B; s.V = h->d.vocab;
+    s.lam = c.lam;
+    s.root_bits = c.bias->root_bits.as<uint32_t>();
+    s.trans_off = c.bias->trans_off.as<int>(); s.trans_tok = c.bias->trans_tok.as<int>();
+    s.trans_dst = c.bias->trans_dst.as<int>(); s.root_child = c.bias->root_child.as<int>();
+    s.state = next_ids + B; s.finished = next_ids + 2 * B;
+    s.eos = h->d.eos_token_id; s.pad = h->d.pad_token_id; s.min_new = c.min_new;
+    s.step = ints + I_STEP; s.pos = pos; s.next_ids = next_ids;
+    s.out_ids = h->outbuf.as<int>(); s.out_ld = c.out_ld;
+    s.part_val = h->part_val.as<float>(); s.part_idx = h->part_idx.as<int>(); s.nchunk = h->nchunk;
+    s.all_done = ints + I_DONE;
+    select_greedy(s, h->hs);
+  } else {
+    advance_forced(next_ids, c.forced, B, c.forced_ld, pos, h->hs);
+  }
+}
+
+
+}  // namespace
+
+extern "C" {
+
+int wcb_log_mel(wcb_handle* h, const float* pcm, int B, int n_samples, int64_t pcm_stride, float* mel_out, void* stream) {
+  return guarded(h, [&] {
+    REQUIRE(h && pcm && mel_out && B > 0 && n_samples > 0, "bad argument");
+    REQUIRE(pcm_stride >= std::min(n_samples, kNSamp), "pcm_stride < n_samples");
+    sync_in(h, stream);
+    h->clip_max.ensure((size_t)std::max(B, h->enc_B) * 4);
+    h->timed("log_mel", 0, (double)B * (std::min(n_samples, kNSamp) * 4.0 + h->d.n_mel * kFrames * 4.0 * 3), [&] {
+      logmel_power_mel(pcm, (long)pcm_stride, n_samples, B, h->dft.as<float>(), h->mel_lo.as<int>(), h->mel_hi.as<int>(),
+                       h->mel_w.as<float>(), h->d.n_mel, mel_out, h->clip_max.as<unsigned>(), h->hs);
+      logmel_normalize(mel_out, h->clip_max.as<unsigned>(), B, h->d.n_mel, h->hs);
+    });
+    sync_out(h, stream);
+  });
+}
+
+int wcb_encode(wcb_handle* h, const float* mel, int B, void* enc_out, void* stream) {
+  return guarded(h, [&] {
+    REQUIRE(h && mel && B > 0, "bad argument");
+    if (!h->ready) throw WcbError(WCB_ERR_STATE, "weights not finalized");
+    sync_in(h, stream);
+    encode_impl(h, mel, B, enc_out);
+    sync_out(h, stream);
+  });
+}
+
+int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg, const wcb_bias* bias,
+                 const int32_t* prefix, int prefix_len, int32_t* out_ids, int32_t* out_steps, void* stream) {
+  return guarded(h, [&] {
+    REQUIRE(h && cfg && out_ids && out_steps && B > 0, "bad argument");
+    if (!h->ready) throw WcbError(WCB_ERR_STATE, "weights not finalized");
+    REQUIRE(cfg->num_beams == 1, "num_beams > 1 is not implemented in this build");
+    REQUIRE(cfg->bias_boost >= 0.f, "bias_boost must be >= 0");
+    REQUIRE(cfg->max_new_tokens >= 1, "max_new_tokens must be >= 1");
+    const int P = prefix ? prefix_len : 1;
+    REQUIRE(P >= 1, "prefix_len must be >= 1");
+    const int T = P + cfg->max_new_tokens;
+    REQUIRE(T <= h->d.n_text_ctx + 1, "prefix + max_new_tokens exceeds max_target_positions");
+    const wcb_bias* bs = bias ? bias : h->empty_bias.get();
+    REQUIRE(bs->vocab == h->d.vocab, "bias automaton built for another vocabulary");
+    sync_in(h, stream);
+    if (mel) encode_impl(h, mel, B, nullptr);
+    else REQUIRE(h->enc_B >= B, "mel == NULL requires a preceding wcb_encode");
+    const int out_ld = cfg->max_new_tokens;
+    const int Tc = std::min(T, h->d.n_text_ctx);
+    ensure_dec_ws(h, B, Tc, out_ld);
+    h->timed("xkv_gemm_total", 0, 0, [&] { cross_kv(h, B); });
+    // state: step = 0, pos = 0, next = first prefix token
+    int* ints = h->ints.as<int>();
+    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 3 * B) * 4, h->hs));
+    if (prefix) {
+      h->forced.ensure((size_t)B * P * 4);
+      for (int b = 0; b < B; ++b)
+        HIPCHK(hipMemcpyAsync(h->forced.as<int>() + (size_t)b * P, prefix, (size_t)P * 4, hipMemcpyHostToDevice, h->hs));
+      gather_col(ints + I_NEXT, h->forced.as<int>(), B, P, 0, h->hs);
+    } else {
+      fill_i32(ints + I_NEXT, h->d.decoder_start_token_id, B, h->hs);
+    }
+    StepCfg sc{B, Tc, out_ld, false, false, h->logits.as<float>(), (long)h->d.vocab, bs, cfg->bias_boost,
+               cfg->min_new_tokens, h->forced.as<int>(), P};
+    for (int p = 0; p + 1 < P; ++p) decode_step(h, sc);   // prompt prefill, teacher-forced
+    sc.lm_head = true;
+    sc.select = true;
+    char key[256];
+    snprintf(key, sizeof key, "%d/%d/%d/%p/%a/%d", B, Tc, out_ld, (const void*)bs, cfg->bias_boost, cfg->min_new_tokens);
+    const int max_new = cfg->max_new_tokens;
+    const int chunk = 8;
+    int done = 0, steps = 0;
+    if (cfg->use_graph) {
+      if (!h->gexec || h->gkey != key) {
+        if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
+        hipGraph_t graph;
+        HIPCHK(hipStreamBeginCapture(h->hs, hipStreamCaptureModeThreadLocal));
+        decode_step(h, sc);
+        HIPCHK(hipStreamEndCapture(h->hs, &graph));
+        HIPCHK(hipGraphInstantiate(&h->gexec, graph, nullptr, nullptr, 0));
+        HIPCHK(hipGraphDestroy(graph));
+        h->gkey = key;
+      }
+    }
+    h->timed("decode_loop", 0, 0, [&] {
+      while (steps < max_new) {
+        const int n = std::min(chunk, max_new - steps);
+        for (int i = 0; i < n; ++i) {
+          if (cfg->use_graph) HIPCHK(hipGraphLaunch(h->gexec, h->hs));
+          else decode_step(h, sc);
+        }
+        steps += n;
+        if (cfg->min_new_tokens >= max_new) continue;   // EOS masked throughout: no early exit
+        HIPCHK(hipMemcpyAsync(&done, ints + I_DONE, 4, hipMemcpyDeviceToHost, h->hs));
+        HIPCHK(hipStreamSynchronize(h->hs));
+        if (done > 0) break;
+      }
+    });
+    if (done <= 0) done = steps;
+    HIPCHK(hipMemcpyAsync(out_ids, h->outbuf.p, (size_t)B * out_ld * 4, hipMemcpyDeviceToDevice, h->hs));
+    *out_steps = std::min(done, max_new);
+    sync_out(h, stream);
+  });
+}
+
+int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, int T, float* logits, void* enc_out,
+                void* stream) {
+  return guarded(h, [&] {
+    REQUIRE(h && dec_ids && logits && B > 0 && T > 0, "bad argument");
+    if (!h->ready) throw WcbError(WCB_ERR_STATE, "weights not finalized");
+    REQUIRE(T <= h->d.n_text_ctx, "decoder_input_ids longer than max_target_positions");
+    sync_in(h, stream);
+    if (mel) encode_impl(h, mel, B, enc_out);
+    else REQUIRE(h->enc_B >= B, "mel == NULL requires a preceding wcb_encode");
+    ensure_dec_ws(h, B, T, 1);
+    cross_kv(h, B);
+    int* ints = h->ints.as<int>();
+    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 3 * B) * 4, h->hs));
+    gather_col(ints + I_NEXT, dec_ids, B, T, 0, h->hs);
+    // forced column T is never read: feed positions 0..T-1 (advance reads column pos+1 < T except last)
+    h->forced.ensure((size_t)B * (T + 1) * 4);
+    HIPCHK(hipMemsetAsync(h->forced.p, 0, (size_t)B * (T + 1) * 4, h->hs));
+    HIPCHK(hipMemcpy2DAsync(h->forced.p, (size_t)(T + 1) * 4, dec_ids, (size_t)T * 4, (size_t)T * 4, B,
+                            hipMemcpyDeviceToDevice, h->hs));
+    for (int t = 0; t < T; ++t) {
+      StepCfg sc{B, T, 1, true, false, logits + (size_t)t * h->d.vocab, (long)T * h->d.vocab, nullptr, 0.f, 0,
+                 h->forced.as<int>(), T + 1};
+      decode_step(h, sc);
+    }
+    sync_out(h, stream);
+  });
+}
+
+// ------------------------------------------------------------------------------ bias automaton
+int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets, int n_phrases, wcb_bias** out) {
+  return guarded(h, [&] {
+    REQUIRE(h && out && n_phrases >= 0 && (n_phrases == 0 || (tokens && offsets)), "bad argument");
+    const int V = h->d.vocab;
+    // trie
+    std::vector<std::map<int, int>> ch(1);
+    std::vector<int> depth(1, 0);
+    for (int p = 0; p < n_phrases; ++p) {
+      int s = 0;
+      REQUIRE(offsets[p + 1] >= offsets[p], "offsets must be non-decreasing");
+      for (int i = offsets[p]; i < offsets[p + 1]; ++i) {
+        const int v = tokens[i];
+        REQUIRE(v >= 0 && v < V, "bias token id out of range");
+        auto it = ch[s].find(v);
+        if (it == ch[s].end()) {
+          ch.emplace_back();
+          depth.push_back(depth[s] + 1);
+          const int nn = (int)ch.size() - 1;
+          ch[s][v] = nn;
+          s = nn;
+        } else {
+          s = it->second;
+        }
+      }
+    }
+    const int ns = (int)ch.size();
+    std::vector<int> fail(ns, 0), order;
+    order.reserve(ns);
+    std::deque<int> q;
+    for (auto& kv : ch[0]) { fail[kv.second] = 0; q.push_back(kv.second); }
+    while (!q.empty()) {
+      const int s = q.front();
+      q.pop_front();
+      order.push_back(s);
+      for (auto& kv : ch[s]) {
+        int f = fail[s];
+        while (f && !ch[f].count(kv.first)) f = fail[f];
+        auto it = ch[f].find(kv.first);
+        fail[kv.second] = (it != ch[f].end() && it->second != kv.second) ? it->second : 0;
+        q.push_back(kv.second);
+      }
+    }
+    // trans(s): every token whose transition from s lands at depth >= 2 (root children are the
+    // vocabulary-wide bitmap). Walk the failure chain; the first (deepest) state owning the token wins.
+    std::vector<int> off(ns + 1, 0), tok, dst;
+    for (int s = 0; s < ns; ++s) {
+      std::map<int, int> t;
+      for (int f = s; f != 0; f = fail[f])
+        for (auto& kv : ch[f])
+          if (!t.count(kv.first)) t[kv.first] = kv.second;
+      for (auto& kv : t)
+        if (depth[kv.second] >= 2) { tok.push_back(kv.first); dst.push_back(kv.second); }
+      off[s + 1] = (int)tok.size();
+    }
+    std::vector<uint32_t> bits((V + 31) / 32, 0u);
+    std::vector<int> rc(V, -1);
+    for (auto& kv : ch[0]) { bits[kv.first >> 5] |= 1u << (kv.first & 31); rc[kv.first] = kv.second; }
+    auto b = std::make_unique<wcb_bias>();
+    b->n_states = ns;
+    b->vocab = V;
+    HIPCHK(hipSetDevice(h->device));
+    b->root_bits.ensure(bits.size() * 4);
+    HIPCHK(hipMemcpy(b->root_bits.p, bits.data(), bits.size() * 4, hipMemcpyHostToDevice));
+    b->root_child.ensure(rc.size() * 4);
+    HIPCHK(hipMemcpy(b->root_child.p, rc.data(), rc.size() * 4, hipMemcpyHostToDevice));
+    b->trans_off.ensure(off.size() * 4);
+    HIPCHK(hipMemcpy(b->trans_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+    b->trans_tok.ensure(std::max<size_t>(tok.size(), 1) * 4);
+    b->trans_dst.ensure(std::max<size_t>(dst.size(), 1) * 4);
+    if (!tok.empty()) {
+      HIPCHK(hipMemcpy(b->trans_tok.p, tok.data(), tok.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(b->trans_dst.p, dst.data(), dst.size() * 4, hipMemcpyHostToDevice));
+    }
+    *out = b.release();
+  });
+}
+
+void wcb_bias_destroy(wcb_bias* b) {
+  if (!b) return;
+  for (DevBuf* x : {&b->root_bits, &b->root_child, &b->trans_off, &b->trans_tok, &b->trans_dst}) x->release();
+  delete b;
+}
+
+int wcb_bias_num_states(const wcb_bias* b) { return b ? b->n_states : 0; }
+
+int wcb_profile_enable(wcb_handle* h, int enable) {
+  return guarded(h, [&] {
+    REQUIRE(h, "null handle");
+    h->prof_collect();
+    h->prof = enable != 0;
+    h->prof_e.clear();
+  });
+}
+
+int wcb_profile_read(wcb_handle* h, int n, char (*names)[32], int64_t* launches, double* ms, double* flops, double* bytes) {
+  int count = 0;
+  const int rc = guarded(h, [&] {
+    REQUIRE(h, "null handle");
+    h->prof_collect();
+    for (size_t i = 0; i < h->prof_e.size() && (int)i < n; ++i) {
+      snprintf(names[i], 32, "%s", h->prof_e[i].name.c_str());
+      launches[i] = h->prof_e[i].launches;
+      ms[i] = h->prof_e[i].ms;
+      flops[i] = h->prof_e[i].flops;
+      bytes[i] = h->prof_e[i].bytes;
+    }
+    count = (int)h->prof_e.size();
+  });
+  return rc == WCB_OK ? count : rc;
+}
+
+// ------------------------------------------------------------------------------ kernel-level ops
+int wcb_op_gemm(int dtype, const void* A, const void* W, int M, int N, int K, const float* bias, int act,
+                const float* resid, void* out, int out_f32, void* stream) {
+  return guarded(nullptr, [&] {
+    REQUIRE(A && W && out && M > 0 && N > 0 && K > 0, "bad argument");
+    REQUIRE(N % 8 == 0, "N must be a multiple of 8");
+    REQUIRE(K % (dtype == WCB_F32 ? 32 : 64) == 0, "K must be a multiple of the 128-byte K tile");
+    GemmArgs g = rowgemm(A, K, W, M, N, K, out, N);
+    g.bias = bias; g.act = act; g.resid = resid; g.out_f32 = out_f32;
+    gemm(DType(dtype), g, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+int wcb_op_layernorm(int dtype, const float* x, const float* w, const float* b, void* y, int M, int d, void* stream) {
+  return guarded(nullptr, [&] {
+    REQUIRE(x && w && b && y && M > 0 && d > 0 && d % 64 == 0 && d <= 2048, "bad argument");
+    layernorm(DType(dtype), x, w, b, y, M, d, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk,
+                     int flash, void* stream) {
+  return guarded(nullptr, [&] {
+    REQUIRE(q && k && v && o && B > 0 && H > 0 && Sq > 0 && Sk > 0 && Sk <= 2048, "bad argument");
+    AttnArgs a;
+    const long ld = (long)H * 64;
+    a.q = q; a.ldq = ld; a.q_Sb = Sq; a.Sq = Sq;
+    a.k = k; a.v = v; a.k_sb = (long)Sk * ld; a.k_sh = 64; a.k_sk = ld;
+    a.o = o; a.ldo = ld; a.o_Sb = Sq; a.B = B; a.H = H; a.nkeys = Sk;
+    if (flash) {
+      REQUIRE(dtype != WCB_F32, "flash attention needs a 16-bit dtype");
+      REQUIRE(Sq == Sk, "flash path is the encoder self-attention (Sq == Sk)");
+      attention_flash(DType(dtype), a, (hipStream_t)stream);
+    } else {
+      attention_decode(DType(dtype), a, (hipStream_t)stream);
+    }
+    HIPCHK(hipGetLastError());
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,305 @@
+"""Drop-in inference surface of the reference model class, backed by libwcb.so.
+
+`WhisperCB` mirrors the parts of `WhisperForConditionalGenerationWeightCE`
+(`models/whisper_medical.py:12-172`) that the reference's evaluation path touches
+(`scripts/evaluation.py:164-206` → `[tf] trainer_seq2seq.py:329`):
+
+* `generate(input_features, labels=None, bias_spans=None, max_length=...)` → LongTensor [B, ≤max_length]
+  without the start token, right-padded with pad_token_id (same return convention as HF);
+  `return_dict_in_generate=True` returns `.sequences` that include the start token.
+* `forward(input_features, decoder_input_ids, labels=None, bias_spans=None)` → output with
+  `.logits` f32 [B, T, V], `.encoder_last_hidden_state`, and the reference's weighted-CE `.loss`
+  (`models/whisper_medical.py:113-156`, computed host-side on the returned logits: a training-loss
+  path, not the inference hot path).
+* `generation_config`, `config.use_cache`, `config.suppress_tokens`, `freeze_encoder()` and `.to()` are
+  accepted exactly as the reference mutates them (`scripts/evaluation.py:173-183`).
+
+All arithmetic runs in hand-written HIP kernels through the C ABI; torch only holds device
+memory and streams. There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from types import SimpleNamespace
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import N_SAMPLES, WhisperDims, dims_from_hf_config, get_dims
+
+_TORCH_DT = {_lib.WCB_BF16: torch.bfloat16, _lib.WCB_F16: torch.float16, _lib.WCB_F32: torch.float32}
+
+
+def _ptr(t: torch.Tensor) -> int:
+    return t.data_ptr()
+
+
+def _stream(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+@dataclass
+class GenerateOutput:
+    sequences: torch.Tensor
+
+
+@dataclass
+class Seq2SeqLMOutput:
+    loss: Optional[torch.Tensor]
+    logits: torch.Tensor
+    encoder_last_hidden_state: torch.Tensor
+
+    def __getitem__(self, i):
+        return (self.logits, self.encoder_last_hidden_state)[i] if self.loss is None else \
+            (self.loss, self.logits, self.encoder_last_hidden_state)[i]
+
+
+class BiasList:
+    """Device Aho-Corasick automaton of a bias list (list of token-id sequences)."""
+
+    def __init__(self, model: "WhisperCB", phrases: Sequence[Sequence[int]]):
+        lib = _lib.load()
+        phrases = [list(map(int, p)) for p in phrases if len(p) > 0]
+        toks = np.asarray([t for p in phrases for t in p] or [0], dtype=np.int32)
+        offs = np.zeros(len(phrases) + 1, dtype=np.int32)
+        offs[1:] = np.cumsum([len(p) for p in phrases]) if phrases else []
+        h = C.c_void_p()
+        _lib.check(lib.wcb_bias_create(model._h, toks.ctypes.data, offs.ctypes.data, len(phrases),
+                                       C.byref(h)), model._h, "wcb_bias_create")
+        self._h = h
+        self.n_phrases = len(phrases)
+        self.n_states = lib.wcb_bias_num_states(h)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _lib.load().wcb_bias_destroy(self._h)
+            self._h = None
+
+
+class WhisperCB:
+    main_input_name = "input_features"
+
+    def __init__(self, dims: WhisperDims, dtype: str = "bf16", device: int = 0, bias_weight: float = 10.0):
+        if not torch.cuda.is_available():
+            raise _lib.WcbError("WhisperCB needs a ROCm GPU (no CPU fallback by design)")
+        lib = _lib.load()
+        self.dims = dims
+        self.dtype_code = _lib.DTYPES[dtype]
+        self.device = torch.device("cuda", device)
+        self.bias_weight = bias_weight
+        desc = _lib.WcbModelDesc(dims.d_model, dims.n_layers, dims.n_heads, dims.ffn, dims.vocab,
+                                 dims.n_mel, dims.n_audio_ctx, dims.n_text_ctx, dims.eos_token_id,
+                                 dims.pad_token_id, dims.decoder_start_token_id, self.dtype_code)
+        h = C.c_void_p()
+        _lib.check(lib.wcb_create(C.byref(desc), device, C.byref(h)), None, "wcb_create")
+        self._h = h
+        self._lib = lib
+        self.config = SimpleNamespace(use_cache=True, suppress_tokens=[], forced_decoder_ids=None,
+                                      decoder_start_token_id=dims.decoder_start_token_id,
+                                      pad_token_id=dims.pad_token_id, eos_token_id=dims.eos_token_id,
+                                      vocab_size=dims.vocab, d_model=dims.d_model,
+                                      max_target_positions=dims.n_text_ctx, num_mel_bins=dims.n_mel)
+        self.generation_config = SimpleNamespace(max_length=448, pad_token_id=dims.pad_token_id,
+                                                 eos_token_id=dims.eos_token_id,
+                                                 decoder_start_token_id=dims.decoder_start_token_id,
+                                                 use_cache=True, num_beams=1, forced_decoder_ids=None)
+        self._bias_cache: Dict[tuple, BiasList] = {}
+        self._loaded = False
+
+    # ------------------------------------------------------------------ construction / weights
+    @classmethod
+    def from_state_dict(cls, dims_or_config, state_dict, dtype: str = "bf16", device: int = 0,
+                        bias_weight: float = 10.0) -> "WhisperCB":
+        dims = dims_or_config if isinstance(dims_or_config, WhisperDims) else (
+            get_dims(dims_or_config) if isinstance(dims_or_config, str) else dims_from_hf_config(dims_or_config))
+        m = cls(dims, dtype=dtype, device=device, bias_weight=bias_weight)
+        m.load_state_dict(state_dict)
+        return m
+
+    @classmethod
+    def from_seed(cls, size: str, seed: int = 0, recipe: str = "diverse", dtype: str = "bf16",
+                  device: int = 0) -> "WhisperCB":
+        from .weights import make_weights
+        dims = get_dims(size)
+        return cls.from_state_dict(dims, make_weights(dims, seed=seed, recipe=recipe), dtype, device)
+
+    def load_state_dict(self, state_dict):
+        for name, t in state_dict.items():
+            if isinstance(t, torch.Tensor):
+                a = t.detach().to("cpu", torch.float32).contiguous().numpy()
+            else:
+                a = np.ascontiguousarray(t, dtype=np.float32)
+            shape = (C.c_int64 * a.ndim)(*a.shape)
+            _lib.check(self._lib.wcb_set_weight(self._h, name.encode(), a.ctypes.data, shape, a.ndim),
+                       self._h, f"wcb_set_weight({name})")
+        _lib.check(self._lib.wcb_finalize_weights(self._h), self._h, "wcb_finalize_weights")
+        self._loaded = True
+        return self
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._bias_cache.clear()
+            self._lib.wcb_destroy(self._h)
+            self._h = None
+
+    # reference-compatible no-ops (scripts/evaluation.py:181-183)
+    def freeze_encoder(self):
+        return self
+
+    def to(self, device=None, *a, **k):
+        return self
+
+    def eval(self):
+        return self
+
+    # --------------------------------------------------------------------------- front end
+    @property
+    def torch_dtype(self):
+        return _TORCH_DT[self.dtype_code]
+
+    def log_mel(self, pcm) -> torch.Tensor:
+        """WhisperFeatureExtractor equivalent: f32 PCM [B, N] (or [N]) → f32 mel [B, n_mel, 3000]."""
+        x = torch.as_tensor(pcm, dtype=torch.float32)
+        if x.dim() == 1:
+            x = x[None]
+        x = x.to(self.device).contiguous()
+        B, N = x.shape
+        out = torch.empty(B, self.dims.n_mel, 3000, dtype=torch.float32, device=self.device)
+        _lib.check(self._lib.wcb_log_mel(self._h, _ptr(x), B, min(N, N_SAMPLES), N, _ptr(out),
+                                         _stream(self.device)), self._h, "wcb_log_mel")
+        return out
+
+    def _features(self, input_features) -> torch.Tensor:
+        x = torch.as_tensor(input_features)
+        if x.dim() == 2:
+            x = x[None]
+        if x.shape[-1] != 3000:
+            # same check as [tf] modeling_whisper.py:612-616
+            raise ValueError(f"Whisper expects the mel input features to be of length 3000, but found {x.shape[-1]}")
+        if x.shape[-2] != self.dims.n_mel:
+            raise ValueError(f"expected {self.dims.n_mel} mel bins, got {x.shape[-2]}")
+        return x.to(self.device, torch.float32).contiguous()
+
+    def encode(self, input_features) -> torch.Tensor:
+        x = self._features(input_features)
+        B = x.shape[0]
+        enc = torch.empty(B, self.dims.n_audio_ctx, self.dims.d_model, dtype=self.torch_dtype, device=self.device)
+        _lib.check(self._lib.wcb_encode(self._h, _ptr(x), B, _ptr(enc), _stream(self.device)), self._h, "wcb_encode")
+        return enc
+
+    # ------------------------------------------------------------------------------ biasing
+    def bias_list(self, phrases: Sequence[Sequence[int]]) -> BiasList:
+        key = tuple(tuple(int(t) for t in p) for p in phrases)
+        b = self._bias_cache.get(key)
+        if b is None:
+            b = BiasList(self, phrases)
+            self._bias_cache[key] = b
+        return b
+
+    def _spans_to_phrases(self, bias_spans) -> List[List[int]]:
+        """Union of the collator's padded per-sample spans ([B, N, L], pad 50256 —
+        data_utils/data_collator.py:107-125) with the padding stripped."""
+        pad = 50256
+        arr = torch.as_tensor(bias_spans).cpu().numpy()
+        out, seen = [], set()
+        for sample in arr:
+            for span in sample:
+                toks = tuple(int(t) for t in span if int(t) != pad)
+                if toks and any(toks) and toks not in seen:
+                    seen.add(toks)
+                    out.append(list(toks))
+        return out
+
+    # ---------------------------------------------------------------------------- generation
+    def generate(self, input_features=None, labels=None, bias_spans=None, max_length: Optional[int] = None,
+                 num_beams: Optional[int] = None, bias_list=None, bias_boost: float = 0.0,
+                 min_new_tokens: int = 0, prompt_ids=None, return_dict_in_generate: bool = False,
+                 generation_config=None, use_graph: bool = True, **kwargs):
+        """Greedy decode with the reference's eval semantics.
+
+        `labels` / `bias_spans` are accepted and ignored for token selection exactly like the
+        reference (`[tf] trainer_seq2seq.py:310-329`), unless `bias_boost > 0` and no explicit
+        `bias_list` is given — then the batch's spans form the boosted bias list.
+        """
+        if not self._loaded:
+            raise _lib.WcbError("weights not loaded")
+        gc = generation_config or self.generation_config
+        max_length = int(max_length if max_length is not None else getattr(gc, "max_length", 448))
+        num_beams = int(num_beams if num_beams is not None else getattr(gc, "num_beams", 1) or 1)
+        if num_beams != 1:
+            raise NotImplementedError("beam search is not implemented in this build (greedy only)")
+        x = self._features(input_features)
+        B = x.shape[0]
+        prefix = [self.dims.decoder_start_token_id]
+        if prompt_ids is not None:
+            prefix = [int(t) for t in prompt_ids] + prefix
+        max_new = min(max_length, self.dims.n_text_ctx + 1 - len(prefix))
+        phrases = bias_list
+        if phrases is None and bias_boost > 0 and bias_spans is not None:
+            phrases = self._spans_to_phrases(bias_spans)
+        bl = self.bias_list(phrases) if (phrases and bias_boost > 0) else None
+        cfg = _lib.WcbGenCfg(max_new, int(min_new_tokens), 1, float(bias_boost), int(use_graph))
+        out = torch.empty(B, max_new, dtype=torch.int32, device=self.device)
+        steps = C.c_int32(0)
+        pre = np.asarray(prefix, dtype=np.int32)
+        _lib.check(self._lib.wcb_generate(self._h, _ptr(x), B, C.byref(cfg), bl._h if bl else None,
+                                          pre.ctypes.data if len(prefix) > 1 else None, len(prefix),
+                                          _ptr(out), C.byref(steps), _stream(self.device)),
+                   self._h, "wcb_generate")
+        ids = out[:, :steps.value].to(torch.int64)
+        if return_dict_in_generate:
+            sot = torch.tensor(prefix, dtype=torch.int64, device=self.device)[None].expand(B, -1)
+            return GenerateOutput(sequences=torch.cat([sot, ids], dim=1))
+        return ids
+
+    # ------------------------------------------------------------------------------- forward
+    def forward(self, input_features=None, decoder_input_ids=None, labels=None, bias_spans=None,
+                encoder_outputs=None, return_dict: bool = True, **kwargs) -> Seq2SeqLMOutput:
+        if labels is not None:
+            labels = torch.as_tensor(labels)
+            if labels.shape[1] > self.dims.n_text_ctx:
+                raise ValueError(f"Labels' sequence length {labels.shape[1]} cannot exceed the maximum allowed "
+                                 f"length of {self.dims.n_text_ctx} tokens.")
+            if decoder_input_ids is None:
+                # shift_tokens_right ([tf] modeling_whisper.py:67-80)
+                dec = torch.full_like(labels, self.dims.pad_token_id)
+                dec[:, 1:] = labels[:, :-1].clone()
+                dec[:, 0] = self.dims.decoder_start_token_id
+                dec[dec == -100] = self.dims.pad_token_id
+                decoder_input_ids = dec
+        ids = torch.as_tensor(decoder_input_ids).to(self.device, torch.int32).contiguous()
+        x = self._features(input_features)
+        B, T = ids.shape
+        logits = torch.empty(B, T, self.dims.vocab, dtype=torch.float32, device=self.device)
+        enc = torch.empty(B, self.dims.n_audio_ctx, self.dims.d_model, dtype=self.torch_dtype, device=self.device)
+        _lib.check(self._lib.wcb_forward(self._h, _ptr(x), B, _ptr(ids), T, _ptr(logits), _ptr(enc),
+                                         _stream(self.device)), self._h, "wcb_forward")
+        loss = None
+        if labels is not None:
+            from .loss import weighted_ce
+            loss = weighted_ce(logits, labels.to(self.device), bias_spans, self.bias_weight)
+        return Seq2SeqLMOutput(loss=loss, logits=logits, encoder_last_hidden_state=enc)
+
+    __call__ = forward
+
+    # ---------------------------------------------------------------------------- profiling
+    def profile_enable(self, on: bool = True):
+        _lib.check(self._lib.wcb_profile_enable(self._h, int(on)), self._h, "wcb_profile_enable")
+
+    def profile_read(self) -> Dict[str, dict]:
+        n = 32
+        names = (C.c_char * 32 * n)()
+        launches = (C.c_int64 * n)()
+        ms = (C.c_double * n)()
+        flops = (C.c_double * n)()
+        byts = (C.c_double * n)()
+        cnt = _lib.check(self._lib.wcb_profile_read(self._h, n, names, launches, ms, flops, byts), self._h,
+                         "wcb_profile_read")
+        out = {}
+        for i in range(min(cnt, n)):
+            nm = bytes(names[i]).split(b"\0", 1)[0].decode()
+            out[nm] = dict(launches=launches[i], ms=ms[i], flops=flops[i], bytes=byts[i])
+        return out
