@@ -98,6 +98,11 @@ int wcb_profile_enable(wcb_handle* h, int enable);
 int wcb_profile_read(wcb_handle* h, int n, char (*names)[32], int64_t* launches, double* ms,
                      double* flops, double* bytes);
 
+/* debug: copy an internal workspace buffer (xt, hbuf, x, h, qkv, att, ffn, encout, xkv, logits)
+ * into dst (device) after synchronising; enc_layers limits later encodes to that many layers
+ * (-1 = all). bytes == 0 only sets the limit. */
+int wcb_debug_copy(wcb_handle* h, const char* name, void* dst, int64_t bytes, int enc_layers);
+
 /* ---- kernel-level entry points (parity tests and microbenchmarks) ---- */
 /* out[M][N] = act(A[M][K] · W[N][K]ᵀ + bias) (+ resid), row-major, dtype of A/W = dtype */
 int wcb_op_gemm(int dtype, const void* A, const void* W, int M, int N, int K, const float* bias, int act,

@@ -44,6 +44,7 @@ SIGNATURES = {
     "wcb_bias_create": (C.c_int, [_P, _P, _P, C.c_int, C.POINTER(_P)]),
     "wcb_bias_destroy": (None, [_P]),
     "wcb_bias_num_states": (C.c_int, [_P]),
+    "wcb_debug_copy": (C.c_int, [_P, C.c_char_p, _P, C.c_int64, C.c_int]),
     "wcb_profile_enable": (C.c_int, [_P, C.c_int]),
     "wcb_profile_read": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, _P]),
     "wcb_op_gemm": (C.c_int, [C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P, _P,

@@ -124,6 +124,7 @@ struct wcb_handle {
   std::map<std::string, std::vector<float>> host_w;
   std::vector<DevBuf> owned;
   bool ready = false;
+  int dbg_enc_layers = -1;   // debug: run only this many encoder layers (-1 = all)
   // weights
   void *conv1_w = nullptr, *conv2_w = nullptr;
   float *conv1_b = nullptr, *conv2_b = nullptr, *enc_pos = nullptr;
@@ -518,11 +519,12 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
   {  // conv2 (stride 2) + GELU + positions → x (f32 residual stream)
     GemmArgs g = rowgemm(h->hbuf.p, 2L * d, h->conv2_w, (int)M, d, 3 * d, h->x.p, d);
     g.a_Mb = S; g.a_strideB = hb_stride;
-    g.c_Mb = S;
+    g.c_Mb = S; g.c_strideB = (long)S * d;   // c_Mb also indexes the position table
     g.bias = h->conv2_b; g.act = 1; g.addrow = h->enc_pos; g.out_f32 = 1;
     run_gemm(h, "enc_gemm", g);
   }
-  for (int l = 0; l < h->d.n_layers; ++l) {
+  const int nl = h->dbg_enc_layers >= 0 ? std::min(h->dbg_enc_layers, h->d.n_layers) : h->d.n_layers;
+  for (int l = 0; l < nl; ++l) {
     const LayerW& w = h->enc[l];
     h->timed("layernorm", 0, M * d * (4.0 + e), [&] { layernorm(h->dt, h->x.as<float>(), w.ln1_w, w.ln1_b, h->h.p, (int)M, d, h->hs); });
     GemmArgs q = rowgemm(h->h.p, d, w.qkv_w, (int)M, 3 * d, d, h->qkv.p, 3 * d);
@@ -892,6 +894,23 @@ void wcb_bias_destroy(wcb_bias* b) {
 }
 
 int wcb_bias_num_states(const wcb_bias* b) { return b ? b->n_states : 0; }
+
+int wcb_debug_copy(wcb_handle* h, const char* name, void* dst, int64_t bytes, int enc_layers) {
+  return guarded(h, [&] {
+    REQUIRE(h && name, "bad argument");
+    h->dbg_enc_layers = enc_layers;
+    const std::map<std::string, DevBuf*> bufs = {{"xt", &h->xt}, {"hbuf", &h->hbuf}, {"x", &h->x}, {"h", &h->h},
+                                                 {"qkv", &h->qkv}, {"att", &h->att}, {"ffn", &h->ffn},
+                                                 {"encout", &h->encout}, {"xkv", &h->xkv}, {"logits", &h->logits}};
+    if (bytes == 0) return;   // only set the layer limit
+    REQUIRE(dst, "null dst");
+    auto it = bufs.find(name);
+    REQUIRE(it != bufs.end(), std::string("unknown buffer ") + name);
+    REQUIRE((size_t)bytes <= it->second->bytes, "bytes exceeds buffer size");
+    HIPCHK(hipStreamSynchronize(h->hs));
+    HIPCHK(hipMemcpy(dst, it->second->p, (size_t)bytes, hipMemcpyDeviceToDevice));
+  });
+}
 
 int wcb_profile_enable(wcb_handle* h, int enable) {
   return guarded(h, [&] {
