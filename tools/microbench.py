@@ -1,0 +1,91 @@
+"""Kernel microbenchmarks through the C ABI, replayed from a captured graph (no host overhead).
+Prints per-launch device time (graph of `reps` back-to-back launches / reps)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from whisper_context_biasing_amd import _lib  # noqa: E402
+
+lib = _lib.load()
+
+
+def per_launch_us(fn, reps=50, iters=5):
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(reps):
+                fn()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (reps * iters)
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def gemm_case(M, N, K, dt=torch.bfloat16):
+    A = torch.randn(M, K, device="cuda").to(dt)
+    W = torch.randn(N, K, device="cuda").to(dt)
+    out = torch.empty(M, N, device="cuda", dtype=dt)
+    code = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2}[dt]
+
+    def fn():
+        lib.wcb_op_gemm(code, A.data_ptr(), W.data_ptr(), M, N, K, None, 0, None, out.data_ptr(), 0, stream())
+    us = per_launch_us(fn, reps=20 if M > 64 else 50)
+    flops = 2.0 * M * N * K
+    byts = (M * K + N * K + M * N) * A.element_size()
+    print(f"gemm M={M:6d} N={N:6d} K={K:5d}: {us:9.2f} us  {flops / us / 1e6:8.1f} TFLOP/s  {byts / us / 1e3:8.1f} GB/s")
+
+
+def ln_case(M, d):
+    x = torch.randn(M, d, device="cuda")
+    w = torch.ones(d, device="cuda")
+    b = torch.zeros(d, device="cuda")
+    y = torch.empty(M, d, device="cuda", dtype=torch.bfloat16)
+
+    def fn():
+        lib.wcb_op_layernorm(0, x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), M, d, stream())
+    us = per_launch_us(fn)
+    print(f"layernorm M={M:6d} d={d}: {us:8.2f} us  {M * d * 6 / us / 1e3:8.1f} GB/s")
+
+
+def attn_case(B, H, Sq, Sk, flash):
+    q = torch.randn(B, Sq, H * 64, device="cuda").bfloat16()
+    k = torch.randn(B, Sk, H * 64, device="cuda").bfloat16()
+    v = torch.randn(B, Sk, H * 64, device="cuda").bfloat16()
+    o = torch.empty_like(q)
+
+    def fn():
+        lib.wcb_op_attention(0, q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), B, H, Sq, Sk, flash, stream())
+    us = per_launch_us(fn, reps=10 if flash else 50)
+    byts = 2 * B * Sk * H * 64 * 2
+    fl = 4.0 * B * H * Sq * Sk * 64
+    print(f"attn B={B} H={H} Sq={Sq} Sk={Sk} flash={flash}: {us:9.2f} us  {byts / us / 1e3:8.1f} GB/s (KV)  "
+          f"{fl / us / 1e6:8.1f} TFLOP/s")
+
+
+if __name__ == "__main__":
+    torch.manual_seed(0)
+    ln_case(1, 768)
+    ln_case(32, 768)
+    ln_case(48000, 768)
+    for (M, N, K) in [(32, 768, 768), (32, 2304, 768), (32, 3072, 768), (32, 768, 3072), (32, 51865 // 8 * 8, 768),
+                      (48000, 2304, 768), (48000, 768, 768), (48000, 3072, 768), (48000, 768, 3072),
+                      (48000, 18432, 768), (8192, 8192, 8192)]:
+        gemm_case(M, N, K)
+    attn_case(32, 12, 1, 1500, 0)
+    attn_case(32, 12, 1, 64, 0)
+    attn_case(32, 12, 1500, 1500, 1)

@@ -15,6 +15,9 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdio>
+#include <type_traits>
+
 namespace wcb {
 
 WCB_DEV void glds16(const void* gptr, void* lds_wave_base) {
@@ -198,39 +201,92 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(GemmArgs g) {
   }
 }
 
-template <typename T, int MF, int NW>
+// Skinny GEMM for the decode step (M = batch <= 64 rows): one workgroup = 16 output columns, its
+// NW waves split K into NW contiguous ranges of KS 32-deep MFMA steps, every load of the wave is
+// issued up front (weights are streamed once from HBM, activations come from L2), partial tiles
+// are summed through LDS. With LN the A operand is the f32 residual stream normalised on the fly
+// (the decoder's pre-attention / pre-MLP LayerNorm fused into the projection that consumes it).
+template <typename T, int MF, int NW, int KS, bool LN>
 __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
   using Frag = typename DT<T>::frag;
   __shared__ __attribute__((aligned(16))) float red[NW][MF * 16][17];
+  __shared__ float lnred[NW][MF * 16][2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 16;
   const long n = min(n0 + (lane & 15), g.N - 1);
-  const T* W = reinterpret_cast<const T*>(g.W) + n * g.ldw + 8 * (lane >> 4);
-  const T* A = reinterpret_cast<const T*>(g.A);
-  const T* ap[MF];
+  const int kb = wave * (KS * 32) + 8 * (lane >> 4);
+  const T* W = reinterpret_cast<const T*>(g.W) + n * g.ldw + kb;
+  Frag b[KS];
 #pragma unroll
-  for (int i = 0; i < MF; ++i) {
-    const long m = min(i * 16 + (lane & 15), g.M - 1);
-    ap[i] = A + a_row(g, m) + 8 * (lane >> 4);
-  }
+  for (int ks = 0; ks < KS; ++ks) b[ks] = load_frag<T>(W + ks * 32);
   f32x4 acc[MF];
 #pragma unroll
   for (int i = 0; i < MF; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int KW = g.K / NW;
-  const int kb = wave * KW, ke = kb + KW;
-  int k = kb;
-  for (; k + 64 <= ke; k += 64) {
-    const Frag b0 = load_frag<T>(W + k), b1 = load_frag<T>(W + k + 32);
-    Frag a0[MF], a1[MF];
+  if constexpr (LN) {
+    float gw[KS][8], gb[KS][8];
 #pragma unroll
-    for (int i = 0; i < MF; ++i) { a0[i] = load_frag<T>(ap[i] + k); a1[i] = load_frag<T>(ap[i] + k + 32); }
+    for (int ks = 0; ks < KS; ++ks) {
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(g.ln_w + kb + ks * 32);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(g.ln_w + kb + ks * 32 + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(g.ln_b + kb + ks * 32);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(g.ln_b + kb + ks * 32 + 4);
 #pragma unroll
-    for (int i = 0; i < MF; ++i) { acc[i] = mma16(a0[i], b0, acc[i]); acc[i] = mma16(a1[i], b1, acc[i]); }
-  }
-  for (; k < ke; k += 32) {
-    const Frag b0 = load_frag<T>(W + k);
+      for (int e = 0; e < 4; ++e) { gw[ks][e] = w0[e]; gw[ks][e + 4] = w1[e]; gb[ks][e] = b0[e]; gb[ks][e + 4] = b1[e]; }
+    }
+    // one pass over this wave's K range: keep the x fragments, reduce Σx and Σx² per row over the
+    // four lane groups and then over the waves (LDS) — no second read of the residual stream
+    const float* X = reinterpret_cast<const float*>(g.A);
+    float xv[MF][KS][8];
 #pragma unroll
-    for (int i = 0; i < MF; ++i) acc[i] = mma16(load_frag<T>(ap[i] + k), b0, acc[i]);
+    for (int i = 0; i < MF; ++i) {
+      const int m = min(i * 16 + (lane & 15), g.M - 1);
+      const float* xr = X + a_row(g, m) + kb;
+      float ps = 0.f, pq = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(xr + ks * 32);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(xr + ks * 32 + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { xv[i][ks][e] = x0[e]; xv[i][ks][e + 4] = x1[e]; }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { ps += xv[i][ks][e]; pq += xv[i][ks][e] * xv[i][ks][e]; }
+      }
+      ps += __shfl_xor(ps, 16, 64); ps += __shfl_xor(ps, 32, 64);
+      pq += __shfl_xor(pq, 16, 64); pq += __shfl_xor(pq, 32, 64);
+      if (lane < 16) { lnred[wave][i * 16 + lane][0] = ps; lnred[wave][i * 16 + lane][1] = pq; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) { s1 += lnred[w][i * 16 + (lane & 15)][0]; s2 += lnred[w][i * 16 + (lane & 15)][1]; }
+      const float mean = s1 / g.K;
+      const float rstd = rsqrtf(fmaxf(s2 / g.K - mean * mean, 0.f) + 1e-5f);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        Frag a;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = (xv[i][ks][e] - mean) * rstd * gw[ks][e] + gb[ks][e];
+          if constexpr (sizeof(T) == 4) a[e] = v;
+          else a[e] = __builtin_bit_cast(typename std::remove_reference<decltype(a[0])>::type, DT<T>::fromf(v));
+        }
+        acc[i] = mma16(a, b[ks], acc[i]);
+      }
+    }
+  } else {
+    const T* A = reinterpret_cast<const T*>(g.A);
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const int m = min(i * 16 + (lane & 15), g.M - 1);
+      const T* ap = A + a_row(g, m) + kb;
+      Frag a[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) a[ks] = load_frag<T>(ap + ks * 32);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc[i] = mma16(a[ks], b[ks], acc[i]);
+    }
   }
 #pragma unroll
   for (int i = 0; i < MF; ++i)
@@ -263,25 +319,33 @@ static void launch_tile(const GemmArgs& g, hipStream_t s) {
   hipLaunchKernelGGL((gemm_tile_kernel<T, BM, BN, WM, WN>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
 }
 
-template <typename T, int MF>
-static void launch_skinny_mf(const GemmArgs& g, hipStream_t s) {
+template <typename T, int MF, int NW, int KS>
+static void launch_skinny_k(const GemmArgs& g, hipStream_t s) {
   const int grid = (g.N + 15) / 16;
-  if (g.K % (32 * 8) == 0 && g.K >= 512)
-    hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, 8>), dim3(grid), dim3(512), 0, s, g);
-  else if (g.K % (32 * 4) == 0)
-    hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, 4>), dim3(grid), dim3(256), 0, s, g);
-  else if (g.K % (32 * 2) == 0)
-    hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, 2>), dim3(grid), dim3(128), 0, s, g);
-  else
-    hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, 1>), dim3(grid), dim3(64), 0, s, g);
+  if (g.ln_w) hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NW, KS, true>), dim3(grid), dim3(NW * 64), 0, s, g);
+  else hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NW, KS, false>), dim3(grid), dim3(NW * 64), 0, s, g);
+}
+
+// K = NW waves x KS steps x 32: pick the wave count first, then the (compile-time) steps per wave.
+template <typename T, int MF>
+static bool launch_skinny_mf(const GemmArgs& g, hipStream_t s) {
+  const int K = g.K;
+#define WCB_SK(nw, ks) if (K == nw * ks * 32) { launch_skinny_k<T, MF, nw, ks>(g, s); return true; }
+  WCB_SK(1, 1) WCB_SK(1, 2) WCB_SK(2, 2) WCB_SK(4, 2) WCB_SK(4, 3) WCB_SK(4, 4) WCB_SK(8, 2)
+  WCB_SK(8, 3) WCB_SK(8, 4) WCB_SK(8, 5) WCB_SK(8, 6) WCB_SK(16, 4) WCB_SK(16, 5) WCB_SK(16, 6)
+  WCB_SK(16, 8) WCB_SK(16, 10) WCB_SK(16, 12)
+#undef WCB_SK
+  return false;
 }
 
 template <typename T>
 static void gemm_t(const GemmArgs& g, hipStream_t s) {
-  if (g.M <= 64 || g.mode == 2) {
-    if (g.M <= 16) launch_skinny_mf<T, 1>(g, s);
-    else if (g.M <= 32) launch_skinny_mf<T, 2>(g, s);
-    else launch_skinny_mf<T, 4>(g, s);
+  if (g.M <= 64 || g.mode == 2 || g.ln_w) {
+    bool ok;
+    if (g.M <= 16) ok = launch_skinny_mf<T, 1>(g, s);
+    else if (g.M <= 32) ok = launch_skinny_mf<T, 2>(g, s);
+    else ok = launch_skinny_mf<T, 4>(g, s);
+    if (!ok) fprintf(stderr, "wcb: no skinny GEMM instance for K=%d\n", g.K);
     return;
   }
   // Tile choice: 128x128 (4 waves 2x2) when N fills it, else 128x64.

@@ -53,61 +53,63 @@ __global__ __launch_bounds__(256) void select_partial_kernel(SelectArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void select_finalize_kernel(SelectArgs a) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// One wave per row; the last row to finish (atomic ticket) advances the step/position counters.
+__global__ __launch_bounds__(64) void select_finalize_kernel(SelectArgs a) {
+  const int m = blockIdx.x, lane = threadIdx.x;
   const int step = *a.step;
   const bool mask_eos = step < a.min_new;
-  __shared__ int n_unfinished;
-  if (threadIdx.x == 0) n_unfinished = 0;
-  __syncthreads();
-  for (int m = wave; m < a.M; m += 4) {
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int c = lane; c < a.nchunk; c += 64) {
-      const float v = a.part_val[m * a.nchunk + c];
-      const int i = a.part_idx[m * a.nchunk + c];
-      if (better(v, i, bv, bi)) { bv = v; bi = i; }
-    }
-    const int s = a.state[m];
-    if (a.lam != 0.f) {
-      const float* row = a.logits + (long)m * a.ld;
-      for (int t = a.trans_off[s] + lane; t < a.trans_off[s + 1]; t += 64) {
-        const int v = a.trans_tok[t];
-        if (a.root_child[v] >= 0) continue;     // already boosted in the vocabulary pass
-        float x = row[v] + a.lam;
-        if (mask_eos && v == a.eos) x = -INFINITY;
-        if (better(x, v, bv, bi)) { bv = x; bi = v; }
-      }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-    }
-    const bool fin = a.finished[m] != 0;
-    const int tok = fin ? a.pad : bi;
-    // AC transition: look tok up in trans(s) (sorted), else the root child, else root
-    int dst = -1;
-    for (int t = a.trans_off[s] + lane; t < a.trans_off[s + 1]; t += 64)
-      if (a.trans_tok[t] == tok) dst = a.trans_dst[t];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) dst = max(dst, __shfl_xor(dst, o, 64));
-    if (lane == 0) {
-      if (dst < 0) dst = (tok >= 0 && tok < a.V && a.root_child[tok] >= 0) ? a.root_child[tok] : 0;
-      a.state[m] = dst;
-      a.next_ids[m] = tok;
-      a.out_ids[(long)m * a.out_ld + step] = tok;
-      const bool nf = fin || tok == a.eos;
-      a.finished[m] = nf ? 1 : 0;
-      if (!nf) atomicAdd(&n_unfinished, 1);
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int c = lane; c < a.nchunk; c += 64) {
+    const float v = a.part_val[m * a.nchunk + c];
+    const int i = a.part_idx[m * a.nchunk + c];
+    if (better(v, i, bv, bi)) { bv = v; bi = i; }
+  }
+  const int s = a.state[m];
+  const int t0 = a.trans_off[s], t1 = a.trans_off[s + 1];
+  if (a.lam != 0.f) {
+    const float* row = a.logits + (long)m * a.ld;
+    for (int t = t0 + lane; t < t1; t += 64) {
+      const int v = a.trans_tok[t];
+      if (a.root_child[v] >= 0) continue;     // already boosted in the vocabulary pass
+      float x = row[v] + a.lam;
+      if (mask_eos && v == a.eos) x = -INFINITY;
+      if (better(x, v, bv, bi)) { bv = x; bi = v; }
     }
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    *a.step = step + 1;
-    *a.pos = *a.pos + 1;
-    if (n_unfinished == 0 && *a.all_done == 0) *a.all_done = step + 1;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+  }
+  const bool fin = a.finished[m] != 0;
+  const int tok = fin ? a.pad : bi;
+  // AC transition: tok in trans(s) → its target, else the root child, else root
+  int dst = -1;
+  for (int t = t0 + lane; t < t1; t += 64)
+    if (a.trans_tok[t] == tok) dst = a.trans_dst[t];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) dst = max(dst, __shfl_xor(dst, o, 64));
+  if (lane == 0) {
+    if (dst < 0) dst = (tok >= 0 && tok < a.V && a.root_child[tok] >= 0) ? a.root_child[tok] : 0;
+    a.state[m] = dst;
+    a.next_ids[m] = tok;
+    a.out_ids[(long)m * a.out_ld + step] = tok;
+    const bool nf = fin || tok == a.eos;
+    a.finished[m] = nf ? 1 : 0;
+    if (!nf) atomicAdd(a.unfinished, 1);
+    __threadfence();
+    if (atomicAdd(a.ticket, 1) == a.M - 1) {       // every row has arrived
+      __threadfence();
+      const int nun = atomicAdd(a.unfinished, 0);
+      *a.step = step + 1;
+      *a.pos = *a.pos + 1;
+      if (nun == 0 && *a.all_done == 0) *a.all_done = step + 1;
+      *a.unfinished = 0;
+      *a.ticket = 0;
+      __threadfence();
+    }
   }
 }
 
@@ -133,7 +135,7 @@ void gather_col(int* dst, const int* src, int M, int ld, int col, hipStream_t s)
 
 void select_greedy(const SelectArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(select_partial_kernel, dim3(a.nchunk, a.M), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(select_finalize_kernel, dim3(1), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(select_finalize_kernel, dim3(a.M), dim3(64), 0, s, a);
 }
 
 }  // namespace wcb

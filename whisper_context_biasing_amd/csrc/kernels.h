@@ -15,6 +15,8 @@ struct GemmArgs {
   const void* W = nullptr; long ldw = 0;
   int M = 0, N = 0, K = 0;
   const float* bias = nullptr;     // [N] f32
+  const float* ln_w = nullptr;     // fused LayerNorm of the f32 A rows (skinny path): gamma, beta
+  const float* ln_b = nullptr;
   int act = 0;                     // 0 none, 1 gelu(erf)
   const float* resid = nullptr;    // f32, same addressing as out (mode 0), may alias out
   const float* addrow = nullptr;   // f32 [c_Mb][N] row table added after act (encoder positions)
@@ -70,6 +72,7 @@ struct SelectArgs {
   int* next_ids = nullptr; int* out_ids = nullptr; int out_ld = 0;
   float* part_val = nullptr; int* part_idx = nullptr; int nchunk = 0;
   int* all_done = nullptr;
+  int* ticket = nullptr; int* unfinished = nullptr;   // zero between steps (reset by the last row)
 };
 void select_greedy(const SelectArgs& a, hipStream_t s);
 void advance_forced(int* next_ids, const int* forced, int M, int ld, int* pos, hipStream_t s);

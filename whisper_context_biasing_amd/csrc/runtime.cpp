@@ -555,7 +555,7 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
     HIPCHK(hipMemcpyAsync(h->encout.p, enc_out, M * d * e, hipMemcpyDeviceToDevice, h->hs));
 }
 
-enum { I_STEP = 0, I_POS = 1, I_DONE = 2, I_NEXT = 16 };
+enum { I_STEP = 0, I_POS = 1, I_DONE = 2, I_TICKET = 3, I_UNFIN = 4, I_NEXT = 16 };
 
 void ensure_dec_ws(wcb_handle* h, int B, int T, int out_ld) {
   const size_t e = esize(h->d.dtype), d = h->d.d_model, L = h->d.n_layers, S = h->S();
@@ -613,9 +613,9 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
   const size_t xkv_l = 2 * (size_t)B * H * S * 64;
   for (int l = 0; l < L; ++l) {
     const LayerW& w = h->dec[l];
-    layernorm(h->dt, x, w.ln1_w, w.ln1_b, h->dh.p, B, d, h->hs);
     char* cache = (char*)h->kvself.p + l * cache_l * e;
-    GemmArgs q = rowgemm(h->dh.p, d, w.qkv_w, B, 3 * d, d, h->dq.p, d);
+    GemmArgs q = rowgemm(x, d, w.qkv_w, B, 3 * d, d, h->dq.p, d);   // LayerNorm fused (f32 A rows)
+    q.ln_w = w.ln1_w; q.ln_b = w.ln1_b;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
     gemm(h->dt, q, h->hs);
     AttnArgs a;
@@ -628,8 +628,8 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     o.bias = w.o_b; o.resid = x; o.out_f32 = 1;
     gemm(h->dt, o, h->hs);
     // cross attention over the precomputed encoder K/V
-    layernorm(h->dt, x, w.lnx_w, w.lnx_b, h->dh.p, B, d, h->hs);
-    GemmArgs xq = rowgemm(h->dh.p, d, w.xq_w, B, d, d, h->dq.p, d);
+    GemmArgs xq = rowgemm(x, d, w.xq_w, B, d, d, h->dq.p, d);
+    xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b;
     xq.bias = w.xq_b;
     gemm(h->dt, xq, h->hs);
     AttnArgs xa;
@@ -643,8 +643,8 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1;
     gemm(h->dt, xo, h->hs);
     // MLP
-    layernorm(h->dt, x, w.ln2_w, w.ln2_b, h->dh.p, B, d, h->hs);
-    GemmArgs f1 = rowgemm(h->dh.p, d, w.fc1_w, B, h->d.ffn, d, h->dffn.p, h->d.ffn);
+    GemmArgs f1 = rowgemm(x, d, w.fc1_w, B, h->d.ffn, d, h->dffn.p, h->d.ffn);
+    f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b;
     f1.bias = w.fc1_b; f1.act = 1;
     gemm(h->dt, f1, h->hs);
     GemmArgs f2 = rowgemm(h->dffn.p, h->d.ffn, w.fc2_w, B, d, h->d.ffn, x, d);
@@ -652,8 +652,8 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     gemm(h->dt, f2, h->hs);
   }
   if (c.lm_head) {
-    layernorm(h->dt, x, h->dec_ln_w, h->dec_ln_b, h->dh.p, B, d, h->hs);
-    GemmArgs lm = rowgemm(h->dh.p, d, h->tok_emb, B, h->d.vocab, d, c.logits_out, c.logits_ld);
+    GemmArgs lm = rowgemm(x, d, h->tok_emb, B, h->d.vocab, d, c.logits_out, c.logits_ld);
+    lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b;
     lm.out_f32 = 1;
     gemm(h->dt, lm, h->hs);
   }
@@ -670,6 +670,7 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     s.out_ids = h->outbuf.as<int>(); s.out_ld = c.out_ld;
     s.part_val = h->part_val.as<float>(); s.part_idx = h->part_idx.as<int>(); s.nchunk = h->nchunk;
     s.all_done = ints + I_DONE;
+    s.ticket = ints + I_TICKET; s.unfinished = ints + I_UNFIN;
     select_greedy(s, h->hs);
   } else {
     advance_forced(next_ids, c.forced, B, c.forced_ld, pos, h->hs);
@@ -712,6 +713,7 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     REQUIRE(h && cfg && out_ids && out_steps && B > 0, "bad argument");
     if (!h->ready) throw WcbError(WCB_ERR_STATE, "weights not finalized");
     REQUIRE(cfg->num_beams == 1, "num_beams > 1 is not implemented in this build");
+    REQUIRE(B <= 64, "batch > 64 per handle: split the batch (decode GEMMs are the skinny M<=64 path)");
     REQUIRE(cfg->bias_boost >= 0.f, "bias_boost must be >= 0");
     REQUIRE(cfg->max_new_tokens >= 1, "max_new_tokens must be >= 1");
     const int P = prefix ? prefix_len : 1;
