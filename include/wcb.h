@@ -107,6 +107,11 @@ int wcb_debug_copy(wcb_handle* h, const char* name, void* dst, int64_t bytes, in
 /* out[M][N] = act(A[M][K] · W[N][K]ᵀ + bias) (+ resid), row-major, dtype of A/W = dtype */
 int wcb_op_gemm(int dtype, const void* A, const void* W, int M, int N, int K, const float* bias, int act,
                 const float* resid, void* out, int out_f32, void* stream);
+/* decode-step fused form: out[M][N] = act(LN(X) · W[N][K]ᵀ + bias), X f32 [M][K] (M <= 64), with the
+ * LayerNorm row statistics taken from stats[M][K/16][2] = per-16-column (Σx, Σx²) partials */
+int wcb_op_gemm_ln(int dtype, const float* X, const float* ln_w, const float* ln_b, const float* stats,
+                   const void* W, int M, int N, int K, const float* bias, int act, void* out, int out_f32,
+                   void* stream);
 /* y[M][d] (dtype) = LayerNorm(x f32 [M][d]) * w + b, eps 1e-5 */
 int wcb_op_layernorm(int dtype, const float* x, const float* w, const float* b, void* y, int M, int d,
                      void* stream);

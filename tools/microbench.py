@@ -50,6 +50,21 @@ def gemm_case(M, N, K, dt=torch.bfloat16):
     print(f"gemm M={M:6d} N={N:6d} K={K:5d}: {us:9.2f} us  {flops / us / 1e6:8.1f} TFLOP/s  {byts / us / 1e3:8.1f} GB/s")
 
 
+def gemm_ln_case(M, N, K):
+    X = torch.randn(M, K, device="cuda")
+    w = torch.randn(K, device="cuda")
+    b = torch.randn(K, device="cuda")
+    st = torch.stack([X.view(M, K // 16, 16).sum(-1), (X * X).view(M, K // 16, 16).sum(-1)], -1).contiguous()
+    W = torch.randn(N, K, device="cuda").bfloat16()
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+
+    def fn():
+        lib.wcb_op_gemm_ln(0, X.data_ptr(), w.data_ptr(), b.data_ptr(), st.data_ptr(), W.data_ptr(), M, N, K, None, 0,
+                           out.data_ptr(), 0, stream())
+    us = per_launch_us(fn)
+    print(f"gemm_ln M={M:6d} N={N:6d} K={K:5d}: {us:9.2f} us  {N * K * 2 / us / 1e3:8.1f} GB/s (weights)")
+
+
 def ln_case(M, d):
     x = torch.randn(M, d, device="cuda")
     w = torch.ones(d, device="cuda")
@@ -86,6 +101,8 @@ if __name__ == "__main__":
                       (48000, 2304, 768), (48000, 768, 768), (48000, 3072, 768), (48000, 768, 3072),
                       (48000, 18432, 768), (8192, 8192, 8192)]:
         gemm_case(M, N, K)
+    for N in (768, 2304, 3072):
+        gemm_ln_case(32, N, 768)
     attn_case(32, 12, 1, 1500, 0)
     attn_case(32, 12, 1, 64, 0)
     attn_case(32, 12, 1500, 1500, 1)

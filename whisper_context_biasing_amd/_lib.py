@@ -49,6 +49,8 @@ SIGNATURES = {
     "wcb_profile_read": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, _P]),
     "wcb_op_gemm": (C.c_int, [C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P, _P,
                               C.c_int, _P]),
+    "wcb_op_gemm_ln": (C.c_int, [C.c_int, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P,
+                                 C.c_int, _P]),
     "wcb_op_layernorm": (C.c_int, [C.c_int, _P, _P, _P, _P, C.c_int, C.c_int, _P]),
     "wcb_op_attention": (C.c_int, [C.c_int, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.c_int, _P]),

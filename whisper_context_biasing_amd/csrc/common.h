@@ -22,12 +22,8 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 #define WCB_DEV __device__ __forceinline__
 
 WCB_DEV float bf16_to_f(bf16_t v) { return __uint_as_float(uint32_t(v) << 16); }
-WCB_DEV bf16_t f_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return bf16_t((u >> 16) | 0x40);  // keep NaN a NaN
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return bf16_t(u >> 16);
-}
+// round-to-nearest-even; a plain __bf16 cast lowers to v_cvt_pk_bf16_f32 on gfx950 (NaN stays NaN)
+WCB_DEV bf16_t f_to_bf16(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 
 template <typename T> struct DT;
 template <> struct DT<bf16_t> {

@@ -24,16 +24,21 @@ WCB_DEV void glds16(const void* gptr, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(gptr, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-WCB_DEV long a_row(const GemmArgs& g, long m) { return (m / g.a_Mb) * g.a_strideB + (m % g.a_Mb) * g.lda; }
-WCB_DEV long c_row(const GemmArgs& g, long m) { return (m / g.c_Mb) * g.c_strideB + (m % g.c_Mb) * g.ldc; }
+// 32-bit row arithmetic (M < 2^31); the batched form only for the conv stem
+WCB_DEV long a_row(const GemmArgs& g, int m) {
+  return g.a_Mb ? (long)(m / g.a_Mb) * g.a_strideB + (long)(m % g.a_Mb) * g.lda : (long)m * g.lda;
+}
+WCB_DEV long c_row(const GemmArgs& g, int m) {
+  return g.c_Mb ? (long)(m / g.c_Mb) * g.c_strideB + (long)(m % g.c_Mb) * g.ldc : (long)m * g.ldc;
+}
 
 // Store 8 consecutive output columns n..n+7 of row m (n % 8 == 0, all in one head for mode 1).
 template <typename T>
-WCB_DEV void epi_store8(const GemmArgs& g, long m, int n, float* v) {
+WCB_DEV void epi_store8(const GemmArgs& g, int m, int n, float* v) {
   if (g.mode == 1) {
     const int hh = n >> 6, dd = n & 63;
     const int grp = hh / g.hs_H, h = hh % g.hs_H;
-    const long b = m / g.hs_S, t = m % g.hs_S;
+    const int b = m / g.hs_S, t = m % g.hs_S;
     const long off = ((((long)grp * g.hs_B + b) * g.hs_H + h) * g.hs_S + t) * 64 + dd;
     store8<T>(reinterpret_cast<T*>(g.out) + off, v);
     return;
@@ -50,33 +55,34 @@ WCB_DEV void epi_store8(const GemmArgs& g, long m, int n, float* v) {
 }
 
 template <typename T>
-WCB_DEV void epi_store1(const GemmArgs& g, long m, int n, float v) {
+WCB_DEV float epi_store1(const GemmArgs& g, int m, int n, float v) {
   if (g.mode == 2 && n >= g.n_split) {
     const int n2 = n - g.n_split;
     const int hh = n2 >> 6, dd = n2 & 63;
     const int kv = hh / g.hs_H, h = hh % g.hs_H;
     const long off = ((((long)kv * g.hs_B + m) * g.hs_H + h) * g.kv_T + *g.pos) * 64 + dd;
     reinterpret_cast<T*>(g.kv_out)[off] = DT<T>::fromf(v);
-    return;
+    return v;
   }
   if (g.mode == 1) {
     const int hh = n >> 6, dd = n & 63;
     const int grp = hh / g.hs_H, h = hh % g.hs_H;
-    const long b = m / g.hs_S, t = m % g.hs_S;
+    const int b = m / g.hs_S, t = m % g.hs_S;
     const long off = ((((long)grp * g.hs_B + b) * g.hs_H + h) * g.hs_S + t) * 64 + dd;
     reinterpret_cast<T*>(g.out)[off] = DT<T>::fromf(v);
-    return;
+    return v;
   }
   const long off = c_row(g, m) + n;
   if (g.resid) v += g.resid[off];
   if (g.out_f32) reinterpret_cast<float*>(g.out)[off] = v;
   else reinterpret_cast<T*>(g.out)[off] = DT<T>::fromf(v);
+  return v;
 }
 
-WCB_DEV float epi_pointwise(const GemmArgs& g, long m, int n, float v) {
+WCB_DEV float epi_pointwise(const GemmArgs& g, int m, int n, float v) {
   if (g.bias) v += g.bias[n];
   if (g.act == 1) v = gelu_erf(v);
-  if (g.addrow) v += g.addrow[(m % g.c_Mb) * g.N + n];
+  if (g.addrow) v += g.addrow[(long)(g.c_Mb ? (int)m % g.c_Mb : (int)m) * g.N + n];
   return v;
 }
 
@@ -108,7 +114,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(GemmArgs g) {
 #pragma unroll
   for (int i = 0; i < IA; ++i) {
     const int r = (wave + i * NW) * 8 + (lane >> 3);
-    const long m = min(m0 + r, g.M - 1);
+    const int m = min(m0 + r, g.M - 1);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
     a_src[i] = A + a_row(g, m) + c * CE;
   }
@@ -180,7 +186,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(GemmArgs g) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = wm * TM + i * 16 + (lane >> 4) * 4 + e;
-        const long m = min((long)m0 + row, (long)g.M - 1);
+        const int m = min(m0 + row, g.M - 1);
         ct[row * LDC + col] = epi_pointwise(g, m, n, acc[i][j][e]);
       }
   }
@@ -189,7 +195,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(GemmArgs g) {
 #pragma unroll 2
   for (int idx = tid; idx < BM * C8; idx += NT) {
     const int row = idx / C8, c8 = idx % C8;
-    const long m = m0 + row;
+    const int m = m0 + row;
     const int n = n0 + c8 * 8;
     if (m >= g.M || n >= g.N) continue;
     float v[8];
@@ -201,28 +207,77 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(GemmArgs g) {
   }
 }
 
-// Skinny GEMM for the decode step (M = batch <= 64 rows): one workgroup = 16 output columns, its
-// NW waves split K into NW contiguous ranges of KS 32-deep MFMA steps, every load of the wave is
+// Skinny GEMM for the decode step (M = batch <= 64 rows): one workgroup = NF·16 output columns,
+// its NW waves split K into NW contiguous ranges of KS 32-deep MFMA steps, every load of a wave is
 // issued up front (weights are streamed once from HBM, activations come from L2), partial tiles
-// are summed through LDS. With LN the A operand is the f32 residual stream normalised on the fly
-// (the decoder's pre-attention / pre-MLP LayerNorm fused into the projection that consumes it).
-template <typename T, int MF, int NW, int KS, bool LN>
+// are summed through LDS.
+//  * LN: the A operand is the f32 residual stream, normalised on the fly (the decoder's pre-block
+//    LayerNorm fused into the projection that consumes it). Row statistics come from the
+//    deterministic per-16-column partial sums (Σx, Σx²) the producer of x wrote (st_in).
+//  * st_out: a residual-writing GEMM (NF = 1) publishes those partial sums of the new x rows.
+//  * sel_val: the LM head reduces its logits tile to a per-row (max, argmax) partial with the
+//    bias-list root boost and the EOS mask applied (k_select.hip finishes the reduction).
+template <typename T, int MF, int NF, int NW, int KS, bool LN>
 __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
   using Frag = typename DT<T>::frag;
-  __shared__ __attribute__((aligned(16))) float red[NW][MF * 16][17];
-  __shared__ float lnred[NW][MF * 16][2];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * 16;
-  const long n = min(n0 + (lane & 15), g.N - 1);
-  const int kb = wave * (KS * 32) + 8 * (lane >> 4);
-  const T* W = reinterpret_cast<const T*>(g.W) + n * g.ldw + kb;
-  Frag b[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) b[ks] = load_frag<T>(W + ks * 32);
-  f32x4 acc[MF];
-#pragma unroll
-  for (int i = 0; i < MF; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int NT = NW * 64, BNC = NF * 16;
+  // LDS slabs for the cross-wave K reduction: as many as fit in 48 KB, extra waves accumulate in rounds
+  constexpr int SLAB = MF * 16 * (BNC + 1) * 4;
+  constexpr int SL = (NW * SLAB <= 49152) ? NW : (NW / 2 * SLAB <= 49152) ? NW / 2 : (NW / 4 * SLAB <= 49152) ? NW / 4 : 1;
+  __shared__ __attribute__((aligned(16))) float red[SL][MF * 16][BNC + 1];
+  __shared__ float st_mean[MF * 16], st_rstd[MF * 16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // LN statistics partials first: the oldest loads retire first (in-order vmcnt), so the row
+  // statistics are ready while the weight stream is still in flight
+  constexpr int NB = NW * KS * 2;                          // 16-column blocks per row (K / 16)
+  constexpr int TPR = NB % 16 == 0 ? 16 : NB % 8 == 0 ? 8 : NB % 4 == 0 ? 4 : NB % 2 == 0 ? 2 : 1;
+  constexpr int RPP = NT / TPR;                            // rows per pass
+  constexpr int PASSES = (MF * 16 + RPP - 1) / RPP;
+  float s1[PASSES], s2[PASSES];
   if constexpr (LN) {
+#pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+      const int m = min(ps * RPP + tid / TPR, g.M - 1);
+      s1[ps] = 0.f;
+      s2[ps] = 0.f;
+      float2 pv[NB / TPR];
+#pragma unroll
+      for (int j = 0; j < NB / TPR; ++j)
+        pv[j] = *reinterpret_cast<const float2*>(g.st_in + ((long)m * NB + j * TPR + tid % TPR) * 2);
+#pragma unroll
+      for (int j = 0; j < NB / TPR; ++j) { s1[ps] += pv[j].x; s2[ps] += pv[j].y; }
+    }
+  }
+  const int n0 = blockIdx.x * BNC;
+  const int kb = wave * (KS * 32) + 8 * (lane >> 4);
+  Frag b[NF][KS];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const long n = min(n0 + j * 16 + (lane & 15), g.N - 1);
+    const T* W = reinterpret_cast<const T*>(g.W) + n * g.ldw + kb;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) b[j][ks] = load_frag<T>(W + ks * 32);
+  }
+  f32x4 acc[MF][NF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (LN) {
+    const float* X = reinterpret_cast<const float*>(g.A);
+    float xv[MF][KS][8];
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const int m = min(i * 16 + (lane & 15), g.M - 1);
+      const float* xr = X + a_row(g, m) + kb;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(xr + ks * 32);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(xr + ks * 32 + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { xv[i][ks][e] = x0[e]; xv[i][ks][e + 4] = x1[e]; }
+      }
+    }
     float gw[KS][8], gb[KS][8];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -233,36 +288,23 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) { gw[ks][e] = w0[e]; gw[ks][e + 4] = w1[e]; gb[ks][e] = b0[e]; gb[ks][e + 4] = b1[e]; }
     }
-    // one pass over this wave's K range: keep the x fragments, reduce Σx and Σx² per row over the
-    // four lane groups and then over the waves (LDS) — no second read of the residual stream
-    const float* X = reinterpret_cast<const float*>(g.A);
-    float xv[MF][KS][8];
+    // row statistics: TPR threads per row, fixed-order sums of the producer's partials
 #pragma unroll
-    for (int i = 0; i < MF; ++i) {
-      const int m = min(i * 16 + (lane & 15), g.M - 1);
-      const float* xr = X + a_row(g, m) + kb;
-      float ps = 0.f, pq = 0.f;
+    for (int ps = 0; ps < PASSES; ++ps) {
+      float a1 = s1[ps], a2 = s2[ps];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const f32x4 x0 = *reinterpret_cast<const f32x4*>(xr + ks * 32);
-        const f32x4 x1 = *reinterpret_cast<const f32x4*>(xr + ks * 32 + 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { xv[i][ks][e] = x0[e]; xv[i][ks][e + 4] = x1[e]; }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { ps += xv[i][ks][e]; pq += xv[i][ks][e] * xv[i][ks][e]; }
+      for (int o = 1; o < TPR; o <<= 1) { a1 += __shfl_xor(a1, o, 64); a2 += __shfl_xor(a2, o, 64); }
+      const int r = ps * RPP + tid / TPR;
+      if (tid % TPR == 0 && r < MF * 16) {
+        const float mean = a1 / g.K;
+        st_mean[r] = mean;
+        st_rstd[r] = rsqrtf(fmaxf(a2 / g.K - mean * mean, 0.f) + 1e-5f);
       }
-      ps += __shfl_xor(ps, 16, 64); ps += __shfl_xor(ps, 32, 64);
-      pq += __shfl_xor(pq, 16, 64); pq += __shfl_xor(pq, 32, 64);
-      if (lane < 16) { lnred[wave][i * 16 + lane][0] = ps; lnred[wave][i * 16 + lane][1] = pq; }
     }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) { s1 += lnred[w][i * 16 + (lane & 15)][0]; s2 += lnred[w][i * 16 + (lane & 15)][1]; }
-      const float mean = s1 / g.K;
-      const float rstd = rsqrtf(fmaxf(s2 / g.K - mean * mean, 0.f) + 1e-5f);
+      const float mean = st_mean[i * 16 + (lane & 15)], rstd = st_rstd[i * 16 + (lane & 15)];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         Frag a;
@@ -272,7 +314,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
           if constexpr (sizeof(T) == 4) a[e] = v;
           else a[e] = __builtin_bit_cast(typename std::remove_reference<decltype(a[0])>::type, DT<T>::fromf(v));
         }
-        acc[i] = mma16(a, b[ks], acc[i]);
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = mma16(a, b[j][ks], acc[i][j]);
       }
     }
   } else {
@@ -285,22 +328,71 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) a[ks] = load_frag<T>(ap + ks * 32);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) acc[i] = mma16(a[ks], b[ks], acc[i]);
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = mma16(a[ks], b[j][ks], acc[i][j]);
     }
   }
 #pragma unroll
-  for (int i = 0; i < MF; ++i)
+  for (int round = 0; round < NW / SL; ++round) {
+    if (wave / SL == round) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) red[wave][i * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[i][e];
-  __syncthreads();
-  for (int t = threadIdx.x; t < MF * 16 * 16; t += NW * 64) {
-    const int row = t >> 4, col = t & 15;
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float& r = red[wave % SL][i * 16 + (lane >> 4) * 4 + e][j * 16 + (lane & 15)];
+            r = round == 0 ? acc[i][j][e] : r + acc[i][j][e];
+          }
+    }
+    __syncthreads();
+  }
+  const bool mask_eos = g.sel_val && *g.sel_step < g.sel_min_new;
+  // epilogue: thread → (row, col) with the columns of a row contiguous in the wave, so row-wise
+  // reductions (stats partials: 16 lanes; argmax partial: BNC lanes) are shuffles
+  for (int t0 = 0; t0 < MF * 16 * BNC; t0 += NT) {
+    const int t = t0 + tid;
+    const int row = t / BNC, col = t % BNC;
     const int nn = n0 + col;
-    if (row >= g.M || nn >= g.N) continue;
+    const bool valid = t < MF * 16 * BNC && row < g.M && nn < g.N;
     float v = 0.f;
+    if (valid) {
 #pragma unroll
-    for (int w = 0; w < NW; ++w) v += red[w][row][col];
-    epi_store1<T>(g, row, nn, epi_pointwise(g, row, nn, v));
+      for (int w = 0; w < SL; ++w) v += red[w][row][col];
+      v = epi_pointwise(g, row, nn, v);
+      v = epi_store1<T>(g, row, nn, v);
+    }
+    if (g.st_out) {   // NF == 1: 16 contiguous lanes hold one row of the block
+      float s1 = valid ? v : 0.f, s2 = valid ? v * v : 0.f;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      if (valid && (t & 15) == 0) {
+        float* p = g.st_out + ((long)row * g.st_nb + blockIdx.x) * 2;
+        p[0] = s1;
+        p[1] = s2;
+      }
+    }
+    if (g.sel_val) {  // BNC == 64: one wave per row
+      float x = -INFINITY;
+      int xi = 0x7fffffff;
+      if (valid) {
+        x = v;
+        if (g.sel_lam != 0.f && ((g.sel_root_bits[nn >> 5] >> (nn & 31)) & 1u)) x += g.sel_lam;
+        if (mask_eos && nn == g.sel_eos) x = -INFINITY;
+        xi = nn;
+      }
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float ov = __shfl_xor(x, o, 64);
+        const int oi = __shfl_xor(xi, o, 64);
+        if (ov > x || (ov == x && oi < xi)) { x = ov; xi = oi; }
+      }
+      if (lane == 0 && row < g.M) {
+        g.sel_val[(long)row * gridDim.x + blockIdx.x] = x;
+        g.sel_idx[(long)row * gridDim.x + blockIdx.x] = xi;
+      }
+    }
   }
 }
 
@@ -319,18 +411,18 @@ static void launch_tile(const GemmArgs& g, hipStream_t s) {
   hipLaunchKernelGGL((gemm_tile_kernel<T, BM, BN, WM, WN>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
 }
 
-template <typename T, int MF, int NW, int KS>
+template <typename T, int MF, int NF, int NW, int KS>
 static void launch_skinny_k(const GemmArgs& g, hipStream_t s) {
-  const int grid = (g.N + 15) / 16;
-  if (g.ln_w) hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NW, KS, true>), dim3(grid), dim3(NW * 64), 0, s, g);
-  else hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NW, KS, false>), dim3(grid), dim3(NW * 64), 0, s, g);
+  const int grid = (g.N + NF * 16 - 1) / (NF * 16);
+  if (g.ln_w) hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NF, NW, KS, true>), dim3(grid), dim3(NW * 64), 0, s, g);
+  else hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NF, NW, KS, false>), dim3(grid), dim3(NW * 64), 0, s, g);
 }
 
 // K = NW waves x KS steps x 32: pick the wave count first, then the (compile-time) steps per wave.
-template <typename T, int MF>
+template <typename T, int MF, int NF>
 static bool launch_skinny_mf(const GemmArgs& g, hipStream_t s) {
   const int K = g.K;
-#define WCB_SK(nw, ks) if (K == nw * ks * 32) { launch_skinny_k<T, MF, nw, ks>(g, s); return true; }
+#define WCB_SK(nw, ks) if (K == nw * ks * 32) { launch_skinny_k<T, MF, NF, nw, ks>(g, s); return true; }
   WCB_SK(1, 1) WCB_SK(1, 2) WCB_SK(2, 2) WCB_SK(4, 2) WCB_SK(4, 3) WCB_SK(4, 4) WCB_SK(8, 2)
   WCB_SK(8, 3) WCB_SK(8, 4) WCB_SK(8, 5) WCB_SK(8, 6) WCB_SK(16, 4) WCB_SK(16, 5) WCB_SK(16, 6)
   WCB_SK(16, 8) WCB_SK(16, 10) WCB_SK(16, 12)
@@ -342,9 +434,13 @@ template <typename T>
 static void gemm_t(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 64 || g.mode == 2 || g.ln_w) {
     bool ok;
-    if (g.M <= 16) ok = launch_skinny_mf<T, 1>(g, s);
-    else if (g.M <= 32) ok = launch_skinny_mf<T, 2>(g, s);
-    else ok = launch_skinny_mf<T, 4>(g, s);
+    if (g.sel_val) {   // LM head: 64 columns per workgroup (A re-read 4x less), fused argmax partial
+      if (g.M <= 16) ok = launch_skinny_mf<T, 1, 4>(g, s);
+      else if (g.M <= 32) ok = launch_skinny_mf<T, 2, 4>(g, s);
+      else ok = launch_skinny_mf<T, 4, 4>(g, s);
+    } else if (g.M <= 16) ok = launch_skinny_mf<T, 1, 1>(g, s);
+    else if (g.M <= 32) ok = launch_skinny_mf<T, 2, 1>(g, s);
+    else ok = launch_skinny_mf<T, 4, 1>(g, s);
     if (!ok) fprintf(stderr, "wcb: no skinny GEMM instance for K=%d\n", g.K);
     return;
   }

@@ -77,25 +77,41 @@ void layernorm(DType t, const float* x, const float* w, const float* b, void* y,
   }
 }
 
+// also publishes the per-16-column partial sums (Σx, Σx²) of the new row for the fused LayerNorm
+// of the first decoder GEMM (deterministic fixed-order sums, see k_gemm.hip st_in)
 template <typename T>
-__global__ void embed_kernel(const T* __restrict__ emb, const T* __restrict__ pemb, const int* __restrict__ ids,
-                             const int* __restrict__ pos, float* __restrict__ x, int M, int d) {
+__global__ __launch_bounds__(256) void embed_kernel(const T* __restrict__ emb, const T* __restrict__ pemb, const int* __restrict__ ids,
+                                                    const int* __restrict__ pos, float* __restrict__ x, float* __restrict__ st,
+                                                    int M, int d) {
   const int row = blockIdx.x;
   const int p = *pos;
   const long id = ids[row];
-  for (int c = threadIdx.x; c < d; c += blockDim.x)
-    x[(long)row * d + c] = DT<T>::tof(emb[id * d + c]) + DT<T>::tof(pemb[(long)p * d + c]);
+  for (int c0 = 0; c0 < d; c0 += 256) {
+    const int c = c0 + threadIdx.x;
+    float v = 0.f;
+    if (c < d) {
+      v = DT<T>::tof(emb[id * d + c]) + DT<T>::tof(pemb[(long)p * d + c]);
+      x[(long)row * d + c] = v;
+    }
+    float s1 = v, s2 = v * v;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+    if (st && c < d && (c & 15) == 0) {
+      st[((long)row * (d / 16) + c / 16) * 2] = s1;
+      st[((long)row * (d / 16) + c / 16) * 2 + 1] = s2;
+    }
+  }
 }
 
-void embed(DType t, const void* emb, const void* pemb, const int* ids, const int* pos, float* x, int M, int d,
-           hipStream_t s) {
+void embed(DType t, const void* emb, const void* pemb, const int* ids, const int* pos, float* x, float* st, int M,
+           int d, hipStream_t s) {
   switch (t) {
     case kBF16: hipLaunchKernelGGL(embed_kernel<bf16_t>, dim3(M), dim3(256), 0, s, (const bf16_t*)emb,
-                                   (const bf16_t*)pemb, ids, pos, x, M, d); break;
+                                   (const bf16_t*)pemb, ids, pos, x, st, M, d); break;
     case kF16: hipLaunchKernelGGL(embed_kernel<f16_t>, dim3(M), dim3(256), 0, s, (const f16_t*)emb,
-                                  (const f16_t*)pemb, ids, pos, x, M, d); break;
+                                  (const f16_t*)pemb, ids, pos, x, st, M, d); break;
     case kF32: hipLaunchKernelGGL(embed_kernel<float>, dim3(M), dim3(256), 0, s, (const float*)emb,
-                                  (const float*)pemb, ids, pos, x, M, d); break;
+                                  (const float*)pemb, ids, pos, x, st, M, d); break;
   }
 }
 

@@ -133,6 +133,10 @@ void gather_col(int* dst, const int* src, int M, int ld, int col, hipStream_t s)
   hipLaunchKernelGGL(gather_col_kernel, dim3(1), dim3(256), 0, s, dst, src, M, ld, col);
 }
 
+void select_finalize(const SelectArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(select_finalize_kernel, dim3(a.M), dim3(64), 0, s, a);
+}
+
 void select_greedy(const SelectArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(select_partial_kernel, dim3(a.nchunk, a.M), dim3(256), 0, s, a);
   hipLaunchKernelGGL(select_finalize_kernel, dim3(a.M), dim3(64), 0, s, a);

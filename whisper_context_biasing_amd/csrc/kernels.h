@@ -8,10 +8,11 @@ namespace wcb {
 enum DType : int { kBF16 = 0, kF16 = 1, kF32 = 2 };
 
 // C[M,N] = epilogue(A[M,K] · W[N,K]ᵀ).  A row m lives at A + (m / a_Mb)·a_strideB + (m % a_Mb)·lda
+// (a_Mb == 0: A + m·lda)
 // (elements): one formula covers plain row-major operands, per-clip batched operands and the
 // overlapping im2col rows of the two conv-stem convolutions.
 struct GemmArgs {
-  const void* A = nullptr; long lda = 0; long a_Mb = 1L << 40; long a_strideB = 0;
+  const void* A = nullptr; long lda = 0; int a_Mb = 0; long a_strideB = 0;   // a_Mb 0: plain rows
   const void* W = nullptr; long ldw = 0;
   int M = 0, N = 0, K = 0;
   const float* bias = nullptr;     // [N] f32
@@ -22,10 +23,17 @@ struct GemmArgs {
   const float* addrow = nullptr;   // f32 [c_Mb][N] row table added after act (encoder positions)
   void* out = nullptr; int out_f32 = 0;
   int mode = 0;                    // 0 rows, 1 head-split, 2 decode qkv (q rows + kv-cache append)
-  long ldc = 0; long c_Mb = 1L << 40; long c_strideB = 0;
+  long ldc = 0; int c_Mb = 0; long c_strideB = 0;
   int hs_S = 0, hs_H = 0, hs_B = 0;        // mode 1: [g][B][H][S][64]; mode 2: rows of the cache
   const int* pos = nullptr; int kv_T = 0;  // mode 2: cache position (device) and cache length
   void* kv_out = nullptr; int n_split = 0; // mode 2: columns >= n_split go to the cache
+  // decode-step fusions (skinny path)
+  const float* st_in = nullptr;    // LN row statistics partials [M][st_nb][2] (Σx, Σx²) of A
+  float* st_out = nullptr;         // partials of the written f32 rows (residual GEMMs, NF = 1)
+  int st_nb = 0;                   // 16-column blocks per row (d / 16)
+  float* sel_val = nullptr; int* sel_idx = nullptr;   // LM head: per-(row, workgroup) argmax partial
+  const uint32_t* sel_root_bits = nullptr; float sel_lam = 0.f;
+  int sel_eos = -1; const int* sel_step = nullptr; int sel_min_new = 0;
 };
 
 void gemm(DType t, const GemmArgs& g, hipStream_t s);
@@ -36,7 +44,7 @@ void layernorm(DType t, const float* x, const float* w, const float* b, void* y,
 
 // x[r][:] = emb[ids[r]][:] + pos_emb[*pos + r_pos][:] (f32 out), r_pos = r % rows_per_seq.
 void embed(DType t, const void* emb, const void* pos_emb, const int* ids, const int* pos, float* x,
-           int M, int d, hipStream_t s);
+           float* stats, int M, int d, hipStream_t s);
 
 // Attention over heads of 64. q row for (b, i): q + (b·q_Sb + i)·ldq + h·64.
 // key j of (b, h): k + b·k_sb + h·k_sh + j·k_sk (same strides for v).
@@ -74,7 +82,8 @@ struct SelectArgs {
   int* all_done = nullptr;
   int* ticket = nullptr; int* unfinished = nullptr;   // zero between steps (reset by the last row)
 };
-void select_greedy(const SelectArgs& a, hipStream_t s);
+void select_greedy(const SelectArgs& a, hipStream_t s);          // vocabulary pass + finalize
+void select_finalize(const SelectArgs& a, hipStream_t s);        // partials already written (fused LM head)
 void advance_forced(int* next_ids, const int* forced, int M, int ld, int* pos, hipStream_t s);
 void gather_col(int* dst, const int* src, int M, int ld, int col, hipStream_t s);
 

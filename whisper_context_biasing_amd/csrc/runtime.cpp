@@ -140,7 +140,7 @@ struct wcb_handle {
   DevBuf xt, hbuf, x, h, qkv, att, ffn, encout;
   // decoder workspace
   int dec_B = 0, dec_T = 0;
-  DevBuf xkv, kvself, dx, dh, dq, datt, dffn, logits, part_val, part_idx, ints, outbuf, forced;
+  DevBuf xkv, kvself, dx, dh, dq, datt, dffn, dstats, logits, part_val, part_idx, ints, outbuf, forced;
   int nchunk = 64;
   // graph cache
   hipGraphExec_t gexec = nullptr;
@@ -573,6 +573,8 @@ void ensure_dec_ws(wcb_handle* h, int B, int T, int out_ld) {
   h->datt.ensure((size_t)B * d * e);
   h->dffn.ensure((size_t)B * h->d.ffn * e);
   h->logits.ensure((size_t)B * h->d.vocab * 4);
+  h->dstats.ensure((size_t)B * (d / 16) * 2 * 4);
+  h->nchunk = (h->d.vocab + 63) / 64;      // one argmax partial per LM-head workgroup (64 columns)
   h->part_val.ensure((size_t)B * h->nchunk * 4);
   h->part_idx.ensure((size_t)B * h->nchunk * 4);
   h->ints.ensure((size_t)(I_NEXT + 3 * B + 16) * 4);
@@ -608,14 +610,16 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
   int* pos = ints + I_POS;
   int* next_ids = ints + I_NEXT;
   float* x = h->dx.as<float>();
-  embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, x, B, d, h->hs);
+  float* st = h->dstats.as<float>();
+  const int nb = d / 16;
+  embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, x, st, B, d, h->hs);
   const size_t cache_l = 2 * (size_t)B * H * T * 64;   // elements per layer (K then V)
   const size_t xkv_l = 2 * (size_t)B * H * S * 64;
   for (int l = 0; l < L; ++l) {
     const LayerW& w = h->dec[l];
     char* cache = (char*)h->kvself.p + l * cache_l * e;
     GemmArgs q = rowgemm(x, d, w.qkv_w, B, 3 * d, d, h->dq.p, d);   // LayerNorm fused (f32 A rows)
-    q.ln_w = w.ln1_w; q.ln_b = w.ln1_b;
+    q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nb;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
     gemm(h->dt, q, h->hs);
     AttnArgs a;
@@ -625,11 +629,11 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     a.o = h->datt.p; a.ldo = d; a.o_Sb = 1; a.B = B; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1;
     attention_decode(h->dt, a, h->hs);
     GemmArgs o = rowgemm(h->datt.p, d, w.o_w, B, d, d, x, d);
-    o.bias = w.o_b; o.resid = x; o.out_f32 = 1;
+    o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st; o.st_nb = nb;
     gemm(h->dt, o, h->hs);
     // cross attention over the precomputed encoder K/V
     GemmArgs xq = rowgemm(x, d, w.xq_w, B, d, d, h->dq.p, d);
-    xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b;
+    xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nb;
     xq.bias = w.xq_b;
     gemm(h->dt, xq, h->hs);
     AttnArgs xa;
@@ -640,21 +644,26 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     xa.o = h->datt.p; xa.ldo = d; xa.o_Sb = 1; xa.B = B; xa.H = H; xa.nkeys = S;
     attention_decode(h->dt, xa, h->hs);
     GemmArgs xo = rowgemm(h->datt.p, d, w.xo_w, B, d, d, x, d);
-    xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1;
+    xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st; xo.st_nb = nb;
     gemm(h->dt, xo, h->hs);
     // MLP
     GemmArgs f1 = rowgemm(x, d, w.fc1_w, B, h->d.ffn, d, h->dffn.p, h->d.ffn);
-    f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b;
+    f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nb;
     f1.bias = w.fc1_b; f1.act = 1;
     gemm(h->dt, f1, h->hs);
     GemmArgs f2 = rowgemm(h->dffn.p, h->d.ffn, w.fc2_w, B, d, h->d.ffn, x, d);
-    f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1;
+    f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st; f2.st_nb = nb;
     gemm(h->dt, f2, h->hs);
   }
   if (c.lm_head) {
     GemmArgs lm = rowgemm(x, d, h->tok_emb, B, h->d.vocab, d, c.logits_out, c.logits_ld);
-    lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b;
+    lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b; lm.st_in = st; lm.st_nb = nb;
     lm.out_f32 = 1;
+    if (c.select) {   // argmax partials with the root boost + EOS mask fused into the LM head
+      lm.sel_val = h->part_val.as<float>(); lm.sel_idx = h->part_idx.as<int>();
+      lm.sel_root_bits = c.bias->root_bits.as<uint32_t>(); lm.sel_lam = c.lam;
+      lm.sel_eos = h->d.eos_token_id; lm.sel_step = ints + I_STEP; lm.sel_min_new = c.min_new;
+    }
     gemm(h->dt, lm, h->hs);
   }
   if (c.select) {
@@ -671,7 +680,7 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     s.part_val = h->part_val.as<float>(); s.part_idx = h->part_idx.as<int>(); s.nchunk = h->nchunk;
     s.all_done = ints + I_DONE;
     s.ticket = ints + I_TICKET; s.unfinished = ints + I_UNFIN;
-    select_greedy(s, h->hs);
+    select_finalize(s, h->hs);
   } else {
     advance_forced(next_ids, c.forced, B, c.forced_ld, pos, h->hs);
   }
@@ -949,6 +958,18 @@ int wcb_op_gemm(int dtype, const void* A, const void* W, int M, int N, int K, co
     REQUIRE(K % (dtype == WCB_F32 ? 32 : 64) == 0, "K must be a multiple of the 128-byte K tile");
     GemmArgs g = rowgemm(A, K, W, M, N, K, out, N);
     g.bias = bias; g.act = act; g.resid = resid; g.out_f32 = out_f32;
+    gemm(DType(dtype), g, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+int wcb_op_gemm_ln(int dtype, const float* X, const float* ln_w, const float* ln_b, const float* stats,
+                   const void* W, int M, int N, int K, const float* bias, int act, void* out, int out_f32, void* stream) {
+  return guarded(nullptr, [&] {
+    REQUIRE(X && ln_w && ln_b && stats && W && out && M > 0 && M <= 64 && N > 0 && K % 16 == 0, "bad argument");
+    GemmArgs g = rowgemm(X, K, W, M, N, K, out, N);
+    g.ln_w = ln_w; g.ln_b = ln_b; g.st_in = stats; g.st_nb = K / 16;
+    g.bias = bias; g.act = act; g.out_f32 = out_f32;
     gemm(DType(dtype), g, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
   });
