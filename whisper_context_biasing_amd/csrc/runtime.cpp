@@ -19,6 +19,7 @@
 #include <stdexcept>
 #include <string>
 #include <vector>
+#include <cstdlib>
 #include <deque>
 
 #include "../../include/wcb.h"
@@ -120,7 +121,11 @@ struct wcb_handle {
   int device = 0;
   std::string err;
   hipStream_t hs = nullptr;
-  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr;
+  static constexpr int kMaxSub = 4;
+  hipStream_t sub[kMaxSub] = {};
+  hipEvent_t ev_join[kMaxSub] = {};
+  int n_sub = 2;   // decode row groups on concurrent streams
   std::map<std::string, std::vector<float>> host_w;
   std::vector<DevBuf> owned;
   bool ready = false;
@@ -289,6 +294,12 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     HIPCHK(hipStreamCreateWithFlags(&h->hs, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    for (int i = 0; i < wcb_handle::kMaxSub; ++i) {
+      HIPCHK(hipStreamCreateWithFlags(&h->sub[i], hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&h->ev_join[i], hipEventDisableTiming));
+    }
+    if (const char* ns = getenv("WCB_DECODE_SPLIT")) h->n_sub = std::max(1, std::min(atoi(ns), (int)wcb_handle::kMaxSub));
     // DFT table [416 cols][416 k]: col 2b = win·cos(2πbk/400), col 2b+1 = −win·sin(2πbk/400)
     std::vector<float> dft((size_t)kNCol * kNCol, 0.f);
     for (int c = 0; c < 402; ++c) {
@@ -350,6 +361,11 @@ void wcb_destroy(wcb_handle* h) {
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   if (h->ev_out) (void)hipEventDestroy(h->ev_out);
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  for (int i = 0; i < wcb_handle::kMaxSub; ++i) {
+    if (h->ev_join[i]) (void)hipEventDestroy(h->ev_join[i]);
+    if (h->sub[i]) (void)hipStreamDestroy(h->sub[i]);
+  }
   if (h->hs) (void)hipStreamDestroy(h->hs);
   delete h;
 }
@@ -600,71 +616,99 @@ struct StepCfg {
   const int* forced; int forced_ld;    // advance_forced source when !select
 };
 
-// One decoder step for every row (WhisperDecoder.forward with a KV cache, [tf] modeling_whisper.py:690-795),
-// LM head and token selection. Every position-dependent quantity is read on the device, so the
-// same launch sequence replays as a hipGraph.
-void decode_step(wcb_handle* h, const StepCfg& c) {
+// Decoder layers + LM head for rows [b0, b0 + nb) of the batch on stream `st_`: WhisperDecoder.forward
+// with a KV cache ([tf] modeling_whisper.py:690-795). Every position-dependent quantity is read on
+// the device, so the launch sequence replays as a hipGraph. Row-indexed buffers are addressed with
+// the row offset; the KV caches keep the full-batch layout ([kv][B][H][T][64]).
+void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, hipStream_t st_) {
   const int d = h->d.d_model, S = h->S(), H = h->H(), L = h->d.n_layers, B = c.B, T = c.T;
   const size_t e = esize(h->d.dtype);
   int* ints = h->ints.as<int>();
   int* pos = ints + I_POS;
-  int* next_ids = ints + I_NEXT;
-  float* x = h->dx.as<float>();
-  float* st = h->dstats.as<float>();
-  const int nb = d / 16;
-  embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, x, st, B, d, h->hs);
+  float* x = h->dx.as<float>() + (size_t)b0 * d;
+  const int nbk = d / 16;
+  float* st = h->dstats.as<float>() + (size_t)b0 * nbk * 2;
+  char* dq = (char*)h->dq.p + (size_t)b0 * d * e;
+  char* datt = (char*)h->datt.p + (size_t)b0 * d * e;
+  char* dffn = (char*)h->dffn.p + (size_t)b0 * h->d.ffn * e;
   const size_t cache_l = 2 * (size_t)B * H * T * 64;   // elements per layer (K then V)
   const size_t xkv_l = 2 * (size_t)B * H * S * 64;
   for (int l = 0; l < L; ++l) {
     const LayerW& w = h->dec[l];
-    char* cache = (char*)h->kvself.p + l * cache_l * e;
-    GemmArgs q = rowgemm(x, d, w.qkv_w, B, 3 * d, d, h->dq.p, d);   // LayerNorm fused (f32 A rows)
-    q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nb;
+    char* cache = (char*)h->kvself.p + (l * cache_l + (size_t)b0 * H * T * 64) * e;
+    GemmArgs q = rowgemm(x, d, w.qkv_w, nb, 3 * d, d, dq, d);   // LayerNorm fused (f32 A rows)
+    q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nbk;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
-    gemm(h->dt, q, h->hs);
+    gemm(h->dt, q, st_);
     AttnArgs a;
-    a.q = h->dq.p; a.ldq = d; a.q_Sb = 1; a.Sq = 1;
+    a.q = dq; a.ldq = d; a.q_Sb = 1; a.Sq = 1;
     a.k = cache; a.v = cache + (size_t)B * H * T * 64 * e;
     a.k_sb = (long)H * T * 64; a.k_sh = (long)T * 64; a.k_sk = 64;
-    a.o = h->datt.p; a.ldo = d; a.o_Sb = 1; a.B = B; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1;
-    attention_decode(h->dt, a, h->hs);
-    GemmArgs o = rowgemm(h->datt.p, d, w.o_w, B, d, d, x, d);
-    o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st; o.st_nb = nb;
-    gemm(h->dt, o, h->hs);
+    a.o = datt; a.ldo = d; a.o_Sb = 1; a.B = nb; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1;
+    attention_decode(h->dt, a, st_);
+    GemmArgs o = rowgemm(datt, d, w.o_w, nb, d, d, x, d);
+    o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st; o.st_nb = nbk;
+    gemm(h->dt, o, st_);
     // cross attention over the precomputed encoder K/V
-    GemmArgs xq = rowgemm(x, d, w.xq_w, B, d, d, h->dq.p, d);
-    xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nb;
+    GemmArgs xq = rowgemm(x, d, w.xq_w, nb, d, d, dq, d);
+    xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk;
     xq.bias = w.xq_b;
-    gemm(h->dt, xq, h->hs);
+    gemm(h->dt, xq, st_);
     AttnArgs xa;
-    const char* xkv = (const char*)h->xkv.p + l * xkv_l * e;
-    xa.q = h->dq.p; xa.ldq = d; xa.q_Sb = 1; xa.Sq = 1;
+    const char* xkv = (const char*)h->xkv.p + (l * xkv_l + (size_t)b0 * H * S * 64) * e;
+    xa.q = dq; xa.ldq = d; xa.q_Sb = 1; xa.Sq = 1;
     xa.k = xkv; xa.v = xkv + (size_t)B * H * S * 64 * e;
     xa.k_sb = (long)H * S * 64; xa.k_sh = (long)S * 64; xa.k_sk = 64;
-    xa.o = h->datt.p; xa.ldo = d; xa.o_Sb = 1; xa.B = B; xa.H = H; xa.nkeys = S;
-    attention_decode(h->dt, xa, h->hs);
-    GemmArgs xo = rowgemm(h->datt.p, d, w.xo_w, B, d, d, x, d);
-    xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st; xo.st_nb = nb;
-    gemm(h->dt, xo, h->hs);
+    xa.o = datt; xa.ldo = d; xa.o_Sb = 1; xa.B = nb; xa.H = H; xa.nkeys = S;
+    attention_decode(h->dt, xa, st_);
+    GemmArgs xo = rowgemm(datt, d, w.xo_w, nb, d, d, x, d);
+    xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st; xo.st_nb = nbk;
+    gemm(h->dt, xo, st_);
     // MLP
-    GemmArgs f1 = rowgemm(x, d, w.fc1_w, B, h->d.ffn, d, h->dffn.p, h->d.ffn);
-    f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nb;
+    GemmArgs f1 = rowgemm(x, d, w.fc1_w, nb, h->d.ffn, d, dffn, h->d.ffn);
+    f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nbk;
     f1.bias = w.fc1_b; f1.act = 1;
-    gemm(h->dt, f1, h->hs);
-    GemmArgs f2 = rowgemm(h->dffn.p, h->d.ffn, w.fc2_w, B, d, h->d.ffn, x, d);
-    f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st; f2.st_nb = nb;
-    gemm(h->dt, f2, h->hs);
+    gemm(h->dt, f1, st_);
+    GemmArgs f2 = rowgemm(dffn, h->d.ffn, w.fc2_w, nb, d, h->d.ffn, x, d);
+    f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st; f2.st_nb = nbk;
+    gemm(h->dt, f2, st_);
   }
   if (c.lm_head) {
-    GemmArgs lm = rowgemm(x, d, h->tok_emb, B, h->d.vocab, d, c.logits_out, c.logits_ld);
-    lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b; lm.st_in = st; lm.st_nb = nb;
+    GemmArgs lm = rowgemm(x, d, h->tok_emb, nb, h->d.vocab, d, c.logits_out + (size_t)b0 * c.logits_ld, c.logits_ld);
+    lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b; lm.st_in = st; lm.st_nb = nbk;
     lm.out_f32 = 1;
     if (c.select) {   // argmax partials with the root boost + EOS mask fused into the LM head
-      lm.sel_val = h->part_val.as<float>(); lm.sel_idx = h->part_idx.as<int>();
+      lm.sel_val = h->part_val.as<float>() + (size_t)b0 * h->nchunk;
+      lm.sel_idx = h->part_idx.as<int>() + (size_t)b0 * h->nchunk;
       lm.sel_root_bits = c.bias->root_bits.as<uint32_t>(); lm.sel_lam = c.lam;
       lm.sel_eos = h->d.eos_token_id; lm.sel_step = ints + I_STEP; lm.sel_min_new = c.min_new;
     }
-    gemm(h->dt, lm, h->hs);
+    gemm(h->dt, lm, st_);
+  }
+}
+
+// One decode step for the whole batch: embedding, then the batch split into `h->n_sub` row groups
+// whose layer chains run on separate streams (fork/join events, captured into the same graph) so
+// the latency-bound projections of one group overlap the HBM-bound cross-attention of another;
+// token selection (or teacher forcing) joins them.
+void decode_step(wcb_handle* h, const StepCfg& c) {
+  const int d = h->d.d_model, B = c.B;
+  int* ints = h->ints.as<int>();
+  int* pos = ints + I_POS;
+  int* next_ids = ints + I_NEXT;
+  embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, h->dx.as<float>(), h->dstats.as<float>(), B, d, h->hs);
+  const int ns = std::max(1, std::min(h->n_sub, B));
+  if (ns == 1) {
+    decode_rows(h, c, 0, B, h->hs);
+  } else {
+    HIPCHK(hipEventRecord(h->ev_fork, h->hs));
+    for (int i = 0; i < ns; ++i) {
+      const int b0 = (int)((long)B * i / ns), b1 = (int)((long)B * (i + 1) / ns);
+      HIPCHK(hipStreamWaitEvent(h->sub[i], h->ev_fork, 0));
+      decode_rows(h, c, b0, b1 - b0, h->sub[i]);
+      HIPCHK(hipEventRecord(h->ev_join[i], h->sub[i]));
+    }
+    for (int i = 0; i < ns; ++i) HIPCHK(hipStreamWaitEvent(h->hs, h->ev_join[i], 0));
   }
   if (c.select) {
     SelectArgs s;
@@ -685,7 +729,6 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     advance_forced(next_ids, c.forced, B, c.forced_ld, pos, h->hs);
   }
 }
-
 
 }  // namespace
 
