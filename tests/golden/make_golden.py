@@ -145,7 +145,24 @@ def model_fixture(size, seed, recipe, B, n_tokens, tf_len, beams=True):
           "eager/sdpa enc diff", out["eager_vs_sdpa_enc_maxdiff"])
 
 
+def metric_fixture():
+    """Reference-run transcript dumps (results/*.txt, `Ref :`/`Pred:` format of
+    utils/compute_metric.py:150-153) + the matching JSONL bias_words: data for the metric goldens."""
+    import gzip
+    import json
+    for split, res in (("dev", "refs_and_pred_desc_only.txt"), ("test", "refs_and_pred_baseline_ko_prompt.txt")):
+        raw = open(os.path.join(REF, "results", res), encoding="utf-8").read()
+        jl = os.path.join(REF, "data", "medical-united-syn-med-75-jsonl", f"{split}.jsonl")
+        bw = [json.loads(line).get("bias_words") or [] for line in open(jl, encoding="utf-8")]
+        with gzip.open(os.path.join(HERE, f"metric_{split}.json.gz"), "wt", encoding="utf-8") as f:
+            json.dump({"source_results": f"results/{res}",
+                       "source_bias_words": f"data/medical-united-syn-med-75-jsonl/{split}.jsonl",
+                       "raw_lines": raw, "bias_words": bw}, f)
+    print("metric fixtures written")
+
+
 if __name__ == "__main__":
+    metric_fixture()
     torch.set_num_threads(8)
     mel_fixture()
     model_fixture("micro", 0, "diverse", B=2, n_tokens=32, tf_len=8)

@@ -1,0 +1,506 @@
+// MFMA GEMMs for the encoder stack, the conv stem (implicit im2col), the cross-KV precompute and
+// the decode-step projections / LM head.
+//
+// Replaces the nn.Linear / nn.Conv1d calls of WhisperEncoderLayer / WhisperDecoderLayer /
+// WhisperAttention ([tf] modeling_whisper.py:284-356, 379-413, 448-505, 566-567, 618-624) and the
+// reference LM head `proj_out` (models/whisper_medical.py:19,111).
+//
+// gemm_tile_kernel: BMxBN tile per workgroup, 128-byte K rows (BK = 64 bf16/f16 or 32 f32)
+//   staged HBM → LDS with global_load_lds (16 B per lane, 2 LDS stages), XOR-swizzled on the
+//   SOURCE address so ds_read_b128 fragment reads are conflict-free (chunk ^= (row>>1)&7),
+//   16x16x32 MFMA per wave, epilogue staged through LDS as f32 and written 16 B per lane.
+// gemm_skinny_kernel: M <= 64 rows (decode), 16 output columns per workgroup, K split over the
+//   workgroup's waves, fragments straight from global memory (weights are streamed once), wave
+//   partials reduced through LDS.
+#pragma once
+#include "common.h"
+#include "kernels.h"
+
+#include <cstdio>
+#include <type_traits>
+
+namespace wcb {
+
+WCB_DEV void glds16(const void* gptr, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(gptr, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// 32-bit row arithmetic (M < 2^31); the batched form only for the conv stem
+WCB_DEV long a_row(const GemmArgs& g, int m) {
+  return g.a_Mb ? (long)(m / g.a_Mb) * g.a_strideB + (long)(m % g.a_Mb) * g.lda : (long)m * g.lda;
+}
+WCB_DEV long c_row(const GemmArgs& g, int m) {
+  return g.c_Mb ? (long)(m / g.c_Mb) * g.c_strideB + (long)(m % g.c_Mb) * g.ldc : (long)m * g.ldc;
+}
+
+// Epilogue selection. EPI is a compile-time set of E_* bits for the encoder's fixed shapes
+// (no per-element branches); E_RUNTIME reads the same options from GemmArgs at run time.
+enum : int { E_BIAS = 1, E_GELU = 2, E_RESID = 4, E_F32 = 8, E_ADDROW = 16, E_HEAD = 32, E_RUNTIME = 1 << 30 };
+
+template <int EPI> WCB_DEV bool has(const GemmArgs& g, int bit) {
+  if constexpr (EPI == E_RUNTIME) {
+    switch (bit) {
+      case E_BIAS: return g.bias != nullptr;
+      case E_GELU: return g.act == 1;
+      case E_RESID: return g.resid != nullptr;
+      case E_F32: return g.out_f32 != 0;
+      case E_ADDROW: return g.addrow != nullptr;
+      case E_HEAD: return g.mode == 1;
+      default: return false;
+    }
+  } else {
+    return (EPI & bit) != 0;
+  }
+}
+
+// GELU(erf). f32 ("exact" parity mode) keeps ocml erff; 16-bit modes use a branch-free
+// Abramowitz-Stegun 7.1.26 erfc (|err| <= 1.5e-7 absolute, far below bf16/f16 resolution).
+template <typename T> WCB_DEV float gelu_t(float x) {
+  if constexpr (sizeof(T) == 4) {
+    return gelu_erf(x);
+  } else {
+    const float z = fabsf(x) * 0.70710678118654752f;
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+    float p = fmaf(1.061405429f, t, -1.453152027f);
+    p = fmaf(p, t, 1.421413741f);
+    p = fmaf(p, t, -0.284496736f);
+    p = fmaf(p, t, 0.254829592f);
+    const float q = p * t * __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);   // erfc(|x|/√2)
+    return 0.5f * x * (x >= 0.f ? 2.0f - q : q);
+  }
+}
+
+// Store 8 consecutive output columns n..n+7 of row m (n % 8 == 0, all in one head for E_HEAD).
+template <typename T, int EPI>
+WCB_DEV void epi_store8(const GemmArgs& g, int m, int n, float* v) {
+  if (has<EPI>(g, E_HEAD)) {
+    const int hh = n >> 6, dd = n & 63;
+    const int grp = hh / g.hs_H, h = hh % g.hs_H;
+    const int b = m / g.hs_S, t = m % g.hs_S;
+    const long off = ((((long)grp * g.hs_B + b) * g.hs_H + h) * g.hs_S + t) * 64 + dd;
+    store8<T>(reinterpret_cast<T*>(g.out) + off, v);
+    return;
+  }
+  const long off = c_row(g, m) + n;
+  if (has<EPI>(g, E_RESID)) {
+    const f32x4 r0 = *reinterpret_cast<const f32x4*>(g.resid + off);
+    const f32x4 r1 = *reinterpret_cast<const f32x4*>(g.resid + off + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] += r0[j]; v[j + 4] += r1[j]; }
+  }
+  if (has<EPI>(g, E_F32)) store8<float>(reinterpret_cast<float*>(g.out) + off, v);
+  else store8<T>(reinterpret_cast<T*>(g.out) + off, v);
+}
+
+template <typename T>
+WCB_DEV float epi_store1(const GemmArgs& g, int m, int n, float v) {
+  if (g.mode == 2 && n >= g.n_split) {
+    const int n2 = n - g.n_split;
+    const int hh = n2 >> 6, dd = n2 & 63;
+    const int kv = hh / g.hs_H, h = hh % g.hs_H;
+    const long off = ((((long)kv * g.hs_B + m) * g.hs_H + h) * g.kv_T + *g.pos) * 64 + dd;
+    reinterpret_cast<T*>(g.kv_out)[off] = DT<T>::fromf(v);
+    return v;
+  }
+  if (g.mode == 1) {
+    const int hh = n >> 6, dd = n & 63;
+    const int grp = hh / g.hs_H, h = hh % g.hs_H;
+    const int b = m / g.hs_S, t = m % g.hs_S;
+    const long off = ((((long)grp * g.hs_B + b) * g.hs_H + h) * g.hs_S + t) * 64 + dd;
+    reinterpret_cast<T*>(g.out)[off] = DT<T>::fromf(v);
+    return v;
+  }
+  const long off = c_row(g, m) + n;
+  if (g.resid) v += g.resid[off];
+  if (g.out_f32) reinterpret_cast<float*>(g.out)[off] = v;
+  else reinterpret_cast<T*>(g.out)[off] = DT<T>::fromf(v);
+  return v;
+}
+
+template <typename T, int EPI = E_RUNTIME>
+WCB_DEV float epi_pointwise(const GemmArgs& g, int m, int n, float v) {
+  if (has<EPI>(g, E_BIAS)) v += g.bias[n];
+  if (has<EPI>(g, E_GELU)) v = gelu_t<T>(v);
+  if (has<EPI>(g, E_ADDROW)) v += g.addrow[(long)(g.c_Mb ? m % g.c_Mb : m) * g.N + n];
+  return v;
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(GemmArgs g) {
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int EB = sizeof(T);
+  constexpr int BK = 128 / EB;           // elements per 128-byte LDS row
+  constexpr int CE = 16 / EB;            // elements per 16-byte chunk
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int KSUB = BK / 32;
+  constexpr int STAGE = (BM + BN) * 128;
+  constexpr int IA = BM / 8 / NW, IB = BN / 8 / NW;
+  static_assert(IA * NW * 8 == BM && IB * NW * 8 == BN, "tile rows must split over waves");
+  using Frag = typename DT<T>::frag;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int m0 = (wg / tiles_n) * BM, n0 = (wg % tiles_n) * BN;
+
+  const T* A = reinterpret_cast<const T*>(g.A);
+  const T* W = reinterpret_cast<const T*>(g.W);
+  const T* a_src[IA];
+  const T* b_src[IB];
+#pragma unroll
+  for (int i = 0; i < IA; ++i) {
+    const int r = (wave + i * NW) * 8 + (lane >> 3);
+    const int m = min(m0 + r, g.M - 1);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    a_src[i] = A + a_row(g, m) + c * CE;
+  }
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    const int r = (wave + i * NW) * 8 + (lane >> 3);
+    const long n = min(n0 + r, g.N - 1);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    b_src[i] = W + n * g.ldw + c * CE;
+  }
+  auto stage = [&](int s, int k0) {
+    char* base = smem + s * STAGE;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) glds16(a_src[i] + k0, base + (wave + i * NW) * 1024);
+#pragma unroll
+    for (int i = 0; i < IB; ++i) glds16(b_src[i] + k0, base + BM * 128 + (wave + i * NW) * 1024);
+  };
+  auto lds_frag = [&](const char* base, int r, int ks) -> Frag {
+    if constexpr (EB == 2) {
+      const int c = ks * 4 + (lane >> 4);
+      return *reinterpret_cast<const Frag*>(base + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+    } else {
+      const int c = 2 * (lane >> 4);
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(base + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(base + r * 128 + (((c + 1) ^ ((r >> 1) & 7)) << 4));
+      return Frag{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = g.K / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int s = kt & 1;
+    if (kt + 1 < nk) stage(s ^ 1, (kt + 1) * BK);
+    const char* base = smem + s * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < KSUB; ++ks) {
+      Frag a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = lds_frag(base, wm * TM + i * 16 + (lane & 15), ks);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = lds_frag(base + BM * 128, wn * TN + j * 16 + (lane & 15), ks);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mma16(a[i], b[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: f32 tile through LDS, then 8 columns (16-32 B) per lane per store
+  constexpr int LDC = BN + 4;
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = wn * TN + j * 16 + (lane & 15);
+    const int n = min(n0 + col, g.N - 1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wm * TM + i * 16 + (lane >> 4) * 4 + e;
+        const int m = min(m0 + row, g.M - 1);
+        ct[row * LDC + col] = epi_pointwise<T, EPI>(g, m, n, acc[i][j][e]);
+      }
+  }
+  __syncthreads();
+  constexpr int C8 = BN / 8;
+#pragma unroll 2
+  for (int idx = tid; idx < BM * C8; idx += NT) {
+    const int row = idx / C8, c8 = idx % C8;
+    const int m = m0 + row;
+    const int n = n0 + c8 * 8;
+    if (m >= g.M || n >= g.N) continue;
+    float v[8];
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(ct + row * LDC + c8 * 8);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(ct + row * LDC + c8 * 8 + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = lo[e]; v[e + 4] = hi[e]; }
+    epi_store8<T, EPI>(g, m, n, v);
+  }
+}
+
+// Skinny GEMM for the decode step (M = batch <= 64 rows): one workgroup = NF·16 output columns,
+// its NW waves split K into NW contiguous ranges of KS 32-deep MFMA steps, every load of a wave is
+// issued up front (weights are streamed once from HBM, activations come from L2), partial tiles
+// are summed through LDS.
+//  * LN: the A operand is the f32 residual stream, normalised on the fly (the decoder's pre-block
+//    LayerNorm fused into the projection that consumes it). Row statistics come from the
+//    deterministic per-16-column partial sums (Σx, Σx²) the producer of x wrote (st_in).
+//  * st_out: a residual-writing GEMM (NF = 1) publishes those partial sums of the new x rows.
+//  * sel_val: the LM head reduces its logits tile to a per-row (max, argmax) partial with the
+//    bias-list root boost and the EOS mask applied (k_select.hip finishes the reduction).
+template <typename T, int MF, int NF, int NW, int KS, bool LN>
+__global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
+  using Frag = typename DT<T>::frag;
+  constexpr int NT = NW * 64, BNC = NF * 16;
+  // LDS slabs for the cross-wave K reduction: as many as fit in 48 KB, extra waves accumulate in rounds
+  constexpr int SLAB = MF * 16 * (BNC + 1) * 4;
+  constexpr int SL = (NW * SLAB <= 49152) ? NW : (NW / 2 * SLAB <= 49152) ? NW / 2 : (NW / 4 * SLAB <= 49152) ? NW / 4 : 1;
+  __shared__ __attribute__((aligned(16))) float red[SL][MF * 16][BNC + 1];
+  __shared__ float st_mean[MF * 16], st_rstd[MF * 16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // LN statistics partials first: the oldest loads retire first (in-order vmcnt), so the row
+  // statistics are ready while the weight stream is still in flight
+  constexpr int NB = NW * KS * 2;                          // 16-column blocks per row (K / 16)
+  constexpr int TPR = NB % 16 == 0 ? 16 : NB % 8 == 0 ? 8 : NB % 4 == 0 ? 4 : NB % 2 == 0 ? 2 : 1;
+  constexpr int RPP = NT / TPR;                            // rows per pass
+  constexpr int PASSES = (MF * 16 + RPP - 1) / RPP;
+  float s1[PASSES], s2[PASSES];
+  if constexpr (LN) {
+#pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+      const int m = min(ps * RPP + tid / TPR, g.M - 1);
+      s1[ps] = 0.f;
+      s2[ps] = 0.f;
+      float2 pv[NB / TPR];
+#pragma unroll
+      for (int j = 0; j < NB / TPR; ++j)
+        pv[j] = *reinterpret_cast<const float2*>(g.st_in + ((long)m * NB + j * TPR + tid % TPR) * 2);
+#pragma unroll
+      for (int j = 0; j < NB / TPR; ++j) { s1[ps] += pv[j].x; s2[ps] += pv[j].y; }
+    }
+  }
+  const int n0 = blockIdx.x * BNC;
+  const int kb = wave * (KS * 32) + 8 * (lane >> 4);
+  Frag b[NF][KS];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const long n = min(n0 + j * 16 + (lane & 15), g.N - 1);
+    const T* W = reinterpret_cast<const T*>(g.W) + n * g.ldw + kb;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) b[j][ks] = load_frag<T>(W + ks * 32);
+  }
+  f32x4 acc[MF][NF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (LN) {
+    const float* X = reinterpret_cast<const float*>(g.A);
+    float xv[MF][KS][8];
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const int m = min(i * 16 + (lane & 15), g.M - 1);
+      const float* xr = X + a_row(g, m) + kb;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(xr + ks * 32);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(xr + ks * 32 + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { xv[i][ks][e] = x0[e]; xv[i][ks][e + 4] = x1[e]; }
+      }
+    }
+    float gw[KS][8], gb[KS][8];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(g.ln_w + kb + ks * 32);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(g.ln_w + kb + ks * 32 + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(g.ln_b + kb + ks * 32);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(g.ln_b + kb + ks * 32 + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { gw[ks][e] = w0[e]; gw[ks][e + 4] = w1[e]; gb[ks][e] = b0[e]; gb[ks][e + 4] = b1[e]; }
+    }
+    // row statistics: TPR threads per row, fixed-order sums of the producer's partials
+#pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+      float a1 = s1[ps], a2 = s2[ps];
+#pragma unroll
+      for (int o = 1; o < TPR; o <<= 1) { a1 += __shfl_xor(a1, o, 64); a2 += __shfl_xor(a2, o, 64); }
+      const int r = ps * RPP + tid / TPR;
+      if (tid % TPR == 0 && r < MF * 16) {
+        const float mean = a1 / g.K;
+        st_mean[r] = mean;
+        st_rstd[r] = rsqrtf(fmaxf(a2 / g.K - mean * mean, 0.f) + 1e-5f);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const float mean = st_mean[i * 16 + (lane & 15)], rstd = st_rstd[i * 16 + (lane & 15)];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        Frag a;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = (xv[i][ks][e] - mean) * rstd * gw[ks][e] + gb[ks][e];
+          if constexpr (sizeof(T) == 4) a[e] = v;
+          else a[e] = __builtin_bit_cast(typename std::remove_reference<decltype(a[0])>::type, DT<T>::fromf(v));
+        }
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = mma16(a, b[j][ks], acc[i][j]);
+      }
+    }
+  } else {
+    const T* A = reinterpret_cast<const T*>(g.A);
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const int m = min(i * 16 + (lane & 15), g.M - 1);
+      const T* ap = A + a_row(g, m) + kb;
+      Frag a[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) a[ks] = load_frag<T>(ap + ks * 32);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = mma16(a[ks], b[j][ks], acc[i][j]);
+    }
+  }
+#pragma unroll
+  for (int round = 0; round < NW / SL; ++round) {
+    if (wave / SL == round) {
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float& r = red[wave % SL][i * 16 + (lane >> 4) * 4 + e][j * 16 + (lane & 15)];
+            r = round == 0 ? acc[i][j][e] : r + acc[i][j][e];
+          }
+    }
+    __syncthreads();
+  }
+  const bool mask_eos = g.sel_val && *g.sel_step < g.sel_min_new;
+  // epilogue: thread → (row, col) with the columns of a row contiguous in the wave, so row-wise
+  // reductions (stats partials: 16 lanes; argmax partial: BNC lanes) are shuffles
+  for (int t0 = 0; t0 < MF * 16 * BNC; t0 += NT) {
+    const int t = t0 + tid;
+    const int row = t / BNC, col = t % BNC;
+    const int nn = n0 + col;
+    const bool valid = t < MF * 16 * BNC && row < g.M && nn < g.N;
+    float v = 0.f;
+    if (valid) {
+#pragma unroll
+      for (int w = 0; w < SL; ++w) v += red[w][row][col];
+      v = epi_pointwise<T>(g, row, nn, v);
+      v = epi_store1<T>(g, row, nn, v);
+    }
+    if (g.st_out) {   // NF == 1: 16 contiguous lanes hold one row of the block
+      float s1 = valid ? v : 0.f, s2 = valid ? v * v : 0.f;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      if (valid && (t & 15) == 0) {
+        float* p = g.st_out + ((long)row * g.st_nb + blockIdx.x) * 2;
+        p[0] = s1;
+        p[1] = s2;
+      }
+    }
+    if (g.sel_val) {  // BNC == 64: one wave per row
+      float x = -INFINITY;
+      int xi = 0x7fffffff;
+      if (valid) {
+        x = v;
+        if (g.sel_lam != 0.f && ((g.sel_root_bits[nn >> 5] >> (nn & 31)) & 1u)) x += g.sel_lam;
+        if (mask_eos && nn == g.sel_eos) x = -INFINITY;
+        xi = nn;
+      }
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float ov = __shfl_xor(x, o, 64);
+        const int oi = __shfl_xor(xi, o, 64);
+        if (ov > x || (ov == x && oi < xi)) { x = ov; xi = oi; }
+      }
+      if (lane == 0 && row < g.M) {
+        g.sel_val[(long)row * gridDim.x + blockIdx.x] = x;
+        g.sel_idx[(long)row * gridDim.x + blockIdx.x] = xi;
+      }
+    }
+  }
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int EPI>
+static void launch_tile_e(const GemmArgs& g, hipStream_t s) {
+  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  constexpr int stage_bytes = 2 * (BM + BN) * 128;
+  constexpr int epi_bytes = BM * (BN + 4) * 4;
+  constexpr int lds = stage_bytes > epi_bytes ? stage_bytes : epi_bytes;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_tile_kernel<T, BM, BN, WM, WN, EPI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemm_tile_kernel<T, BM, BN, WM, WN, EPI>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+static void launch_tile(const GemmArgs& g, hipStream_t s) {
+  const int bits = (g.bias ? E_BIAS : 0) | (g.act == 1 ? E_GELU : 0) | (g.resid ? E_RESID : 0) |
+                   (g.out_f32 ? E_F32 : 0) | (g.addrow ? E_ADDROW : 0) | (g.mode == 1 ? E_HEAD : 0);
+  switch (bits) {   // the encoder's epilogues, specialised; anything else takes the run-time form
+    case E_BIAS: launch_tile_e<T, BM, BN, WM, WN, E_BIAS>(g, s); break;                                   // QKV
+    case E_BIAS | E_GELU: launch_tile_e<T, BM, BN, WM, WN, E_BIAS | E_GELU>(g, s); break;                 // fc1, conv1
+    case E_BIAS | E_RESID | E_F32: launch_tile_e<T, BM, BN, WM, WN, E_BIAS | E_RESID | E_F32>(g, s); break;  // out, fc2
+    case E_BIAS | E_GELU | E_F32 | E_ADDROW:
+      launch_tile_e<T, BM, BN, WM, WN, E_BIAS | E_GELU | E_F32 | E_ADDROW>(g, s); break;                  // conv2
+    case E_BIAS | E_HEAD: launch_tile_e<T, BM, BN, WM, WN, E_BIAS | E_HEAD>(g, s); break;                 // cross K/V
+    default: launch_tile_e<T, BM, BN, WM, WN, E_RUNTIME>(g, s); break;
+  }
+}
+
+template <typename T, int MF, int NF, int NW, int KS>
+static void launch_skinny_k(const GemmArgs& g, hipStream_t s) {
+  const int grid = (g.N + NF * 16 - 1) / (NF * 16);
+  if (g.ln_w) hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NF, NW, KS, true>), dim3(grid), dim3(NW * 64), 0, s, g);
+  else hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NF, NW, KS, false>), dim3(grid), dim3(NW * 64), 0, s, g);
+}
+
+// K = NW waves x KS steps x 32: pick the wave count first, then the (compile-time) steps per wave.
+template <typename T, int MF, int NF>
+static bool launch_skinny_mf(const GemmArgs& g, hipStream_t s) {
+  const int K = g.K;
+#define WCB_SK(nw, ks) if (K == nw * ks * 32) { launch_skinny_k<T, MF, NF, nw, ks>(g, s); return true; }
+  WCB_SK(1, 1) WCB_SK(1, 2) WCB_SK(2, 2) WCB_SK(4, 2) WCB_SK(4, 3) WCB_SK(4, 4) WCB_SK(8, 2)
+  WCB_SK(8, 3) WCB_SK(8, 4) WCB_SK(8, 5) WCB_SK(8, 6) WCB_SK(16, 4) WCB_SK(16, 5) WCB_SK(16, 6)
+  WCB_SK(16, 8) WCB_SK(16, 10) WCB_SK(16, 12)
+#undef WCB_SK
+  return false;
+}
+
+template <typename T>
+static void gemm_t(const GemmArgs& g, hipStream_t s) {
+  if (g.M <= 64 || g.mode == 2 || g.ln_w) {
+    bool ok;
+    if (g.sel_val) {   // LM head: 64 columns per workgroup (A re-read 4x less), fused argmax partial
+      if (g.M <= 16) ok = launch_skinny_mf<T, 1, 4>(g, s);
+      else if (g.M <= 32) ok = launch_skinny_mf<T, 2, 4>(g, s);
+      else ok = launch_skinny_mf<T, 4, 4>(g, s);
+    } else if (g.M <= 16) ok = launch_skinny_mf<T, 1, 1>(g, s);
+    else if (g.M <= 32) ok = launch_skinny_mf<T, 2, 1>(g, s);
+    else ok = launch_skinny_mf<T, 4, 1>(g, s);
+    if (!ok) fprintf(stderr, "wcb: no skinny GEMM instance for K=%d\n", g.K);
+    return;
+  }
+  // Tile choice: 128x128 (4 waves 2x2) when N fills it, else 128x64.
+  if (g.N % 128 == 0) launch_tile<T, 128, 128, 2, 2>(g, s);
+  else launch_tile<T, 128, 64, 2, 2>(g, s);
+}
+
+}  // namespace wcb
