@@ -78,6 +78,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="serialise batches (default: batch i+1's front end + encoder overlap batch i's decode)")
     args = ap.parse_args()
 
     import torch
@@ -127,16 +129,23 @@ def main():
     bias = model.bias_list(phrases)
     use_graph = not args.no_graph
 
+    overlap = not args.no_overlap
+    keep = []   # async mode: inputs/outputs stay alive until the final synchronize
+
     def step():
         mel = model.log_mel(pcm)
-        return model.generate(mel, max_length=args.new_tokens, min_new_tokens=args.new_tokens,
-                              bias_list=phrases, bias_boost=args.boost, use_graph=use_graph)
+        ids = model.generate(mel, max_length=args.new_tokens, min_new_tokens=args.new_tokens,
+                             bias_list=phrases, bias_boost=args.boost, use_graph=use_graph, block=not overlap)
+        keep.append((mel, ids))
+        return ids
 
     for i in range(args.warmup):
         ids = step()
+        model.synchronize()
         torch.cuda.synchronize()
         log(f"warmup {i} done, ids {tuple(ids.shape)}")
     assert ids.shape == (B, args.new_tokens)
+    keep.clear()
     if not args.no_profile:
         model.profile_enable(True)
     if world > 1:
@@ -145,6 +154,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step()
+    model.synchronize()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -186,7 +196,7 @@ def main():
             "config": {"workload": f"C2: whisper-{args.model}, {B} clips/GPU x 30 s, log-mel + encoder + "
                                    f"{args.new_tokens}-token greedy decode, {args.bias_phrases}-phrase bias boost "
                                    f"lambda={args.boost}", "global_batch": world * B, "parallelism": f"utterance-dp{world}",
-                       "hipgraph_decode": use_graph},
+                       "hipgraph_decode": use_graph, "batches_in_flight": 2 if overlap else 1},
             "rtf": round(1.0 / (value / world), 6),
             "roofline": roof,
             "phases": phases,

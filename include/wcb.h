@@ -48,6 +48,8 @@ typedef struct {
   int num_beams;        /* 1 = greedy (the reference eval setting) */
   float bias_boost;     /* lambda >= 0 of the bias-list boost; 0 = plain greedy bit-for-bit */
   int use_graph;        /* replay the decode step as a captured hipGraph */
+  int async_out;        /* 1: do not make `stream` wait for the decode; outputs valid after
+                           wcb_synchronize (lets the next call's front end + encoder overlap it) */
 } wcb_gen_cfg;
 
 /* replaces WhisperForConditionalGenerationWeightCE(config) (models/whisper_medical.py:16-22) */
@@ -76,12 +78,17 @@ int wcb_encode(wcb_handle* h, const float* mel, int B, void* enc_out, void* stre
 /* replaces model.generate(input_features, max_length=...) as called by
  * [tf] trainer_seq2seq.py:329: greedy from [decoder_start] (+ optional prefix), bias boost,
  * out_ids int32 DEVICE [B][cfg->max_new_tokens] (finished rows padded with pad_token_id),
- * *out_steps = number of generated columns (all rows finished or max_new_tokens). */
+ * *out_steps = number of generated columns (all rows finished or max_new_tokens).
+ * The front end/encoder run on one library stream and the decode on another, with two cross-K/V
+ * buffers: call i+1's encoder overlaps call i's decode (async_out = 1 keeps `stream` free). */
 int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg, const wcb_bias* bias,
                  const int32_t* prefix, int prefix_len, int32_t* out_ids, int32_t* out_steps, void* stream);
 
 /* replaces forward(input_features, decoder_input_ids) (models/whisper_medical.py:45-111):
  * dec_ids int32 DEVICE [B][T] → logits f32 DEVICE [B][T][vocab]; enc_out as in wcb_encode. */
+/* wait for every queued front-end / encoder / decode operation of the handle */
+int wcb_synchronize(wcb_handle* h);
+
 int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, int T, float* logits,
                 void* enc_out, void* stream);
 
@@ -116,7 +123,8 @@ int wcb_op_gemm_ln(int dtype, const float* X, const float* ln_w, const float* ln
 int wcb_op_layernorm(int dtype, const float* x, const float* w, const float* b, void* y, int M, int d,
                      void* stream);
 /* o[B][Sq][H*64] = softmax(q kᵀ) v per head (q pre-scaled), k/v [B][Sk][H*64];
- * flash=1 selects the MFMA kernel (16-bit dtypes). */
+ * flash=1 selects the MFMA kernel (16-bit dtypes); 0 the decode kernel; n >= 2 the decode kernel with
+ * n split-KV key chunks combined by the last-arriving chunk. */
 int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H, int Sq,
                      int Sk, int flash, void* stream);
 

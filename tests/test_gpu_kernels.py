@@ -135,16 +135,19 @@ def test_flash_attention_spike():
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f32"])
-@pytest.mark.parametrize("Sq,Sk", [(1, 1500), (3, 700), (1, 1), (5, 33)])
-def test_decode_attention(dt, Sq, Sk):
+@pytest.mark.parametrize("Sq,Sk,split", [(1, 1500, 0), (3, 700, 0), (1, 1, 0), (5, 33, 0), (1, 1500, 4), (2, 1500, 3),
+                                         (1, 5, 4), (1, 2, 4)])
+def test_decode_attention(dt, Sq, Sk, split):
     g = torch.Generator(device="cpu").manual_seed(Sq * 1000 + Sk)
     B, H = 3, 2
     q = (torch.randn(B, Sq, H * 64, generator=g) * 0.3).to(DT[dt][0]).cuda()
     k = torch.randn(B, Sk, H * 64, generator=g).to(DT[dt][0]).cuda()
     v = torch.randn(B, Sk, H * 64, generator=g).to(DT[dt][0]).cuda()
-    o = _attn(dt, q, k, v, False)
+    o = _attn(dt, q, k, v, split)
     tol = 1e-5 if dt == "f32" else 1e-2
     assert (o.double() - _attn_ref(q, k, v)).abs().max().item() < tol
+    if split:   # tickets were reset: a second call combines again, bit-identically
+        assert torch.equal(_attn(dt, q, k, v, split), o)
 
 
 @pytest.mark.parametrize("n_mel", [80, 128])

@@ -25,7 +25,7 @@ class WcbModelDesc(C.Structure):
 
 class WcbGenCfg(C.Structure):
     _fields_ = [("max_new_tokens", C.c_int), ("min_new_tokens", C.c_int), ("num_beams", C.c_int),
-                ("bias_boost", C.c_float), ("use_graph", C.c_int)]
+                ("bias_boost", C.c_float), ("use_graph", C.c_int), ("async_out", C.c_int)]
 
 
 # name -> (restype, argtypes)
@@ -40,6 +40,7 @@ SIGNATURES = {
     "wcb_encode": (C.c_int, [_P, _P, C.c_int, _P, _P]),
     "wcb_generate": (C.c_int, [_P, _P, C.c_int, C.POINTER(WcbGenCfg), _P, _P, C.c_int, _P,
                                C.POINTER(C.c_int32), _P]),
+    "wcb_synchronize": (C.c_int, [_P]),
     "wcb_forward": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, _P, _P, _P]),
     "wcb_bias_create": (C.c_int, [_P, _P, _P, C.c_int, C.POINTER(_P)]),
     "wcb_bias_destroy": (None, [_P]),

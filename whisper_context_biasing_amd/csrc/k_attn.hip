@@ -20,36 +20,50 @@ namespace wcb {
 
 constexpr int kMaxKeys = 2048;
 
+// Split-KV: workgroup (i·nsplit + c, b·H + h) handles key chunk c. With nsplit > 1 each chunk
+// publishes (max, Σexp, Σexp·v[64]) with write-through (sc1) stores, drains them (vmcnt(0)) and takes
+// an agent-scope ticket; the chunk that draws the last ticket reads every partial with sc1 loads,
+// combines them in chunk order (deterministic) and resets the ticket (cdna_hip_programming.md §6
+// Guideline 16, first row of the measured hand-off table).
 template <typename T, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(AttnArgs a) {
   __shared__ float sc[kMaxKeys];
   __shared__ float red[NW][64 + 1];
   __shared__ float stat[2];
-  const int i = blockIdx.x, bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int nsplit = a.nsplit > 0 ? a.nsplit : 1;
+  const int i = blockIdx.x / nsplit, chunk = blockIdx.x % nsplit;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int seg = lane & 7, kg = lane >> 3;
-  const int nk = a.nkeys_dev ? (*a.nkeys_dev + a.nkeys_add) : a.nkeys;
+  const int nk_all = a.nkeys_dev ? (*a.nkeys_dev + a.nkeys_add) : a.nkeys;
+  const int per = (nk_all + nsplit - 1) / nsplit;
+  const int j_lo = chunk * per, j_hi = min(nk_all, j_lo + per);
+  const int nk = max(j_hi - j_lo, 0);
   const T* q = reinterpret_cast<const T*>(a.q) + ((long)b * a.q_Sb + i) * a.ldq + h * 64;
-  const T* kb = reinterpret_cast<const T*>(a.k) + (long)b * a.k_sb + (long)h * a.k_sh + seg * 8;
-  const T* vb = reinterpret_cast<const T*>(a.v) + (long)b * a.k_sb + (long)h * a.k_sh + seg * 8;
+  const T* kb = reinterpret_cast<const T*>(a.k) + (long)b * a.k_sb + (long)h * a.k_sh + (long)j_lo * a.k_sk + seg * 8;
+  const T* vb = reinterpret_cast<const T*>(a.v) + (long)b * a.k_sb + (long)h * a.k_sh + (long)j_lo * a.k_sk + seg * 8;
   float qv[8];
   load8f<T>(q + seg * 8, qv);
 
-  // pass 1: scores (8 keys per wave-instruction, 8 lanes per key)
+  // pass 1: scores. 8 lanes per key (16 B each), U keys per lane in flight (memory-level
+  // parallelism: the K/V stream is the HBM-bound part of the decode step)
+  constexpr int U = 8;
+  constexpr int WSPAN = 8 * U, GSPAN = NW * WSPAN;
   float mx = -INFINITY;
-  constexpr int STEP = NW * 8;
-  for (int j0 = wave * 8; j0 < nk; j0 += STEP * 2) {
-    float kv0[8], kv1[8];
-    const int ja = j0 + kg, jb = j0 + STEP + kg;
-    load8f<T>(kb + (long)min(ja, nk - 1) * a.k_sk, kv0);
-    load8f<T>(kb + (long)min(jb, nk - 1) * a.k_sk, kv1);
-    float d0 = 0.f, d1 = 0.f;
+  for (int j0 = wave * WSPAN; j0 < nk; j0 += GSPAN) {
+    float kv[U][8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { d0 = fmaf(qv[e], kv0[e], d0); d1 = fmaf(qv[e], kv1[e], d1); }
+    for (int u = 0; u < U; ++u) load8f<T>(kb + (long)min(j0 + u * 8 + kg, nk - 1) * a.k_sk, kv[u]);
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1) { d0 += __shfl_xor(d0, o, 64); d1 += __shfl_xor(d1, o, 64); }
-    if (ja < nk) { if (seg == 0) sc[ja] = d0; mx = fmaxf(mx, d0); }
-    if (jb < nk) { if (seg == 0) sc[jb] = d1; mx = fmaxf(mx, d1); }
+    for (int u = 0; u < U; ++u) {
+      float dsum = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dsum = fmaf(qv[e], kv[u][e], dsum);
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) dsum += __shfl_xor(dsum, o, 64);
+      const int j = j0 + u * 8 + kg;
+      if (j < nk) { if (seg == 0) sc[j] = dsum; mx = fmaxf(mx, dsum); }
+    }
   }
   mx = wave_max(mx);
   if (lane == 0) red[wave][0] = mx;
@@ -79,14 +93,17 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(AttnArgs a) {
   }
   // pass 3: o = P·V
   float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int j0 = wave * 8; j0 < nk; j0 += STEP * 2) {
-    float v0[8], v1[8];
-    const int ja = j0 + kg, jb = j0 + STEP + kg;
-    load8f<T>(vb + (long)min(ja, nk - 1) * a.k_sk, v0);
-    load8f<T>(vb + (long)min(jb, nk - 1) * a.k_sk, v1);
-    const float pa = ja < nk ? sc[ja] : 0.f, pb = jb < nk ? sc[jb] : 0.f;
+  for (int j0 = wave * WSPAN; j0 < nk; j0 += GSPAN) {
+    float vv[U][8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = fmaf(pa, v0[e], fmaf(pb, v1[e], o[e]));
+    for (int u = 0; u < U; ++u) load8f<T>(vb + (long)min(j0 + u * 8 + kg, nk - 1) * a.k_sk, vv[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * 8 + kg;
+      const float p = j < nk ? sc[j] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = fmaf(p, vv[u][e], o[e]);
+    }
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -99,21 +116,56 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(AttnArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) red[wave][seg * 8 + e] = o[e];
   __syncthreads();
-  if (tid < 64) {
-    float acc = 0.f;
-    for (int w = 0; w < NW; ++w) acc += red[w][tid];
-    acc /= stat[1];
-    T* out = reinterpret_cast<T*>(a.o) + ((long)b * a.o_Sb + i) * a.ldo + h * 64;
-    out[tid] = DT<T>::fromf(acc);
+  if (wave != 0) return;
+  float acc = 0.f;
+  for (int w = 0; w < NW; ++w) acc += red[w][lane];
+  T* out = reinterpret_cast<T*>(a.o) + ((long)b * a.o_Sb + i) * a.ldo + h * 64;
+  if (nsplit == 1) {
+    out[lane] = DT<T>::fromf(acc / stat[1]);
+    return;
   }
+  // ---- split-KV hand-off: publish this chunk's partial, last arriver combines
+  const long slot = ((long)bh * a.Sq + i);
+  float* part = a.part + slot * nsplit * 66;
+  float* mine = part + chunk * 66;
+  __hip_atomic_store(mine + 2 + lane, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) {
+    __hip_atomic_store(mine, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(mine + 1, stat[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int old = 0;
+  if (lane == 0) old = atomicAdd(a.ticket + slot, 1);
+  old = __shfl(old, 0, 64);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (old != nsplit - 1) return;
+  float M = -INFINITY;
+  for (int c = 0; c < nsplit; ++c) {
+    const float mc = __hip_atomic_load(part + c * 66, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (mc > M) M = mc;
+  }
+  float L = 0.f, O = 0.f;
+  for (int c = 0; c < nsplit; ++c) {
+    const float mc = __hip_atomic_load(part + c * 66, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float lc = __hip_atomic_load(part + c * 66 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float oc = __hip_atomic_load(part + c * 66 + 2 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float w = lc > 0.f ? __expf(mc - M) : 0.f;    // empty chunks publish l = 0
+    L += lc * w;
+    O += oc * w;
+  }
+  out[lane] = DT<T>::fromf(O / L);
+  if (lane == 0) __hip_atomic_store(a.ticket + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 void attention_decode(DType t, const AttnArgs& a, hipStream_t s) {
-  const dim3 grid(a.Sq, a.B * a.H);
+  const int ns = (a.part && a.ticket && a.nsplit > 1) ? a.nsplit : 1;
+  AttnArgs b = a;
+  b.nsplit = ns;
+  const dim3 grid(a.Sq * ns, a.B * a.H);
   switch (t) {
-    case kBF16: hipLaunchKernelGGL((attn_decode_kernel<bf16_t, 8>), grid, dim3(512), 0, s, a); break;
-    case kF16: hipLaunchKernelGGL((attn_decode_kernel<f16_t, 8>), grid, dim3(512), 0, s, a); break;
-    case kF32: hipLaunchKernelGGL((attn_decode_kernel<float, 8>), grid, dim3(512), 0, s, a); break;
+    case kBF16: hipLaunchKernelGGL((attn_decode_kernel<bf16_t, 8>), grid, dim3(512), 0, s, b); break;
+    case kF16: hipLaunchKernelGGL((attn_decode_kernel<f16_t, 8>), grid, dim3(512), 0, s, b); break;
+    case kF32: hipLaunchKernelGGL((attn_decode_kernel<float, 8>), grid, dim3(512), 0, s, b); break;
   }
 }
 

@@ -55,6 +55,9 @@ struct AttnArgs {
   void* o = nullptr; long ldo = 0; long o_Sb = 0;
   int B = 0, H = 0;
   int nkeys = 0; const int* nkeys_dev = nullptr; int nkeys_add = 0;
+  // split-KV (decode): nsplit key chunks per query row, partials [B·H·Sq][nsplit][66] f32, tickets
+  // [B·H·Sq] int (zero-initialised; the combining chunk resets its ticket)
+  int nsplit = 1; float* part = nullptr; int* ticket = nullptr;
 };
 void attention_decode(DType t, const AttnArgs& a, hipStream_t s);   // VALU, any T, any Sq
 bool attention_flash(DType t, const AttnArgs& a, hipStream_t s);    // MFMA encoder (16-bit T)

@@ -46,6 +46,7 @@ struct WcbError : std::runtime_error {
   } while (0)
 
 constexpr int kFrames = 3000, kNCol = 416, kNSamp = 480000;
+constexpr int kXSplit = 4;   // cross-attention key chunks per (row, head): 1500 keys → 4 × 375
 
 int esize(int dt) { return dt == WCB_F32 ? 4 : 2; }
 
@@ -120,7 +121,10 @@ struct wcb_handle {
   DType dt = kBF16;
   int device = 0;
   std::string err;
-  hipStream_t hs = nullptr;
+  hipStream_t hs = nullptr;   // decode stream
+  hipStream_t he = nullptr;   // front end + encoder + cross-K/V stream (overlaps the previous batch's decode)
+  hipEvent_t ev_xkv[2] = {}, ev_dec[2] = {};   // cross-K/V buffer k written / decode reading it done
+  int gen_count = 0;
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr;
   static constexpr int kMaxSub = 4;
   hipStream_t sub[kMaxSub] = {};
@@ -145,11 +149,11 @@ struct wcb_handle {
   DevBuf xt, hbuf, x, h, qkv, att, ffn, encout;
   // decoder workspace
   int dec_B = 0, dec_T = 0;
-  DevBuf xkv, kvself, dx, dh, dq, datt, dffn, dstats, logits, part_val, part_idx, ints, outbuf, forced;
+  DevBuf xkv2[2], kvself, dx, dh, dq, datt, dffn, dstats, xpart, xticket, logits, part_val, part_idx, ints, outbuf, forced;
   int nchunk = 64;
   // graph cache
-  hipGraphExec_t gexec = nullptr;
-  std::string gkey;
+  hipGraphExec_t gexec[2] = {};   // one captured decode step per cross-K/V buffer
+  std::string gkey[2];
   // default (empty) bias automaton
   std::unique_ptr<wcb_bias> empty_bias;
   // profiling
@@ -203,13 +207,13 @@ struct wcb_handle {
     return e;
   }
   template <typename F>
-  void timed(const char* name, double flops, double bytes, F&& f) {
+  void timed(const char* name, double flops, double bytes, hipStream_t st, F&& f) {
     if (!prof) { f(); return; }
     const int id = prof_id(name);
     hipEvent_t a = get_ev(), b = get_ev();
-    HIPCHK(hipEventRecord(a, hs));
+    HIPCHK(hipEventRecord(a, st));
     f();
-    HIPCHK(hipEventRecord(b, hs));
+    HIPCHK(hipEventRecord(b, st));
     prof_e[id].launches += 1;
     prof_e[id].flops += flops;
     prof_e[id].bytes += bytes;
@@ -292,6 +296,11 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     h->dt = DType(desc->dtype);
     h->device = device;
     HIPCHK(hipStreamCreateWithFlags(&h->hs, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&h->he, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) {
+      HIPCHK(hipEventCreateWithFlags(&h->ev_xkv[i], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&h->ev_dec[i], hipEventDisableTiming));
+    }
     HIPCHK(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
@@ -352,10 +361,10 @@ void wcb_destroy(wcb_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
-  if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+  for (auto& g : h->gexec) if (g) (void)hipGraphExecDestroy(g);
   for (auto& b : h->owned) b.release();
   for (DevBuf* b : {&h->dft, &h->mel_lo, &h->mel_hi, &h->mel_w, &h->clip_max, &h->xt, &h->hbuf, &h->x, &h->h,
-                    &h->qkv, &h->att, &h->ffn, &h->encout, &h->xkv, &h->kvself, &h->dx, &h->dh, &h->dq,
+                    &h->qkv, &h->att, &h->ffn, &h->encout, &h->xkv2[0], &h->xkv2[1], &h->kvself, &h->dx, &h->dh, &h->dq,
                     &h->datt, &h->dffn, &h->logits, &h->part_val, &h->part_idx, &h->ints, &h->outbuf, &h->forced})
     b->release();
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
@@ -367,6 +376,11 @@ void wcb_destroy(wcb_handle* h) {
     if (h->sub[i]) (void)hipStreamDestroy(h->sub[i]);
   }
   if (h->hs) (void)hipStreamDestroy(h->hs);
+  if (h->he) (void)hipStreamDestroy(h->he);
+  for (int i = 0; i < 2; ++i) {
+    if (h->ev_xkv[i]) (void)hipEventDestroy(h->ev_xkv[i]);
+    if (h->ev_dec[i]) (void)hipEventDestroy(h->ev_dec[i]);
+  }
   delete h;
 }
 
@@ -481,19 +495,27 @@ int wcb_finalize_weights(wcb_handle* h) {
 // ============================================================================== pipelines
 namespace {
 
-void sync_in(wcb_handle* h, void* stream) {
+// caller stream → library stream `to` (inputs ready)
+void sync_in(wcb_handle* h, void* stream, hipStream_t to) {
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipEventRecord(h->ev_in, (hipStream_t)stream));
-  HIPCHK(hipStreamWaitEvent(h->hs, h->ev_in, 0));
+  HIPCHK(hipStreamWaitEvent(to, h->ev_in, 0));
 }
-void sync_out(wcb_handle* h, void* stream) {
-  HIPCHK(hipEventRecord(h->ev_out, h->hs));
+// library stream `from` → caller stream (outputs ready)
+void sync_out(wcb_handle* h, void* stream, hipStream_t from) {
+  HIPCHK(hipEventRecord(h->ev_out, from));
   HIPCHK(hipStreamWaitEvent((hipStream_t)stream, h->ev_out, 0));
   HIPCHK(hipGetLastError());
+}
+// drain both library streams (before any workspace reallocation)
+void quiesce(wcb_handle* h) {
+  HIPCHK(hipStreamSynchronize(h->he));
+  HIPCHK(hipStreamSynchronize(h->hs));
 }
 
 void ensure_enc_ws(wcb_handle* h, int B) {
   if (B <= h->enc_B) return;
+  quiesce(h);
   const size_t e = esize(h->d.dtype), d = h->d.d_model, S = h->S(), M = (size_t)B * S;
   h->xt.ensure(((size_t)B * (kFrames + 2) * h->d.n_mel + 256) * e);
   h->hbuf.ensure(((size_t)B * (kFrames + 1) * d + 256) * e);
@@ -514,7 +536,7 @@ GemmArgs rowgemm(const void* A, long lda, const void* W, int M, int N, int K, vo
 }
 
 void run_gemm(wcb_handle* h, const char* cls, const GemmArgs& g) {
-  h->timed(cls, 2.0 * g.M * g.N * g.K, 0.0, [&] { gemm(h->dt, g, h->hs); });
+  h->timed(cls, 2.0 * g.M * g.N * g.K, 0.0, h->he, [&] { gemm(h->dt, g, h->he); });
 }
 
 // WhisperEncoder.forward ([tf] modeling_whisper.py:592-646) on mel f32 [B][n_mel][3000]
@@ -524,7 +546,7 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
   const long M = (long)B * S;
   const size_t e = esize(h->d.dtype);
   const long xt_stride = (long)(kFrames + 2) * nm, hb_stride = (long)(kFrames + 1) * d;
-  h->timed("mel_to_conv_input", 0, 0, [&] { mel_to_conv_input(h->dt, mel, B, nm, h->xt.p, xt_stride, h->hs); });
+  h->timed("mel_to_conv_input", 0, 0, h->he, [&] { mel_to_conv_input(h->dt, mel, B, nm, h->xt.p, xt_stride, h->he); });
   {  // conv1 + GELU → hbuf rows 1..3000 of every clip (row 0 = conv2's zero padding)
     GemmArgs g = rowgemm(h->xt.p, nm, h->conv1_w, B * kFrames, d, h->k1pad, (char*)h->hbuf.p + d * e, d);
     g.a_Mb = kFrames; g.a_strideB = xt_stride;
@@ -542,7 +564,7 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
   const int nl = h->dbg_enc_layers >= 0 ? std::min(h->dbg_enc_layers, h->d.n_layers) : h->d.n_layers;
   for (int l = 0; l < nl; ++l) {
     const LayerW& w = h->enc[l];
-    h->timed("layernorm", 0, M * d * (4.0 + e), [&] { layernorm(h->dt, h->x.as<float>(), w.ln1_w, w.ln1_b, h->h.p, (int)M, d, h->hs); });
+    h->timed("layernorm", 0, M * d * (4.0 + e), h->he, [&] { layernorm(h->dt, h->x.as<float>(), w.ln1_w, w.ln1_b, h->h.p, (int)M, d, h->he); });
     GemmArgs q = rowgemm(h->h.p, d, w.qkv_w, (int)M, 3 * d, d, h->qkv.p, 3 * d);
     q.bias = w.qkv_b;
     run_gemm(h, "enc_gemm", q);
@@ -551,13 +573,13 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
     a.k = (char*)h->qkv.p + d * e; a.v = (char*)h->qkv.p + 2 * d * e;
     a.k_sb = (long)S * 3 * d; a.k_sh = 64; a.k_sk = 3 * d;
     a.o = h->att.p; a.ldo = d; a.o_Sb = S; a.B = B; a.H = H; a.nkeys = S;
-    h->timed("enc_attn", 4.0 * B * H * (double)S * S * 64, 0, [&] {
-      if (!attention_flash(h->dt, a, h->hs)) attention_decode(h->dt, a, h->hs);
+    h->timed("enc_attn", 4.0 * B * H * (double)S * S * 64, 0, h->he, [&] {
+      if (!attention_flash(h->dt, a, h->he)) attention_decode(h->dt, a, h->he);
     });
     GemmArgs o = rowgemm(h->att.p, d, w.o_w, (int)M, d, d, h->x.p, d);
     o.bias = w.o_b; o.resid = h->x.as<float>(); o.out_f32 = 1;
     run_gemm(h, "enc_gemm", o);
-    h->timed("layernorm", 0, M * d * (4.0 + e), [&] { layernorm(h->dt, h->x.as<float>(), w.ln2_w, w.ln2_b, h->h.p, (int)M, d, h->hs); });
+    h->timed("layernorm", 0, M * d * (4.0 + e), h->he, [&] { layernorm(h->dt, h->x.as<float>(), w.ln2_w, w.ln2_b, h->h.p, (int)M, d, h->he); });
     GemmArgs f1 = rowgemm(h->h.p, d, w.fc1_w, (int)M, h->d.ffn, d, h->ffn.p, h->d.ffn);
     f1.bias = w.fc1_b; f1.act = 1;
     run_gemm(h, "enc_gemm", f1);
@@ -566,50 +588,64 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
     run_gemm(h, "enc_gemm", f2);
   }
   void* dst = enc_out ? enc_out : h->encout.p;
-  h->timed("layernorm", 0, M * d * (4.0 + e), [&] { layernorm(h->dt, h->x.as<float>(), h->enc_ln_w, h->enc_ln_b, dst, (int)M, d, h->hs); });
+  h->timed("layernorm", 0, M * d * (4.0 + e), h->he, [&] { layernorm(h->dt, h->x.as<float>(), h->enc_ln_w, h->enc_ln_b, dst, (int)M, d, h->he); });
   if (enc_out && enc_out != h->encout.p)
-    HIPCHK(hipMemcpyAsync(h->encout.p, enc_out, M * d * e, hipMemcpyDeviceToDevice, h->hs));
+    HIPCHK(hipMemcpyAsync(h->encout.p, enc_out, M * d * e, hipMemcpyDeviceToDevice, h->he));
 }
 
 enum { I_STEP = 0, I_POS = 1, I_DONE = 2, I_TICKET = 3, I_UNFIN = 4, I_NEXT = 16 };
 
+void drop_graphs(wcb_handle* h) {
+  for (int i = 0; i < 2; ++i) {
+    if (h->gexec[i]) (void)hipGraphExecDestroy(h->gexec[i]);
+    h->gexec[i] = nullptr;
+    h->gkey[i].clear();
+  }
+}
+
 void ensure_dec_ws(wcb_handle* h, int B, int T, int out_ld) {
   const size_t e = esize(h->d.dtype), d = h->d.d_model, L = h->d.n_layers, S = h->S();
-  if (B > h->dec_B || T > h->dec_T) {
-    h->xkv.ensure(2 * L * (size_t)B * S * d * e);
-    h->kvself.ensure(2 * L * (size_t)B * T * d * e);
-    h->dec_B = std::max(h->dec_B, B);
-    h->dec_T = std::max(h->dec_T, T);
-    if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; h->gkey.clear(); }
-  }
-  const size_t before = h->dx.bytes + h->logits.bytes + h->ints.bytes + h->outbuf.bytes + h->dffn.bytes;
+  const size_t need[] = {2 * L * (size_t)B * S * d * e, 2 * L * (size_t)B * T * d * e, (size_t)B * d * 4,
+                         (size_t)B * h->d.ffn * e, (size_t)B * h->d.vocab * 4, (size_t)(I_NEXT + 3 * B + 16) * 4,
+                         (size_t)B * out_ld * 4};
+  const DevBuf* have[] = {&h->xkv2[1], &h->kvself, &h->dx, &h->dffn, &h->logits, &h->ints, &h->outbuf};
+  bool grow = false;
+  for (int i = 0; i < 7; ++i) grow |= need[i] > have[i]->bytes;
+  if (!grow && B <= h->dec_B && T <= h->dec_T) return;
+  quiesce(h);
+  drop_graphs(h);
+  h->xkv2[0].ensure(need[0]);
+  h->xkv2[1].ensure(need[0]);
+  h->kvself.ensure(need[1]);
+  h->dec_B = std::max(h->dec_B, B);
+  h->dec_T = std::max(h->dec_T, T);
   h->dx.ensure((size_t)B * d * 4);
   h->dh.ensure((size_t)B * d * e);
   h->dq.ensure((size_t)B * d * e);
   h->datt.ensure((size_t)B * d * e);
   h->dffn.ensure((size_t)B * h->d.ffn * e);
-  h->logits.ensure((size_t)B * h->d.vocab * 4);
   h->dstats.ensure((size_t)B * (d / 16) * 2 * 4);
+  h->xpart.ensure((size_t)B * h->H() * kXSplit * 66 * 4);
+  h->xticket.ensure((size_t)B * h->H() * 4);     // zeroed on allocation; combiners reset their slot
+  h->logits.ensure((size_t)B * h->d.vocab * 4);
   h->nchunk = (h->d.vocab + 63) / 64;      // one argmax partial per LM-head workgroup (64 columns)
   h->part_val.ensure((size_t)B * h->nchunk * 4);
   h->part_idx.ensure((size_t)B * h->nchunk * 4);
-  h->ints.ensure((size_t)(I_NEXT + 3 * B + 16) * 4);
-  h->outbuf.ensure((size_t)B * out_ld * 4);
-  const size_t after = h->dx.bytes + h->logits.bytes + h->ints.bytes + h->outbuf.bytes + h->dffn.bytes;
-  if (after != before && h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; h->gkey.clear(); }
+  h->ints.ensure(need[5]);
+  h->outbuf.ensure(need[6]);
 }
 
 // cross-attention K/V of every decoder layer from the encoder output (A4), once per clip:
 // one GEMM [B·1500, d] × [2·L·d, d]ᵀ written head-split as [L·2][B][H][1500][64]
-void cross_kv(wcb_handle* h, int B) {
+void cross_kv(wcb_handle* h, int B, int buf) {
   const int d = h->d.d_model, S = h->S(), L = h->d.n_layers;
-  GemmArgs g = rowgemm(h->encout.p, d, h->xkv_w, B * S, 2 * L * d, d, h->xkv.p, 0);
+  GemmArgs g = rowgemm(h->encout.p, d, h->xkv_w, B * S, 2 * L * d, d, h->xkv2[buf].p, 0);
   g.bias = h->xkv_b; g.mode = 1; g.hs_S = S; g.hs_H = h->H(); g.hs_B = B;
   run_gemm(h, "xkv_gemm", g);
 }
 
 struct StepCfg {
-  int B, T, out_ld;
+  int B, T, out_ld, buf;   // buf: which cross-K/V buffer the step reads
   bool lm_head, select;
   float* logits_out; long logits_ld;   // LM head destination
   const wcb_bias* bias; float lam; int min_new;
@@ -655,11 +691,13 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, hipStream_t st
     xq.bias = w.xq_b;
     gemm(h->dt, xq, st_);
     AttnArgs xa;
-    const char* xkv = (const char*)h->xkv.p + (l * xkv_l + (size_t)b0 * H * S * 64) * e;
+    const char* xkv = (const char*)h->xkv2[c.buf].p + (l * xkv_l + (size_t)b0 * H * S * 64) * e;
     xa.q = dq; xa.ldq = d; xa.q_Sb = 1; xa.Sq = 1;
     xa.k = xkv; xa.v = xkv + (size_t)B * H * S * 64 * e;
     xa.k_sb = (long)H * S * 64; xa.k_sh = (long)S * 64; xa.k_sk = 64;
     xa.o = datt; xa.ldo = d; xa.o_Sb = 1; xa.B = nb; xa.H = H; xa.nkeys = S;
+    xa.nsplit = kXSplit; xa.part = h->xpart.as<float>() + (size_t)b0 * H * kXSplit * 66;
+    xa.ticket = h->xticket.as<int>() + (size_t)b0 * H;
     attention_decode(h->dt, xa, st_);
     GemmArgs xo = rowgemm(datt, d, w.xo_w, nb, d, d, x, d);
     xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st; xo.st_nb = nbk;
@@ -738,14 +776,14 @@ int wcb_log_mel(wcb_handle* h, const float* pcm, int B, int n_samples, int64_t p
   return guarded(h, [&] {
     REQUIRE(h && pcm && mel_out && B > 0 && n_samples > 0, "bad argument");
     REQUIRE(pcm_stride >= std::min(n_samples, kNSamp), "pcm_stride < n_samples");
-    sync_in(h, stream);
-    h->clip_max.ensure((size_t)std::max(B, h->enc_B) * 4);
-    h->timed("log_mel", 0, (double)B * (std::min(n_samples, kNSamp) * 4.0 + h->d.n_mel * kFrames * 4.0 * 3), [&] {
+    if ((size_t)B * 4 > h->clip_max.bytes) { quiesce(h); h->clip_max.ensure((size_t)std::max(B, h->enc_B) * 4); }
+    sync_in(h, stream, h->he);
+    h->timed("log_mel", 0, (double)B * (std::min(n_samples, kNSamp) * 4.0 + h->d.n_mel * kFrames * 4.0 * 3), h->he, [&] {
       logmel_power_mel(pcm, (long)pcm_stride, n_samples, B, h->dft.as<float>(), h->mel_lo.as<int>(), h->mel_hi.as<int>(),
-                       h->mel_w.as<float>(), h->d.n_mel, mel_out, h->clip_max.as<unsigned>(), h->hs);
-      logmel_normalize(mel_out, h->clip_max.as<unsigned>(), B, h->d.n_mel, h->hs);
+                       h->mel_w.as<float>(), h->d.n_mel, mel_out, h->clip_max.as<unsigned>(), h->he);
+      logmel_normalize(mel_out, h->clip_max.as<unsigned>(), B, h->d.n_mel, h->he);
     });
-    sync_out(h, stream);
+    sync_out(h, stream, h->he);
   });
 }
 
@@ -753,9 +791,10 @@ int wcb_encode(wcb_handle* h, const float* mel, int B, void* enc_out, void* stre
   return guarded(h, [&] {
     REQUIRE(h && mel && B > 0, "bad argument");
     if (!h->ready) throw WcbError(WCB_ERR_STATE, "weights not finalized");
-    sync_in(h, stream);
+    ensure_enc_ws(h, B);
+    sync_in(h, stream, h->he);
     encode_impl(h, mel, B, enc_out);
-    sync_out(h, stream);
+    sync_out(h, stream, h->he);
   });
 }
 
@@ -768,61 +807,68 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     REQUIRE(B <= 64, "batch > 64 per handle: split the batch (decode GEMMs are the skinny M<=64 path)");
     REQUIRE(cfg->bias_boost >= 0.f, "bias_boost must be >= 0");
     REQUIRE(cfg->max_new_tokens >= 1, "max_new_tokens must be >= 1");
+    REQUIRE(mel != nullptr, "mel is required");
     const int P = prefix ? prefix_len : 1;
     REQUIRE(P >= 1, "prefix_len must be >= 1");
     const int T = P + cfg->max_new_tokens;
     REQUIRE(T <= h->d.n_text_ctx + 1, "prefix + max_new_tokens exceeds max_target_positions");
     const wcb_bias* bs = bias ? bias : h->empty_bias.get();
     REQUIRE(bs->vocab == h->d.vocab, "bias automaton built for another vocabulary");
-    sync_in(h, stream);
-    if (mel) encode_impl(h, mel, B, nullptr);
-    else REQUIRE(h->enc_B >= B, "mel == NULL requires a preceding wcb_encode");
+    const bool fixed_len = cfg->min_new_tokens >= cfg->max_new_tokens;   // EOS masked: no host polling
     const int out_ld = cfg->max_new_tokens;
     const int Tc = std::min(T, h->d.n_text_ctx);
+    ensure_enc_ws(h, B);
     ensure_dec_ws(h, B, Tc, out_ld);
-    h->timed("xkv_gemm_total", 0, 0, [&] { cross_kv(h, B); });
-    // state: step = 0, pos = 0, next = first prefix token
+    const int buf = h->gen_count++ & 1;
+    // ---- encoder stream: front end → encoder → cross-K/V into buffer `buf` once the decode that
+    //      last read that buffer has finished. It overlaps the previous call's decode.
+    sync_in(h, stream, h->he);
+    HIPCHK(hipStreamWaitEvent(h->he, h->ev_dec[buf], 0));
+    encode_impl(h, mel, B, nullptr);
+    h->timed("xkv_gemm_total", 0, 0, h->he, [&] { cross_kv(h, B, buf); });
+    HIPCHK(hipEventRecord(h->ev_xkv[buf], h->he));
+    // ---- decode stream
+    HIPCHK(hipStreamWaitEvent(h->hs, h->ev_xkv[buf], 0));
     int* ints = h->ints.as<int>();
     HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 3 * B) * 4, h->hs));
     if (prefix) {
-      h->forced.ensure((size_t)B * P * 4);
+      if ((size_t)B * P * 4 > h->forced.bytes) { quiesce(h); h->forced.ensure((size_t)B * P * 4); }
       for (int b = 0; b < B; ++b)
         HIPCHK(hipMemcpyAsync(h->forced.as<int>() + (size_t)b * P, prefix, (size_t)P * 4, hipMemcpyHostToDevice, h->hs));
       gather_col(ints + I_NEXT, h->forced.as<int>(), B, P, 0, h->hs);
     } else {
       fill_i32(ints + I_NEXT, h->d.decoder_start_token_id, B, h->hs);
     }
-    StepCfg sc{B, Tc, out_ld, false, false, h->logits.as<float>(), (long)h->d.vocab, bs, cfg->bias_boost,
+    StepCfg sc{B, Tc, out_ld, buf, false, false, h->logits.as<float>(), (long)h->d.vocab, bs, cfg->bias_boost,
                cfg->min_new_tokens, h->forced.as<int>(), P};
     for (int p = 0; p + 1 < P; ++p) decode_step(h, sc);   // prompt prefill, teacher-forced
     sc.lm_head = true;
     sc.select = true;
     char key[256];
-    snprintf(key, sizeof key, "%d/%d/%d/%p/%a/%d", B, Tc, out_ld, (const void*)bs, cfg->bias_boost, cfg->min_new_tokens);
+    snprintf(key, sizeof key, "%d/%d/%d/%p/%a/%d/%d", B, Tc, out_ld, (const void*)bs, cfg->bias_boost, cfg->min_new_tokens,
+             h->n_sub);
     const int max_new = cfg->max_new_tokens;
     const int chunk = 8;
     int done = 0, steps = 0;
-    if (cfg->use_graph) {
-      if (!h->gexec || h->gkey != key) {
-        if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
-        hipGraph_t graph;
-        HIPCHK(hipStreamBeginCapture(h->hs, hipStreamCaptureModeThreadLocal));
-        decode_step(h, sc);
-        HIPCHK(hipStreamEndCapture(h->hs, &graph));
-        HIPCHK(hipGraphInstantiate(&h->gexec, graph, nullptr, nullptr, 0));
-        HIPCHK(hipGraphDestroy(graph));
-        h->gkey = key;
-      }
+    if (cfg->use_graph && (!h->gexec[buf] || h->gkey[buf] != key)) {
+      if (h->gexec[buf]) { (void)hipGraphExecDestroy(h->gexec[buf]); h->gexec[buf] = nullptr; }
+      hipGraph_t graph;
+      HIPCHK(hipStreamBeginCapture(h->hs, hipStreamCaptureModeThreadLocal));
+      decode_step(h, sc);
+      HIPCHK(hipStreamEndCapture(h->hs, &graph));
+      HIPCHK(hipGraphInstantiate(&h->gexec[buf], graph, nullptr, nullptr, 0));
+      HIPCHK(hipGraphDestroy(graph));
+      h->gkey[buf] = key;
     }
-    h->timed("decode_loop", 0, 0, [&] {
+    h->timed("decode_loop", 0, 0, h->hs, [&] {
       while (steps < max_new) {
         const int n = std::min(chunk, max_new - steps);
         for (int i = 0; i < n; ++i) {
-          if (cfg->use_graph) HIPCHK(hipGraphLaunch(h->gexec, h->hs));
+          if (cfg->use_graph) HIPCHK(hipGraphLaunch(h->gexec[buf], h->hs));
           else decode_step(h, sc);
         }
         steps += n;
-        if (cfg->min_new_tokens >= max_new) continue;   // EOS masked throughout: no early exit
+        if (fixed_len) continue;
         HIPCHK(hipMemcpyAsync(&done, ints + I_DONE, 4, hipMemcpyDeviceToHost, h->hs));
         HIPCHK(hipStreamSynchronize(h->hs));
         if (done > 0) break;
@@ -830,36 +876,51 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     });
     if (done <= 0) done = steps;
     HIPCHK(hipMemcpyAsync(out_ids, h->outbuf.p, (size_t)B * out_ld * 4, hipMemcpyDeviceToDevice, h->hs));
+    HIPCHK(hipEventRecord(h->ev_dec[buf], h->hs));
     *out_steps = std::min(done, max_new);
-    sync_out(h, stream);
+    if (!cfg->async_out) sync_out(h, stream, h->hs);
+  });
+}
+
+int wcb_synchronize(wcb_handle* h) {
+  return guarded(h, [&] {
+    REQUIRE(h, "null handle");
+    quiesce(h);
+    HIPCHK(hipGetLastError());
   });
 }
 
 int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, int T, float* logits, void* enc_out,
                 void* stream) {
   return guarded(h, [&] {
-    REQUIRE(h && dec_ids && logits && B > 0 && T > 0, "bad argument");
+    REQUIRE(h && mel && dec_ids && logits && B > 0 && T > 0, "bad argument");
     if (!h->ready) throw WcbError(WCB_ERR_STATE, "weights not finalized");
+    REQUIRE(B <= 64, "batch > 64 per handle");
     REQUIRE(T <= h->d.n_text_ctx, "decoder_input_ids longer than max_target_positions");
-    sync_in(h, stream);
-    if (mel) encode_impl(h, mel, B, enc_out);
-    else REQUIRE(h->enc_B >= B, "mel == NULL requires a preceding wcb_encode");
+    ensure_enc_ws(h, B);
     ensure_dec_ws(h, B, T, 1);
-    cross_kv(h, B);
+    if ((size_t)B * (T + 1) * 4 > h->forced.bytes) { quiesce(h); h->forced.ensure((size_t)B * (T + 1) * 4); }
+    const int buf = h->gen_count++ & 1;
+    sync_in(h, stream, h->he);
+    HIPCHK(hipStreamWaitEvent(h->he, h->ev_dec[buf], 0));
+    encode_impl(h, mel, B, enc_out);
+    cross_kv(h, B, buf);
+    HIPCHK(hipEventRecord(h->ev_xkv[buf], h->he));
+    HIPCHK(hipStreamWaitEvent(h->hs, h->ev_xkv[buf], 0));
     int* ints = h->ints.as<int>();
     HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 3 * B) * 4, h->hs));
     gather_col(ints + I_NEXT, dec_ids, B, T, 0, h->hs);
     // forced column T is never read: feed positions 0..T-1 (advance reads column pos+1 < T except last)
-    h->forced.ensure((size_t)B * (T + 1) * 4);
     HIPCHK(hipMemsetAsync(h->forced.p, 0, (size_t)B * (T + 1) * 4, h->hs));
     HIPCHK(hipMemcpy2DAsync(h->forced.p, (size_t)(T + 1) * 4, dec_ids, (size_t)T * 4, (size_t)T * 4, B,
                             hipMemcpyDeviceToDevice, h->hs));
     for (int t = 0; t < T; ++t) {
-      StepCfg sc{B, T, 1, true, false, logits + (size_t)t * h->d.vocab, (long)T * h->d.vocab, nullptr, 0.f, 0,
+      StepCfg sc{B, T, 1, buf, true, false, logits + (size_t)t * h->d.vocab, (long)T * h->d.vocab, nullptr, 0.f, 0,
                  h->forced.as<int>(), T + 1};
       decode_step(h, sc);
     }
-    sync_out(h, stream);
+    HIPCHK(hipEventRecord(h->ev_dec[buf], h->hs));
+    sync_out(h, stream, h->hs);
   });
 }
 
@@ -955,7 +1016,7 @@ int wcb_debug_copy(wcb_handle* h, const char* name, void* dst, int64_t bytes, in
     h->dbg_enc_layers = enc_layers;
     const std::map<std::string, DevBuf*> bufs = {{"xt", &h->xt}, {"hbuf", &h->hbuf}, {"x", &h->x}, {"h", &h->h},
                                                  {"qkv", &h->qkv}, {"att", &h->att}, {"ffn", &h->ffn},
-                                                 {"encout", &h->encout}, {"xkv", &h->xkv}, {"logits", &h->logits}};
+                                                 {"encout", &h->encout}, {"xkv", &h->xkv2[0]}, {"logits", &h->logits}};
     if (bytes == 0) return;   // only set the layer limit
     REQUIRE(dst, "null dst");
     auto it = bufs.find(name);
@@ -1035,11 +1096,19 @@ int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, voi
     a.q = q; a.ldq = ld; a.q_Sb = Sq; a.Sq = Sq;
     a.k = k; a.v = v; a.k_sb = (long)Sk * ld; a.k_sh = 64; a.k_sk = ld;
     a.o = o; a.ldo = ld; a.o_Sb = Sq; a.B = B; a.H = H; a.nkeys = Sk;
-    if (flash) {
+    if (flash == 1) {
       REQUIRE(dtype != WCB_F32, "flash attention needs a 16-bit dtype");
       REQUIRE(Sq == Sk, "flash path is the encoder self-attention (Sq == Sk)");
       attention_flash(DType(dtype), a, (hipStream_t)stream);
     } else {
+      static DevBuf part, ticket;   // split-KV workspace of this test entry point (zeroed on growth)
+      if (flash > 1) {
+        a.nsplit = flash;
+        part.ensure((size_t)B * H * Sq * flash * 66 * 4);
+        ticket.ensure((size_t)B * H * Sq * 4);
+        a.part = part.as<float>();
+        a.ticket = ticket.as<int>();
+      }
       attention_decode(DType(dtype), a, (hipStream_t)stream);
     }
     HIPCHK(hipGetLastError());

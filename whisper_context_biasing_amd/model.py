@@ -217,12 +217,17 @@ class WhisperCB:
     def generate(self, input_features=None, labels=None, bias_spans=None, max_length: Optional[int] = None,
                  num_beams: Optional[int] = None, bias_list=None, bias_boost: float = 0.0,
                  min_new_tokens: int = 0, prompt_ids=None, return_dict_in_generate: bool = False,
-                 generation_config=None, use_graph: bool = True, **kwargs):
+                 generation_config=None, use_graph: bool = True, block: bool = True, **kwargs):
         """Greedy decode with the reference's eval semantics.
 
         `labels` / `bias_spans` are accepted and ignored for token selection exactly like the
         reference (`[tf] trainer_seq2seq.py:310-329`), unless `bias_boost > 0` and no explicit
         `bias_list` is given — then the batch's spans form the boosted bias list.
+
+        `block=False` (serving pipelines): the caller's stream is not made to wait for the decode, so
+        the next call's front end + encoder overlap this decode; the returned ids (and the inputs)
+        must be kept alive and are valid only after `synchronize()`. Only meaningful with
+        `min_new_tokens >= max_length` (no early-exit polling).
         """
         if not self._loaded:
             raise _lib.WcbError("weights not loaded")
@@ -241,7 +246,7 @@ class WhisperCB:
         if phrases is None and bias_boost > 0 and bias_spans is not None:
             phrases = self._spans_to_phrases(bias_spans)
         bl = self.bias_list(phrases) if (phrases and bias_boost > 0) else None
-        cfg = _lib.WcbGenCfg(max_new, int(min_new_tokens), 1, float(bias_boost), int(use_graph))
+        cfg = _lib.WcbGenCfg(max_new, int(min_new_tokens), 1, float(bias_boost), int(use_graph), int(not block))
         out = torch.empty(B, max_new, dtype=torch.int32, device=self.device)
         steps = C.c_int32(0)
         pre = np.asarray(prefix, dtype=np.int32)
@@ -249,11 +254,17 @@ class WhisperCB:
                                           pre.ctypes.data if len(prefix) > 1 else None, len(prefix),
                                           _ptr(out), C.byref(steps), _stream(self.device)),
                    self._h, "wcb_generate")
+        if not block:
+            return out[:, :steps.value]            # int32, valid after synchronize()
         ids = out[:, :steps.value].to(torch.int64)
         if return_dict_in_generate:
             sot = torch.tensor(prefix, dtype=torch.int64, device=self.device)[None].expand(B, -1)
             return GenerateOutput(sequences=torch.cat([sot, ids], dim=1))
         return ids
+
+    def synchronize(self):
+        """Wait for every queued front-end / encoder / decode operation of this model."""
+        _lib.check(self._lib.wcb_synchronize(self._h), self._h, "wcb_synchronize")
 
     # ------------------------------------------------------------------------------- forward
     def forward(self, input_features=None, decoder_input_ids=None, labels=None, bias_spans=None,
