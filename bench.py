@@ -64,11 +64,25 @@ def cpu_baseline(size: str, n_tokens: int, n_phr: int, boost: float, seed: int =
                       f"{n_tokens} KV-cached greedy tokens with {n_phr}-phrase boost; {dt:.2f} s wall"}
 
 
+def _pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass (profiles/*pmc*.json,
+    written by tools/pmc_traffic.py: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if kernel in d.get("kernels", {}):
+            return d["kernels"][kernel]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="small")
     ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
     ap.add_argument("--new-tokens", type=int, default=64)
@@ -87,7 +101,7 @@ def main():
     from whisper_context_biasing_amd.config import get_dims
     from whisper_context_biasing_amd.model import WhisperCB
     from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list
-    from whisper_context_biasing_amd.weights import make_weights, param_shapes
+    from whisper_context_biasing_amd.shard import broadcast_weights, max_over_ranks, shard_bounds
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -101,30 +115,17 @@ def main():
 
     dims = get_dims(args.model)
     # ---- weights: rank 0 generates, one RCCL broadcast of the packed bf16 blob over xGMI
-    names = [n for n, _ in param_shapes(dims)]
-    shapes = dict(param_shapes(dims))
-    numel = [int(np.prod(shapes[n])) for n in names]
-    if rank == 0:
-        sd = make_weights(dims, seed=0)
-        flat = torch.cat([torch.from_numpy(sd[n]).reshape(-1) for n in names]).to(torch.bfloat16).to(dev)
-        del sd
-    else:
-        flat = torch.empty(sum(numel), dtype=torch.bfloat16, device=dev)
+    t0 = time.perf_counter()
+    sd = broadcast_weights(dims, dev, seed=0)
     if world > 1:
-        t0 = time.perf_counter()
-        dist.broadcast(flat, src=0)
         torch.cuda.synchronize()
-        log(f"rank {rank}: weight broadcast {flat.numel() * 2 / 1e9:.3f} GB in {time.perf_counter() - t0:.3f} s")
-    host = flat.float().cpu().numpy()
-    sd, off = {}, 0
-    for n, k in zip(names, numel):
-        sd[n] = host[off:off + k].reshape(shapes[n])
-        off += k
+        log(f"rank {rank}: weights broadcast in {time.perf_counter() - t0:.3f} s")
     model = WhisperCB.from_state_dict(dims, sd, dtype=args.dtype, device=local)
-    del sd, host, flat
+    del sd
 
     B = args.batch
-    pcm = torch.from_numpy(synth_batch(B, start=rank * B)).to(dev)     # resident in HBM before timing
+    lo, hi = shard_bounds(world * B, rank, world)                      # this rank's utterances
+    pcm = torch.from_numpy(synth_batch(hi - lo, start=lo)).to(dev)     # resident in HBM before timing
     phrases = synth_bias_list(args.bias_phrases, eot=dims.eos_token_id)
     bias = model.bias_list(phrases)
     use_graph = not args.no_graph
@@ -158,26 +159,44 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
     prof = model.profile_read() if not args.no_profile else {}
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B * 30.0 / (elapsed / args.steps)
 
-    roof = None
+    roofs = {}
     if prof.get("enc_gemm"):
+        # encoder tile GEMMs: HIP events on the encoder stream around every launch
         p = prof["enc_gemm"]
-        per_launch_flops = p["flops"] / p["launches"]
         avg_ms = p["ms"] / p["launches"]
-        achieved = per_launch_flops / (avg_ms * 1e-3) / 1e12
+        achieved = p["flops"] / p["launches"] / (avg_ms * 1e-3) / 1e12
         peak = {"bf16": PEAK_BF16_TFLOPS, "f16": PEAK_F16_TFLOPS}.get(args.dtype, PEAK_F32_TFLOPS)
-        roof = {"bound": "mfma", "kernel": "gemm_tile_kernel (encoder conv/QKV/out/fc1/fc2)",
-                "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": None,
-                "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": per_launch_flops}
+        roofs["enc_gemm"] = {"bound": "mfma", "kernel": "gemm_tile_kernel (encoder conv/QKV/out/fc1/fc2)",
+                             "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                             "frac": round(achieved / peak, 4), "traffic": None,
+                             "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": p["flops"] / p["launches"],
+                             "total_ms_per_step": round(p["ms"] / args.steps, 3), "timing": "hip_events"}
+    if prof.get("dec_xattn"):
+        # decode cross-attention: replayed inside the decode hipGraph, so each launch is timed by
+        # s_memrealtime stamps (first workgroup start → last workgroup end) written by the kernel
+        p = prof["dec_xattn"]
+        avg_ms = p["ms"] / p["launches"]
+        bpl = p["bytes"] / p["launches"]
+        achieved = bpl / (avg_ms * 1e-3) / 1e9
+        roofs["dec_xattn"] = {"bound": "hbm", "kernel": "attn_decode_kernel (decoder cross-attention, split-KV)",
+                              "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                              "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                              "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": bpl,
+                              "total_ms_per_step": round(p["ms"] / args.steps, 3),
+                              "timing": "device s_memrealtime stamps (graph node)"}
+    roof = None
+    if roofs:
+        dom = max(roofs, key=lambda k: roofs[k]["total_ms_per_step"])   # dominant = most kernel time
+        roof = dict(roofs[dom])
+        tr = _pmc_traffic(dom)
+        if tr:
+            roof["traffic"], roof["traffic_source"] = tr
+        others = {k: v for k, v in roofs.items() if k != dom}
     phases = {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "launches_per_step": v["launches"] / args.steps}
               for k, v in prof.items()}
 
@@ -199,6 +218,7 @@ def main():
                        "hipgraph_decode": use_graph, "batches_in_flight": 2 if overlap else 1},
             "rtf": round(1.0 / (value / world), 6),
             "roofline": roof,
+            "roofline_other": others if roofs else None,
             "phases": phases,
             "cpu_baseline": cpu,
         }

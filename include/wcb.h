@@ -84,11 +84,11 @@ int wcb_encode(wcb_handle* h, const float* mel, int B, void* enc_out, void* stre
 int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg, const wcb_bias* bias,
                  const int32_t* prefix, int prefix_len, int32_t* out_ids, int32_t* out_steps, void* stream);
 
-/* replaces forward(input_features, decoder_input_ids) (models/whisper_medical.py:45-111):
- * dec_ids int32 DEVICE [B][T] → logits f32 DEVICE [B][T][vocab]; enc_out as in wcb_encode. */
 /* wait for every queued front-end / encoder / decode operation of the handle */
 int wcb_synchronize(wcb_handle* h);
 
+/* replaces forward(input_features, decoder_input_ids) (models/whisper_medical.py:45-111):
+ * dec_ids int32 DEVICE [B][T] → logits f32 DEVICE [B][T][vocab]; enc_out as in wcb_encode. */
 int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, int T, float* logits,
                 void* enc_out, void* stream);
 
@@ -127,6 +127,10 @@ int wcb_op_layernorm(int dtype, const float* x, const float* w, const float* b, 
  * n split-KV key chunks combined by the last-arriving chunk. */
 int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H, int Sq,
                      int Sk, int flash, void* stream);
+/* decode attention in the runtime's layout: q/o [B][H*64], K/V head-major [B][H][Sk][64]; one query
+ * per (row, head), nsplit key chunks (split-KV), kernel variant (k_attn.hip launch_decode). */
+int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H,
+                            int Sk, int nsplit, int variant, void* stream);
 
 #ifdef __cplusplus
 }

@@ -53,6 +53,8 @@ SIGNATURES = {
     "wcb_op_gemm_ln": (C.c_int, [C.c_int, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P,
                                  C.c_int, _P]),
     "wcb_op_layernorm": (C.c_int, [C.c_int, _P, _P, _P, _P, C.c_int, C.c_int, _P]),
+    "wcb_op_attention_decode": (C.c_int, [C.c_int, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                          _P]),
     "wcb_op_attention": (C.c_int, [C.c_int, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.c_int, _P]),
 }
@@ -60,6 +62,10 @@ SIGNATURES = {
 
 class WcbError(RuntimeError):
     pass
+
+
+class WcbArgError(WcbError, ValueError):
+    """WCB_ERR_ARG: the reference raises ValueError for these (e.g. whisper_medical.py:87-90)."""
 
 
 _lib = None
@@ -92,5 +98,6 @@ def check(rc: int, handle=None, what: str = ""):
     if rc < 0:
         lib = load()
         msg = lib.wcb_last_error(handle)
-        raise WcbError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+        cls = WcbArgError if rc == -1 else WcbError
+        raise cls(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
     return rc

@@ -10,6 +10,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "kernels.h"
 
 typedef uint16_t bf16_t;
 typedef _Float16 f16_t;
@@ -105,6 +106,22 @@ template <typename T> WCB_DEV void load8f(const T* src, float* v) {
       v[j] = f[j];
     }
   }
+}
+
+// Per-launch device time stamps (profiling of kernels replayed inside a hipGraph, where HIP events
+// cannot bracket one node). A launch owns kStampSub sub-slots; workgroup w folds its
+// (~t_start, t_end) into sub-slot w % kStampSub with atomicMax (sub-slots keep same-address atomic
+// contention low), stamp_reduce takes max(t_end) − min(t_start) over them. s_memrealtime ticks
+// (100 MHz). Launch slot = pos·stride + idx; slots start zeroed.
+WCB_DEV unsigned long long stamp_now() { return __builtin_amdgcn_s_memrealtime(); }
+WCB_DEV void stamp_commit(const wcb::Stamp& s, unsigned long long t0) {
+  if (!s.base) return;
+  const unsigned long long t1 = stamp_now();
+  const int wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  unsigned long long* slot =
+      s.base + 2 * (((long)(*s.pos) * s.stride + s.idx) * wcb::kStampSub + (wg % wcb::kStampSub));
+  atomicMax(slot, ~t0);
+  atomicMax(slot + 1, t1);
 }
 
 // Bijective XCD-aware remap of a 1-D workgroup id (cdna_hip_programming.md §5 "XCD swizzle").

@@ -297,6 +297,18 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) b[j][ks] = load_frag<T>(W + ks * 32);
   }
+  // Epilogue operands (bias, residual, decode position) are fetched now, behind the weight
+  // stream, instead of after the K reduction: one memory round trip less on the critical path.
+  constexpr int EP = (MF * 16 * BNC + NT - 1) / NT;
+  float pf_bias[EP], pf_res[EP];
+#pragma unroll
+  for (int ep = 0; ep < EP; ++ep) {
+    const int t = ep * NT + tid, row = t / BNC, nn = n0 + t % BNC;
+    const bool ok = t < MF * 16 * BNC && row < g.M && nn < g.N;
+    pf_bias[ep] = (ok && g.bias) ? g.bias[nn] : 0.f;
+    pf_res[ep] = (ok && g.resid && g.mode == 0) ? g.resid[c_row(g, row) + nn] : 0.f;
+  }
+  const int pos_v = g.mode == 2 ? *g.pos : 0;
   f32x4 acc[MF][NF];
 #pragma unroll
   for (int i = 0; i < MF; ++i)
@@ -390,8 +402,9 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
   const bool mask_eos = g.sel_val && *g.sel_step < g.sel_min_new;
   // epilogue: thread → (row, col) with the columns of a row contiguous in the wave, so row-wise
   // reductions (stats partials: 16 lanes; argmax partial: BNC lanes) are shuffles
-  for (int t0 = 0; t0 < MF * 16 * BNC; t0 += NT) {
-    const int t = t0 + tid;
+#pragma unroll
+  for (int ep = 0; ep < EP; ++ep) {
+    const int t = ep * NT + tid;
     const int row = t / BNC, col = t % BNC;
     const int nn = n0 + col;
     const bool valid = t < MF * 16 * BNC && row < g.M && nn < g.N;
@@ -399,8 +412,23 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
     if (valid) {
 #pragma unroll
       for (int w = 0; w < SL; ++w) v += red[w][row][col];
-      v = epi_pointwise<T>(g, row, nn, v);
-      v = epi_store1<T>(g, row, nn, v);
+      v += pf_bias[ep];
+      if (g.act == 1) v = gelu_t<T>(v);
+      if (g.addrow) v += g.addrow[(long)(g.c_Mb ? row % g.c_Mb : row) * g.N + nn];
+      if (g.mode == 2 && nn >= g.n_split) {   // k / v of the new token → self-attention KV cache
+        const int n2 = nn - g.n_split;
+        const int hh = n2 >> 6, dd = n2 & 63;
+        const int kv = hh / g.hs_H, h = hh % g.hs_H;
+        const long off = ((((long)kv * g.hs_B + row) * g.hs_H + h) * g.kv_T + pos_v) * 64 + dd;
+        reinterpret_cast<T*>(g.kv_out)[off] = DT<T>::fromf(v);
+      } else if (g.mode == 1) {
+        v = epi_store1<T>(g, row, nn, v);
+      } else {
+        const long off = c_row(g, row) + nn;
+        v += pf_res[ep];
+        if (g.out_f32) reinterpret_cast<float*>(g.out)[off] = v;
+        else reinterpret_cast<T*>(g.out)[off] = DT<T>::fromf(v);
+      }
     }
     if (g.st_out) {   // NF == 1: 16 contiguous lanes hold one row of the block
       float s1 = valid ? v : 0.f, s2 = valid ? v * v : 0.f;

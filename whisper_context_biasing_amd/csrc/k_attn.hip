@@ -11,22 +11,159 @@
 //
 // attn_decode_kernel — one query row per workgroup (decoder self-attention over the KV cache,
 //   decoder cross-attention over the precomputed encoder K/V, and the f32 "exact" encoder path).
-//   8 lanes per key (16 B each), scores in LDS, exact two-pass softmax, P·V with per-lane
-//   partial rows reduced by shuffles and LDS. HBM-bound on the K/V read.
+//   8 lanes per key (16 B of K and V each), one pass with an online softmax, optional split-KV
+//   over workgroups. HBM-bound on the K/V read.
 #include "common.h"
 #include "kernels.h"
 
 namespace wcb {
 
-constexpr int kMaxKeys = 2048;
-
+// Single pass over the keys (flash-decoding): every lane group of 8 lanes owns one key per load
+// (16 B of K and of V per lane), a wave covers 64 keys per iteration with all 16 K/V loads in flight
+// at once, the online softmax runs at wave level (running max / denominator, the accumulator
+// rescaled when the max moves), waves combine in LDS, key chunks (split-KV) combine through the
+// last-arriver hand-off below.
+//
 // Split-KV: workgroup (i·nsplit + c, b·H + h) handles key chunk c. With nsplit > 1 each chunk
 // publishes (max, Σexp, Σexp·v[64]) with write-through (sc1) stores, drains them (vmcnt(0)) and takes
 // an agent-scope ticket; the chunk that draws the last ticket reads every partial with sc1 loads,
 // combines them in chunk order (deterministic) and resets the ticket (cdna_hip_programming.md §6
 // Guideline 16, first row of the measured hand-off table).
-template <typename T, int NW>
+template <typename T, int NW, int U>
 __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(AttnArgs a) {
+  __shared__ float wo[NW][64];
+  __shared__ float wm[NW], wl[NW];
+  const int nsplit = a.nsplit > 0 ? a.nsplit : 1;
+  const int i = blockIdx.x / nsplit, chunk = blockIdx.x % nsplit;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const unsigned long long t_start = a.stamp.base ? stamp_now() : 0;
+  const int seg = lane & 7, kg = lane >> 3;
+  const int nk_all = a.nkeys_dev ? (*a.nkeys_dev + a.nkeys_add) : a.nkeys;
+  const int per = (nk_all + nsplit - 1) / nsplit;
+  const int j_lo = chunk * per, j_hi = min(nk_all, j_lo + per);
+  const int nk = max(j_hi - j_lo, 0);
+  const T* q = reinterpret_cast<const T*>(a.q) + ((long)b * a.q_Sb + i) * a.ldq + h * 64;
+  const T* kb = reinterpret_cast<const T*>(a.k) + (long)b * a.k_sb + (long)h * a.k_sh + (long)j_lo * a.k_sk + seg * 8;
+  const T* vb = reinterpret_cast<const T*>(a.v) + (long)b * a.k_sb + (long)h * a.k_sh + (long)j_lo * a.k_sk + seg * 8;
+  float qv[8];
+  load8f<T>(q + seg * 8, qv);
+
+  // U keys per lane group per iteration
+  constexpr int WSPAN = 8 * U, GSPAN = NW * WSPAN;
+  float m = -INFINITY, l = 0.f;              // wave-uniform running max; per-lane partial Σp
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int j0 = wave * WSPAN; j0 < nk; j0 += GSPAN) {
+    float kv[U][8], vv[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load8f<T>(kb + (long)min(j0 + u * 8 + kg, nk - 1) * a.k_sk, kv[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) load8f<T>(vb + (long)min(j0 + u * 8 + kg, nk - 1) * a.k_sk, vv[u]);
+    float sc[U];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d = fmaf(qv[e], kv[u][e], d);
+#pragma unroll
+      for (int x = 1; x < 8; x <<= 1) d += __shfl_xor(d, x, 64);
+      sc[u] = (j0 + u * 8 + kg < nk) ? d : -INFINITY;
+      mx = fmaxf(mx, sc[u]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);           // finite: the first iteration has ≥ 1 valid key
+    const float r = __expf(m - mn);          // 0 on the first iteration (m = −inf)
+    m = mn;
+    l *= r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] *= r;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float p = __expf(sc[u] - m);
+      l += p;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = fmaf(p, vv[u][e], o[e]);
+    }
+  }
+  // reduce over the 8 lane groups (each group holds its own keys' p and p·v)
+  l += __shfl_xor(l, 8, 64);
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o[e] += __shfl_xor(o[e], 8, 64);
+    o[e] += __shfl_xor(o[e], 16, 64);
+    o[e] += __shfl_xor(o[e], 32, 64);
+  }
+  if (kg == 0)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) wo[wave][seg * 8 + e] = o[e];
+  if (lane == 0) { wm[wave] = m; wl[wave] = l; }
+  __syncthreads();
+  if (wave != 0) return;
+  float M = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) M = fmaxf(M, wm[w]);
+  float L = 0.f, acc = 0.f;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const float sw = wl[w] > 0.f ? __expf(wm[w] - M) : 0.f;   // waves without keys hold l = 0
+    L += wl[w] * sw;
+    acc += wo[w][lane] * sw;
+  }
+  T* out = reinterpret_cast<T*>(a.o) + ((long)b * a.o_Sb + i) * a.ldo + h * 64;
+  if (nsplit == 1) {
+    out[lane] = DT<T>::fromf(acc / L);
+    if (lane == 0) stamp_commit(a.stamp, t_start);
+    return;
+  }
+  // ---- split-KV hand-off: publish this chunk's partial, last arriver combines
+  const long slot = ((long)bh * a.Sq + i);
+  float* part = a.part + slot * nsplit * 66;
+  float* mine = part + chunk * 66;
+  __hip_atomic_store(mine + 2 + lane, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) {
+    __hip_atomic_store(mine, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(mine + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int old = 0;
+  if (lane == 0) old = atomicAdd(a.ticket + slot, 1);
+  old = __shfl(old, 0, 64);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (old != nsplit - 1) {
+    if (lane == 0) stamp_commit(a.stamp, t_start);
+    return;
+  }
+  float MM = -INFINITY;
+  for (int c = 0; c < nsplit; ++c) {
+    const float mc = __hip_atomic_load(part + c * 66, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float lc = __hip_atomic_load(part + c * 66 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lc > 0.f && mc > MM) MM = mc;
+  }
+  float LL = 0.f, OO = 0.f;
+  for (int c = 0; c < nsplit; ++c) {
+    const float mc = __hip_atomic_load(part + c * 66, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float lc = __hip_atomic_load(part + c * 66 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float oc = __hip_atomic_load(part + c * 66 + 2 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float w = lc > 0.f ? __expf(mc - MM) : 0.f;    // empty chunks publish l = 0
+    LL += lc * w;
+    OO += oc * w;
+  }
+  out[lane] = DT<T>::fromf(OO / LL);
+  if (lane == 0) {
+    __hip_atomic_store(a.ticket + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    stamp_commit(a.stamp, t_start);
+  }
+}
+
+// Previous two-pass kernel (scores in LDS), kept as a variant for the microbenchmark.
+constexpr int kMaxKeys = 2048;
+template <typename T, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_decode2p_kernel(AttnArgs a) {
   __shared__ float sc[kMaxKeys];
   __shared__ float red[NW][64 + 1];
   __shared__ float stat[2];
@@ -157,15 +294,27 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(AttnArgs a) {
   if (lane == 0) __hip_atomic_store(a.ticket + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+template <typename T>
+static void launch_decode(const AttnArgs& b, dim3 grid, int variant, hipStream_t s) {
+  switch (variant) {
+    case 0: hipLaunchKernelGGL((attn_decode2p_kernel<T, 8>), grid, dim3(512), 0, s, b); break;
+    case 1: hipLaunchKernelGGL((attn_decode_kernel<T, 4, 8>), grid, dim3(256), 0, s, b); break;
+    case 2: hipLaunchKernelGGL((attn_decode_kernel<T, 4, 4>), grid, dim3(256), 0, s, b); break;
+    case 3: hipLaunchKernelGGL((attn_decode_kernel<T, 8, 4>), grid, dim3(512), 0, s, b); break;
+    case 4: hipLaunchKernelGGL((attn_decode_kernel<T, 8, 8>), grid, dim3(512), 0, s, b); break;
+    default: hipLaunchKernelGGL((attn_decode_kernel<T, 16, 4>), grid, dim3(1024), 0, s, b); break;
+  }
+}
+
 void attention_decode(DType t, const AttnArgs& a, hipStream_t s) {
   const int ns = (a.part && a.ticket && a.nsplit > 1) ? a.nsplit : 1;
   AttnArgs b = a;
   b.nsplit = ns;
   const dim3 grid(a.Sq * ns, a.B * a.H);
   switch (t) {
-    case kBF16: hipLaunchKernelGGL((attn_decode_kernel<bf16_t, 8>), grid, dim3(512), 0, s, b); break;
-    case kF16: hipLaunchKernelGGL((attn_decode_kernel<f16_t, 8>), grid, dim3(512), 0, s, b); break;
-    case kF32: hipLaunchKernelGGL((attn_decode_kernel<float, 8>), grid, dim3(512), 0, s, b); break;
+    case kBF16: launch_decode<bf16_t>(b, grid, a.variant, s); break;
+    case kF16: launch_decode<f16_t>(b, grid, a.variant, s); break;
+    case kF32: launch_decode<float>(b, grid, a.variant, s); break;
   }
 }
 

@@ -123,4 +123,27 @@ void fill_i32(int* p, int v, long n, hipStream_t s) {
   hipLaunchKernelGGL(fill_i32_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, p, v, n);
 }
 
+__global__ __launch_bounds__(64) void stamp_reduce_kernel(unsigned long long* slots, long n, unsigned long long* acc) {
+  const long i = blockIdx.x * 64L + threadIdx.x;
+  unsigned long long ticks = 0, used = 0;
+  if (i < n) {
+    unsigned long long* s = slots + 2 * i * kStampSub;
+    unsigned long long nt0 = 0, t1 = 0;
+    for (int k = 0; k < kStampSub; ++k) {
+      nt0 = max(nt0, s[2 * k]);
+      t1 = max(t1, s[2 * k + 1]);
+      s[2 * k] = 0; s[2 * k + 1] = 0;
+    }
+    if (t1 != 0) { ticks = t1 - ~nt0; used = 1; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    ticks += __shfl_xor(ticks, o, 64);
+    used += __shfl_xor(used, o, 64);
+  }
+  if (threadIdx.x == 0 && used) { atomicAdd(acc, ticks); atomicAdd(acc + 1, used); }
+}
+void stamp_reduce(unsigned long long* slots, long n, unsigned long long* acc, hipStream_t s) {
+  hipLaunchKernelGGL(stamp_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, slots, n, acc);
+}
+
 }  // namespace wcb

@@ -49,6 +49,12 @@ void embed(DType t, const void* emb, const void* pos_emb, const int* ids, const 
 // Attention over heads of 64. q row for (b, i): q + (b·q_Sb + i)·ldq + h·64.
 // key j of (b, h): k + b·k_sb + h·k_sh + j·k_sk (same strides for v).
 // nkeys: if nkeys_dev != null → *nkeys_dev + nkeys_add (self-attention), else nkeys.
+// Per-launch device time stamps for kernels replayed inside the decode hipGraph (see common.h).
+constexpr int kStampSub = 64;
+struct Stamp {
+  unsigned long long* base = nullptr; const int* pos = nullptr; int stride = 0, idx = 0;
+};
+
 struct AttnArgs {
   const void* q = nullptr; long ldq = 0; long q_Sb = 0; int Sq = 1;
   const void* k = nullptr; const void* v = nullptr; long k_sb = 0, k_sh = 0, k_sk = 0;
@@ -58,6 +64,8 @@ struct AttnArgs {
   // split-KV (decode): nsplit key chunks per query row, partials [B·H·Sq][nsplit][66] f32, tickets
   // [B·H·Sq] int (zero-initialised; the combining chunk resets its ticket)
   int nsplit = 1; float* part = nullptr; int* ticket = nullptr;
+  Stamp stamp;   // profiling (decode graph): per-launch start/end stamps
+  int variant = 1;   // decode kernel variant (k_attn.hip launch_decode)
 };
 void attention_decode(DType t, const AttnArgs& a, hipStream_t s);   // VALU, any T, any Sq
 bool attention_flash(DType t, const AttnArgs& a, hipStream_t s);    // MFMA encoder (16-bit T)
@@ -91,5 +99,8 @@ void advance_forced(int* next_ids, const int* forced, int M, int ld, int* pos, h
 void gather_col(int* dst, const int* src, int M, int ld, int col, hipStream_t s);
 
 void fill_i32(int* p, int v, long n, hipStream_t s);
+// Per launch slot (kStampSub sub-slots each): add max(end) − min(start) to acc[0] (ticks) and 1 to
+// acc[1] if the slot was used; then zero the n launch slots.
+void stamp_reduce(unsigned long long* slots, long n, unsigned long long* acc, hipStream_t s);
 
 }  // namespace wcb

@@ -46,7 +46,7 @@ struct WcbError : std::runtime_error {
   } while (0)
 
 constexpr int kFrames = 3000, kNCol = 416, kNSamp = 480000;
-constexpr int kXSplit = 4;   // cross-attention key chunks per (row, head): 1500 keys → 4 × 375
+constexpr int kXSplit = 8;   // max cross-attention key chunks per (row, head) (partials buffer size)
 
 int esize(int dt) { return dt == WCB_F32 ? 4 : 2; }
 
@@ -130,6 +130,10 @@ struct wcb_handle {
   hipStream_t sub[kMaxSub] = {};
   hipEvent_t ev_join[kMaxSub] = {};
   int n_sub = 2;   // decode row groups on concurrent streams
+  // Cross-attention: one workgroup per (row, head) over all 1500 keys. Measured (tools/xattn_bench.py,
+  // head-major K/V cycling 12 layers): split-KV hand-offs cost more than they hide at 16-32 rows.
+  int xsplit = 1;
+  int xvariant = 0;  // cross-attention kernel variant (k_attn.hip launch_decode)
   std::map<std::string, std::vector<float>> host_w;
   std::vector<DevBuf> owned;
   bool ready = false;
@@ -161,6 +165,9 @@ struct wcb_handle {
   std::vector<ProfEntry> prof_e;
   std::deque<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
   std::vector<hipEvent_t> ev_pool;
+  DevBuf stamps, stamp_acc;                   // decode cross-attention device stamps (graph nodes)
+  double xattn_bytes = 0, xattn_flops = 0;    // algorithmic work of the stamped launches
+  long stamp_slots() const { return (long)d.n_text_ctx * d.n_layers * kMaxSub; }
 
   int H() const { return d.n_heads; }
   int S() const { return d.n_audio_ctx; }
@@ -295,8 +302,28 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     h->d = *desc;
     h->dt = DType(desc->dtype);
     h->device = device;
-    HIPCHK(hipStreamCreateWithFlags(&h->hs, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&h->he, hipStreamNonBlocking));
+    // The decode chain is latency-bound and the encoder of the next batch runs beside it: decode
+    // streams get the highest priority so their workgroups dispatch ahead of encoder tiles.
+    int prio_lo = 0, prio_hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    const char* pe = getenv("WCB_PRIO");   // 0: all normal, 1: decode high, 2: decode high + encoder low
+    const int pmode = pe ? atoi(pe) : 1;
+    const int dprio = pmode >= 1 ? prio_hi : 0, eprio = pmode >= 2 ? prio_lo : 0;
+    HIPCHK(hipStreamCreateWithPriority(&h->hs, hipStreamNonBlocking, dprio));
+    if (const char* cm = getenv("WCB_ENC_CUS")) {   // experiment: confine the encoder stream to a CU subset
+      int dev_cus = 0;
+      HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, device));
+      const int keep = std::max(1, std::min(atoi(cm), dev_cus));
+      const char* pat = getenv("WCB_ENC_CU_PATTERN");
+      std::vector<uint32_t> mask((dev_cus + 31) / 32, 0u);
+      for (int c = 0; c < dev_cus; ++c) {
+        const bool on = (pat && atoi(pat) == 1) ? c < keep : ((long)(c % 8) * dev_cus / 8 + c / 8) < keep;
+        if (on) mask[c / 32] |= 1u << (c % 32);
+      }
+      HIPCHK(hipExtStreamCreateWithCUMask(&h->he, (uint32_t)mask.size(), mask.data()));
+    } else {
+      HIPCHK(hipStreamCreateWithPriority(&h->he, hipStreamNonBlocking, eprio));
+    }
     for (int i = 0; i < 2; ++i) {
       HIPCHK(hipEventCreateWithFlags(&h->ev_xkv[i], hipEventDisableTiming));
       HIPCHK(hipEventCreateWithFlags(&h->ev_dec[i], hipEventDisableTiming));
@@ -305,10 +332,12 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     HIPCHK(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
     for (int i = 0; i < wcb_handle::kMaxSub; ++i) {
-      HIPCHK(hipStreamCreateWithFlags(&h->sub[i], hipStreamNonBlocking));
+      HIPCHK(hipStreamCreateWithPriority(&h->sub[i], hipStreamNonBlocking, dprio));
       HIPCHK(hipEventCreateWithFlags(&h->ev_join[i], hipEventDisableTiming));
     }
     if (const char* ns = getenv("WCB_DECODE_SPLIT")) h->n_sub = std::max(1, std::min(atoi(ns), (int)wcb_handle::kMaxSub));
+    if (const char* xs = getenv("WCB_XSPLIT")) h->xsplit = std::max(1, std::min(atoi(xs), kXSplit));
+    if (const char* xv = getenv("WCB_XVARIANT")) h->xvariant = atoi(xv);
     // DFT table [416 cols][416 k]: col 2b = win·cos(2πbk/400), col 2b+1 = −win·sin(2πbk/400)
     std::vector<float> dft((size_t)kNCol * kNCol, 0.f);
     for (int c = 0; c < 402; ++c) {
@@ -656,7 +685,7 @@ struct StepCfg {
 // with a KV cache ([tf] modeling_whisper.py:690-795). Every position-dependent quantity is read on
 // the device, so the launch sequence replays as a hipGraph. Row-indexed buffers are addressed with
 // the row offset; the KV caches keep the full-batch layout ([kv][B][H][T][64]).
-void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, hipStream_t st_) {
+void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hipStream_t st_) {
   const int d = h->d.d_model, S = h->S(), H = h->H(), L = h->d.n_layers, B = c.B, T = c.T;
   const size_t e = esize(h->d.dtype);
   int* ints = h->ints.as<int>();
@@ -696,8 +725,13 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, hipStream_t st
     xa.k = xkv; xa.v = xkv + (size_t)B * H * S * 64 * e;
     xa.k_sb = (long)H * S * 64; xa.k_sh = (long)S * 64; xa.k_sk = 64;
     xa.o = datt; xa.ldo = d; xa.o_Sb = 1; xa.B = nb; xa.H = H; xa.nkeys = S;
-    xa.nsplit = kXSplit; xa.part = h->xpart.as<float>() + (size_t)b0 * H * kXSplit * 66;
+    xa.nsplit = h->xsplit; xa.part = h->xpart.as<float>() + (size_t)b0 * H * kXSplit * 66;
     xa.ticket = h->xticket.as<int>() + (size_t)b0 * H;
+    xa.variant = h->xvariant;
+    if (h->prof) {
+      xa.stamp.base = h->stamps.as<unsigned long long>(); xa.stamp.pos = pos;
+      xa.stamp.stride = L * wcb_handle::kMaxSub; xa.stamp.idx = l * wcb_handle::kMaxSub + chain;
+    }
     attention_decode(h->dt, xa, st_);
     GemmArgs xo = rowgemm(datt, d, w.xo_w, nb, d, d, x, d);
     xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st; xo.st_nb = nbk;
@@ -737,13 +771,13 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
   embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, h->dx.as<float>(), h->dstats.as<float>(), B, d, h->hs);
   const int ns = std::max(1, std::min(h->n_sub, B));
   if (ns == 1) {
-    decode_rows(h, c, 0, B, h->hs);
+    decode_rows(h, c, 0, B, 0, h->hs);
   } else {
     HIPCHK(hipEventRecord(h->ev_fork, h->hs));
     for (int i = 0; i < ns; ++i) {
       const int b0 = (int)((long)B * i / ns), b1 = (int)((long)B * (i + 1) / ns);
       HIPCHK(hipStreamWaitEvent(h->sub[i], h->ev_fork, 0));
-      decode_rows(h, c, b0, b1 - b0, h->sub[i]);
+      decode_rows(h, c, b0, b1 - b0, i, h->sub[i]);
       HIPCHK(hipEventRecord(h->ev_join[i], h->sub[i]));
     }
     for (int i = 0; i < ns; ++i) HIPCHK(hipStreamWaitEvent(h->hs, h->ev_join[i], 0));
@@ -845,8 +879,8 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     sc.lm_head = true;
     sc.select = true;
     char key[256];
-    snprintf(key, sizeof key, "%d/%d/%d/%p/%a/%d/%d", B, Tc, out_ld, (const void*)bs, cfg->bias_boost, cfg->min_new_tokens,
-             h->n_sub);
+    snprintf(key, sizeof key, "%d/%d/%d/%p/%a/%d/%d/%d", B, Tc, out_ld, (const void*)bs, cfg->bias_boost,
+             cfg->min_new_tokens, h->n_sub, (int)h->prof);
     const int max_new = cfg->max_new_tokens;
     const int chunk = 8;
     int done = 0, steps = 0;
@@ -875,6 +909,12 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
       }
     });
     if (done <= 0) done = steps;
+    if (h->prof) {   // fold this call's cross-attention stamps into the device accumulator
+      const double launches_rows = (double)(P - 1 + steps) * h->d.n_layers * B * h->H() * h->S();
+      h->xattn_bytes += launches_rows * 64 * 2 * esize(h->d.dtype);
+      h->xattn_flops += launches_rows * 64 * 4;
+      stamp_reduce(h->stamps.as<unsigned long long>(), h->stamp_slots(), h->stamp_acc.as<unsigned long long>(), h->hs);
+    }
     HIPCHK(hipMemcpyAsync(out_ids, h->outbuf.p, (size_t)B * out_ld * 4, hipMemcpyDeviceToDevice, h->hs));
     HIPCHK(hipEventRecord(h->ev_dec[buf], h->hs));
     *out_steps = std::min(done, max_new);
@@ -1030,9 +1070,17 @@ int wcb_debug_copy(wcb_handle* h, const char* name, void* dst, int64_t bytes, in
 int wcb_profile_enable(wcb_handle* h, int enable) {
   return guarded(h, [&] {
     REQUIRE(h, "null handle");
+    quiesce(h);
     h->prof_collect();
     h->prof = enable != 0;
     h->prof_e.clear();
+    h->xattn_bytes = h->xattn_flops = 0;
+    if (h->prof) {
+      h->stamps.ensure((size_t)h->stamp_slots() * 16 * kStampSub);
+      h->stamp_acc.ensure(16);
+      HIPCHK(hipMemset(h->stamps.p, 0, (size_t)h->stamp_slots() * 16 * kStampSub));
+      HIPCHK(hipMemset(h->stamp_acc.p, 0, 16));
+    }
   });
 }
 
@@ -1041,6 +1089,18 @@ int wcb_profile_read(wcb_handle* h, int n, char (*names)[32], int64_t* launches,
   const int rc = guarded(h, [&] {
     REQUIRE(h, "null handle");
     h->prof_collect();
+    if (h->prof && h->stamp_acc.p) {   // decode cross-attention: device-stamped launches
+      quiesce(h);
+      unsigned long long acc[2] = {0, 0};
+      HIPCHK(hipMemcpy(acc, h->stamp_acc.p, 16, hipMemcpyDeviceToHost));
+      if (acc[1]) {
+        const int id = h->prof_id("dec_xattn");
+        h->prof_e[id].launches = (int64_t)acc[1];
+        h->prof_e[id].ms = (double)acc[0] / 1e5;   // 100 MHz s_memrealtime ticks
+        h->prof_e[id].bytes = h->xattn_bytes;
+        h->prof_e[id].flops = h->xattn_flops;
+      }
+    }
     for (size_t i = 0; i < h->prof_e.size() && (int)i < n; ++i) {
       snprintf(names[i], 32, "%s", h->prof_e[i].name.c_str());
       launches[i] = h->prof_e[i].launches;
@@ -1083,6 +1143,28 @@ int wcb_op_layernorm(int dtype, const float* x, const float* w, const float* b, 
   return guarded(nullptr, [&] {
     REQUIRE(x && w && b && y && M > 0 && d > 0 && d % 64 == 0 && d <= 2048, "bad argument");
     layernorm(DType(dtype), x, w, b, y, M, d, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H, int Sk,
+                            int nsplit, int variant, void* stream) {
+  return guarded(nullptr, [&] {
+    REQUIRE(q && k && v && o && B > 0 && H > 0 && Sk > 0 && Sk <= 2048 && nsplit >= 1 && nsplit <= 64, "bad argument");
+    AttnArgs a;   // decode layout: q/o [B][H·64], K/V head-major [B][H][Sk][64] (the cross-K/V layout)
+    a.q = q; a.ldq = (long)H * 64; a.q_Sb = 1; a.Sq = 1;
+    a.k = k; a.v = v; a.k_sb = (long)H * Sk * 64; a.k_sh = (long)Sk * 64; a.k_sk = 64;
+    a.o = o; a.ldo = (long)H * 64; a.o_Sb = 1; a.B = B; a.H = H; a.nkeys = Sk;
+    a.variant = variant;
+    static DevBuf part, ticket;
+    if (nsplit > 1) {
+      a.nsplit = nsplit;
+      part.ensure((size_t)B * H * nsplit * 66 * 4);
+      ticket.ensure((size_t)B * H * 4);
+      a.part = part.as<float>();
+      a.ticket = ticket.as<int>();
+    }
+    attention_decode(DType(dtype), a, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
   });
 }

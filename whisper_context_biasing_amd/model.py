@@ -70,12 +70,13 @@ class BiasList:
         _lib.check(lib.wcb_bias_create(model._h, toks.ctypes.data, offs.ctypes.data, len(phrases),
                                        C.byref(h)), model._h, "wcb_bias_create")
         self._h = h
+        self._lib = lib   # held so the destructor still works during interpreter shutdown
         self.n_phrases = len(phrases)
         self.n_states = lib.wcb_bias_num_states(h)
 
     def __del__(self):
-        if getattr(self, "_h", None):
-            _lib.load().wcb_bias_destroy(self._h)
+        if getattr(self, "_h", None) and getattr(self, "_lib", None) is not None:
+            self._lib.wcb_bias_destroy(self._h)
             self._h = None
 
 

@@ -1,0 +1,85 @@
+"""Utterance sharding across ranks (one process per GPU).
+
+The reference evaluates on one device (`scripts/evaluation.py:185-200`, `Seq2SeqTrainer`); clips
+are independent, so N GPUs take disjoint shards of the utterance list and never exchange data on the
+decode path. The only collectives are a one-time weight broadcast (RCCL over xGMI on the GPU box,
+`gloo` in the CPU tests) and the max-over-ranks of the wall time in `bench.py`.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .config import WhisperDims
+from .weights import make_weights, param_shapes
+
+
+def shard_bounds(n_items: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous, balanced [lo, hi) slice of `n_items` for `rank` (sizes differ by at most 1)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} / world {world}")
+    lo = n_items * rank // world
+    hi = n_items * (rank + 1) // world
+    return lo, hi
+
+
+def pack_state_dict(dims: WhisperDims, sd: Dict[str, np.ndarray], dtype=torch.bfloat16) -> torch.Tensor:
+    """All parameters in `param_shapes` order as one flat tensor (one collective moves them all)."""
+    return torch.cat([torch.as_tensor(np.asarray(sd[n], dtype=np.float32)).reshape(-1)
+                      for n, _ in param_shapes(dims)]).to(dtype)
+
+
+def unpack_state_dict(dims: WhisperDims, flat: torch.Tensor) -> Dict[str, np.ndarray]:
+    host = flat.float().cpu().numpy()
+    out, off = {}, 0
+    for n, shape in param_shapes(dims):
+        k = int(np.prod(shape))
+        out[n] = host[off:off + k].reshape(shape)
+        off += k
+    if off != host.size:
+        raise ValueError(f"packed blob has {host.size} elements, parameters need {off}")
+    return out
+
+
+def broadcast_weights(dims: WhisperDims, device: torch.device, seed: int = 0, src: int = 0,
+                      dtype=torch.bfloat16) -> Dict[str, np.ndarray]:
+    """Rank `src` materialises the seeded weights; one broadcast of the packed blob to every rank.
+    Without an initialised process group this is just the local materialisation."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    n_el = sum(int(np.prod(s)) for _, s in param_shapes(dims))
+    if rank == src:
+        flat = pack_state_dict(dims, make_weights(dims, seed=seed), dtype).to(device)
+    else:
+        flat = torch.empty(n_el, dtype=dtype, device=device)
+    if world > 1:
+        dist.broadcast(flat, src=src)
+    return unpack_state_dict(dims, flat)
+
+
+def max_over_ranks(value: float, device: torch.device) -> float:
+    """The slowest rank's time (bench.py reports whole-job throughput against it)."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_shards(local: torch.Tensor, device: torch.device) -> List[torch.Tensor]:
+    """Collect every rank's result rows (evaluation-time convenience; not on the timed path)."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return [local]
+    world = dist.get_world_size()
+    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    mx = int(max(int(x.item()) for x in ns))
+    pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=device)
+    pad[:local.shape[0]] = local.to(device)
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad)
+    return [b[:int(k.item())] for b, k in zip(bufs, ns)]
