@@ -99,7 +99,10 @@ int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets
 void wcb_bias_destroy(wcb_bias* b);
 int wcb_bias_num_states(const wcb_bias* b);
 
-/* per-kernel time accounting for the benchmark's roofline (HIP events on the launch stream) */
+/* per-kernel time accounting for the benchmark's roofline. enable bit 0: HIP events around every
+ * front-end / encoder launch on its stream; bit 1: device time stamps (s_memrealtime) written by the
+ * decode cross-attention kernel, which runs inside the replayed step graph where events cannot
+ * bracket a single node. 0 disables; counters are reset. */
 int wcb_profile_enable(wcb_handle* h, int enable);
 /* fills up to n entries: name, launches, total milliseconds, algorithmic flops, algorithmic bytes */
 int wcb_profile_read(wcb_handle* h, int n, char (*names)[32], int64_t* launches, double* ms,

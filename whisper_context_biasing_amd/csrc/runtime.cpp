@@ -116,20 +116,38 @@ struct wcb_bias {
   DevBuf root_bits, root_child, trans_off, trans_tok, trans_dst;
 };
 
+// Decode state of one in-flight generate call. Two contexts (one per cross-K/V buffer) let call
+// i+1 decode on its own stream while call i is still decoding: two latency-bound step chains share
+// the GPU instead of one.
+struct DecCtx {
+  static constexpr int kMaxSub = 4;
+  hipStream_t hs = nullptr;                     // decode stream of this context
+  hipStream_t sub[kMaxSub] = {};                // row-group chains (fork/join inside the step graph)
+  hipEvent_t ev_fork = nullptr, ev_join[kMaxSub] = {};
+  int dec_B = 0, dec_T = 0;
+  DevBuf kvself, dx, dh, dq, datt, dffn, dstats, xpart, xticket, logits, part_val, part_idx, ints, outbuf, forced;
+  int nchunk = 64;
+  hipGraphExec_t gexec = nullptr;               // captured decode step
+  std::string gkey;
+};
+
 struct wcb_handle {
   wcb_model_desc d{};
   DType dt = kBF16;
   int device = 0;
   std::string err;
-  hipStream_t hs = nullptr;   // decode stream
   hipStream_t he = nullptr;   // front end + encoder + cross-K/V stream (overlaps the previous batch's decode)
-  hipEvent_t ev_xkv[2] = {}, ev_dec[2] = {};   // cross-K/V buffer k written / decode reading it done
+  // Decode contexts in flight: call i decodes in context i % nctx from cross-K/V buffer i % nctx while
+  // the encoder stream already works on the next call. Measured: 2 contexts, one chain each.
+  static constexpr int kMaxCtx = 4;
+  int nctx = 2;
+  hipEvent_t ev_xkv[kMaxCtx] = {}, ev_dec[kMaxCtx] = {};   // cross-K/V buffer k written / decode reading it done
   int gen_count = 0;
-  hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr;
-  static constexpr int kMaxSub = 4;
-  hipStream_t sub[kMaxSub] = {};
-  hipEvent_t ev_join[kMaxSub] = {};
-  int n_sub = 2;   // decode row groups on concurrent streams
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  static constexpr int kMaxSub = DecCtx::kMaxSub;
+  DecCtx dc[kMaxCtx];
+  int n_sub = 1;   // row groups per decode step on concurrent streams (fork/join inside the graph);
+                   // with two decode contexts in flight one chain each measured best
   // Cross-attention: one workgroup per (row, head) over all 1500 keys. Measured (tools/xattn_bench.py,
   // head-major K/V cycling 12 layers): split-KV hand-offs cost more than they hide at 16-32 rows.
   int xsplit = 1;
@@ -151,23 +169,18 @@ struct wcb_handle {
   // encoder workspace
   int enc_B = 0;
   DevBuf xt, hbuf, x, h, qkv, att, ffn, encout;
-  // decoder workspace
-  int dec_B = 0, dec_T = 0;
-  DevBuf xkv2[2], kvself, dx, dh, dq, datt, dffn, dstats, xpart, xticket, logits, part_val, part_idx, ints, outbuf, forced;
-  int nchunk = 64;
-  // graph cache
-  hipGraphExec_t gexec[2] = {};   // one captured decode step per cross-K/V buffer
-  std::string gkey[2];
+  // cross-K/V, double-buffered (buffer k is read by decode context k)
+  DevBuf xkv2[kMaxCtx];
   // default (empty) bias automaton
   std::unique_ptr<wcb_bias> empty_bias;
   // profiling
-  bool prof = false;
+  bool prof = false, prof_stamps = false;
   std::vector<ProfEntry> prof_e;
   std::deque<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
   std::vector<hipEvent_t> ev_pool;
   DevBuf stamps, stamp_acc;                   // decode cross-attention device stamps (graph nodes)
   double xattn_bytes = 0, xattn_flops = 0;    // algorithmic work of the stamped launches
-  long stamp_slots() const { return (long)d.n_text_ctx * d.n_layers * kMaxSub; }
+  long stamp_slots() const { return (long)d.n_text_ctx * d.n_layers * kMaxSub; }   // per context
 
   int H() const { return d.n_heads; }
   int S() const { return d.n_audio_ctx; }
@@ -304,38 +317,29 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     h->device = device;
     // The decode chain is latency-bound and the encoder of the next batch runs beside it: decode
     // streams get the highest priority so their workgroups dispatch ahead of encoder tiles.
+    if (const char* ns = getenv("WCB_DECODE_SPLIT")) h->n_sub = std::max(1, std::min(atoi(ns), (int)wcb_handle::kMaxSub));
     int prio_lo = 0, prio_hi = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     const char* pe = getenv("WCB_PRIO");   // 0: all normal, 1: decode high, 2: decode high + encoder low
     const int pmode = pe ? atoi(pe) : 1;
     const int dprio = pmode >= 1 ? prio_hi : 0, eprio = pmode >= 2 ? prio_lo : 0;
-    HIPCHK(hipStreamCreateWithPriority(&h->hs, hipStreamNonBlocking, dprio));
-    if (const char* cm = getenv("WCB_ENC_CUS")) {   // experiment: confine the encoder stream to a CU subset
-      int dev_cus = 0;
-      HIPCHK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, device));
-      const int keep = std::max(1, std::min(atoi(cm), dev_cus));
-      const char* pat = getenv("WCB_ENC_CU_PATTERN");
-      std::vector<uint32_t> mask((dev_cus + 31) / 32, 0u);
-      for (int c = 0; c < dev_cus; ++c) {
-        const bool on = (pat && atoi(pat) == 1) ? c < keep : ((long)(c % 8) * dev_cus / 8 + c / 8) < keep;
-        if (on) mask[c / 32] |= 1u << (c % 32);
+    HIPCHK(hipStreamCreateWithPriority(&h->he, hipStreamNonBlocking, eprio));
+    if (const char* nc = getenv("WCB_DECODE_CTX")) h->nctx = std::max(1, std::min(atoi(nc), (int)wcb_handle::kMaxCtx));
+    for (int ci = 0; ci < h->nctx; ++ci) {
+      DecCtx& D = h->dc[ci];
+      HIPCHK(hipStreamCreateWithPriority(&D.hs, hipStreamNonBlocking, dprio));
+      HIPCHK(hipEventCreateWithFlags(&D.ev_fork, hipEventDisableTiming));
+      for (int i = 0; i < DecCtx::kMaxSub && h->n_sub > 1; ++i) {   // row-group streams only when used
+        HIPCHK(hipStreamCreateWithPriority(&D.sub[i], hipStreamNonBlocking, dprio));
+        HIPCHK(hipEventCreateWithFlags(&D.ev_join[i], hipEventDisableTiming));
       }
-      HIPCHK(hipExtStreamCreateWithCUMask(&h->he, (uint32_t)mask.size(), mask.data()));
-    } else {
-      HIPCHK(hipStreamCreateWithPriority(&h->he, hipStreamNonBlocking, eprio));
     }
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < h->nctx; ++i) {
       HIPCHK(hipEventCreateWithFlags(&h->ev_xkv[i], hipEventDisableTiming));
       HIPCHK(hipEventCreateWithFlags(&h->ev_dec[i], hipEventDisableTiming));
     }
     HIPCHK(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-    for (int i = 0; i < wcb_handle::kMaxSub; ++i) {
-      HIPCHK(hipStreamCreateWithPriority(&h->sub[i], hipStreamNonBlocking, dprio));
-      HIPCHK(hipEventCreateWithFlags(&h->ev_join[i], hipEventDisableTiming));
-    }
-    if (const char* ns = getenv("WCB_DECODE_SPLIT")) h->n_sub = std::max(1, std::min(atoi(ns), (int)wcb_handle::kMaxSub));
     if (const char* xs = getenv("WCB_XSPLIT")) h->xsplit = std::max(1, std::min(atoi(xs), kXSplit));
     if (const char* xv = getenv("WCB_XVARIANT")) h->xvariant = atoi(xv);
     // DFT table [416 cols][416 k]: col 2b = win·cos(2πbk/400), col 2b+1 = −win·sin(2πbk/400)
@@ -390,23 +394,28 @@ void wcb_destroy(wcb_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
-  for (auto& g : h->gexec) if (g) (void)hipGraphExecDestroy(g);
+  for (DecCtx& D : h->dc) {
+    if (D.gexec) (void)hipGraphExecDestroy(D.gexec);
+    for (DevBuf* b : {&D.kvself, &D.dx, &D.dh, &D.dq, &D.datt, &D.dffn, &D.dstats, &D.xpart, &D.xticket, &D.logits,
+                      &D.part_val, &D.part_idx, &D.ints, &D.outbuf, &D.forced})
+      b->release();
+    if (D.ev_fork) (void)hipEventDestroy(D.ev_fork);
+    for (int i = 0; i < DecCtx::kMaxSub; ++i) {
+      if (D.ev_join[i]) (void)hipEventDestroy(D.ev_join[i]);
+      if (D.sub[i]) (void)hipStreamDestroy(D.sub[i]);
+    }
+    if (D.hs) (void)hipStreamDestroy(D.hs);
+  }
   for (auto& b : h->owned) b.release();
   for (DevBuf* b : {&h->dft, &h->mel_lo, &h->mel_hi, &h->mel_w, &h->clip_max, &h->xt, &h->hbuf, &h->x, &h->h,
-                    &h->qkv, &h->att, &h->ffn, &h->encout, &h->xkv2[0], &h->xkv2[1], &h->kvself, &h->dx, &h->dh, &h->dq,
-                    &h->datt, &h->dffn, &h->logits, &h->part_val, &h->part_idx, &h->ints, &h->outbuf, &h->forced})
+                    &h->qkv, &h->att, &h->ffn, &h->encout, &h->stamps, &h->stamp_acc})
     b->release();
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   if (h->ev_out) (void)hipEventDestroy(h->ev_out);
-  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-  for (int i = 0; i < wcb_handle::kMaxSub; ++i) {
-    if (h->ev_join[i]) (void)hipEventDestroy(h->ev_join[i]);
-    if (h->sub[i]) (void)hipStreamDestroy(h->sub[i]);
-  }
-  if (h->hs) (void)hipStreamDestroy(h->hs);
   if (h->he) (void)hipStreamDestroy(h->he);
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < wcb_handle::kMaxCtx; ++i) {
+    h->xkv2[i].release();
     if (h->ev_xkv[i]) (void)hipEventDestroy(h->ev_xkv[i]);
     if (h->ev_dec[i]) (void)hipEventDestroy(h->ev_dec[i]);
   }
@@ -536,10 +545,11 @@ void sync_out(wcb_handle* h, void* stream, hipStream_t from) {
   HIPCHK(hipStreamWaitEvent((hipStream_t)stream, h->ev_out, 0));
   HIPCHK(hipGetLastError());
 }
-// drain both library streams (before any workspace reallocation)
+// drain every library stream (before any workspace reallocation)
 void quiesce(wcb_handle* h) {
   HIPCHK(hipStreamSynchronize(h->he));
-  HIPCHK(hipStreamSynchronize(h->hs));
+  for (DecCtx& D : h->dc)
+    if (D.hs) HIPCHK(hipStreamSynchronize(D.hs));
 }
 
 void ensure_enc_ws(wcb_handle* h, int B) {
@@ -625,43 +635,46 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
 enum { I_STEP = 0, I_POS = 1, I_DONE = 2, I_TICKET = 3, I_UNFIN = 4, I_NEXT = 16 };
 
 void drop_graphs(wcb_handle* h) {
-  for (int i = 0; i < 2; ++i) {
-    if (h->gexec[i]) (void)hipGraphExecDestroy(h->gexec[i]);
-    h->gexec[i] = nullptr;
-    h->gkey[i].clear();
+  for (DecCtx& D : h->dc) {
+    if (D.gexec) (void)hipGraphExecDestroy(D.gexec);
+    D.gexec = nullptr;
+    D.gkey.clear();
   }
 }
 
 void ensure_dec_ws(wcb_handle* h, int B, int T, int out_ld) {
   const size_t e = esize(h->d.dtype), d = h->d.d_model, L = h->d.n_layers, S = h->S();
+  const DecCtx& D0 = h->dc[h->nctx - 1];   // every context is sized together
   const size_t need[] = {2 * L * (size_t)B * S * d * e, 2 * L * (size_t)B * T * d * e, (size_t)B * d * 4,
                          (size_t)B * h->d.ffn * e, (size_t)B * h->d.vocab * 4, (size_t)(I_NEXT + 3 * B + 16) * 4,
                          (size_t)B * out_ld * 4};
-  const DevBuf* have[] = {&h->xkv2[1], &h->kvself, &h->dx, &h->dffn, &h->logits, &h->ints, &h->outbuf};
+  const DevBuf* have[] = {&h->xkv2[h->nctx - 1], &D0.kvself, &D0.dx, &D0.dffn, &D0.logits, &D0.ints, &D0.outbuf};
   bool grow = false;
   for (int i = 0; i < 7; ++i) grow |= need[i] > have[i]->bytes;
-  if (!grow && B <= h->dec_B && T <= h->dec_T) return;
+  if (!grow && B <= D0.dec_B && T <= D0.dec_T) return;
   quiesce(h);
   drop_graphs(h);
-  h->xkv2[0].ensure(need[0]);
-  h->xkv2[1].ensure(need[0]);
-  h->kvself.ensure(need[1]);
-  h->dec_B = std::max(h->dec_B, B);
-  h->dec_T = std::max(h->dec_T, T);
-  h->dx.ensure((size_t)B * d * 4);
-  h->dh.ensure((size_t)B * d * e);
-  h->dq.ensure((size_t)B * d * e);
-  h->datt.ensure((size_t)B * d * e);
-  h->dffn.ensure((size_t)B * h->d.ffn * e);
-  h->dstats.ensure((size_t)B * (d / 16) * 2 * 4);
-  h->xpart.ensure((size_t)B * h->H() * kXSplit * 66 * 4);
-  h->xticket.ensure((size_t)B * h->H() * 4);     // zeroed on allocation; combiners reset their slot
-  h->logits.ensure((size_t)B * h->d.vocab * 4);
-  h->nchunk = (h->d.vocab + 63) / 64;      // one argmax partial per LM-head workgroup (64 columns)
-  h->part_val.ensure((size_t)B * h->nchunk * 4);
-  h->part_idx.ensure((size_t)B * h->nchunk * 4);
-  h->ints.ensure(need[5]);
-  h->outbuf.ensure(need[6]);
+  for (int ci = 0; ci < h->nctx; ++ci) {
+    DecCtx& D = h->dc[ci];
+    h->xkv2[ci].ensure(need[0]);
+    D.kvself.ensure(need[1]);
+    D.dec_B = std::max(D.dec_B, B);
+    D.dec_T = std::max(D.dec_T, T);
+    D.dx.ensure((size_t)B * d * 4);
+    D.dh.ensure((size_t)B * d * e);
+    D.dq.ensure((size_t)B * d * e);
+    D.datt.ensure((size_t)B * d * e);
+    D.dffn.ensure((size_t)B * h->d.ffn * e);
+    D.dstats.ensure((size_t)B * (d / 16) * 2 * 4);
+    D.xpart.ensure((size_t)B * h->H() * kXSplit * 66 * 4);
+    D.xticket.ensure((size_t)B * h->H() * 4);     // zeroed on allocation; combiners reset their slot
+    D.logits.ensure((size_t)B * h->d.vocab * 4);
+    D.nchunk = (h->d.vocab + 63) / 64;      // one argmax partial per LM-head workgroup (64 columns)
+    D.part_val.ensure((size_t)B * D.nchunk * 4);
+    D.part_idx.ensure((size_t)B * D.nchunk * 4);
+    D.ints.ensure(need[5]);
+    D.outbuf.ensure(need[6]);
+  }
 }
 
 // cross-attention K/V of every decoder layer from the encoder output (A4), once per clip:
@@ -686,21 +699,22 @@ struct StepCfg {
 // the device, so the launch sequence replays as a hipGraph. Row-indexed buffers are addressed with
 // the row offset; the KV caches keep the full-batch layout ([kv][B][H][T][64]).
 void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hipStream_t st_) {
+  DecCtx& D = h->dc[c.buf];
   const int d = h->d.d_model, S = h->S(), H = h->H(), L = h->d.n_layers, B = c.B, T = c.T;
   const size_t e = esize(h->d.dtype);
-  int* ints = h->ints.as<int>();
+  int* ints = D.ints.as<int>();
   int* pos = ints + I_POS;
-  float* x = h->dx.as<float>() + (size_t)b0 * d;
+  float* x = D.dx.as<float>() + (size_t)b0 * d;
   const int nbk = d / 16;
-  float* st = h->dstats.as<float>() + (size_t)b0 * nbk * 2;
-  char* dq = (char*)h->dq.p + (size_t)b0 * d * e;
-  char* datt = (char*)h->datt.p + (size_t)b0 * d * e;
-  char* dffn = (char*)h->dffn.p + (size_t)b0 * h->d.ffn * e;
+  float* st = D.dstats.as<float>() + (size_t)b0 * nbk * 2;
+  char* dq = (char*)D.dq.p + (size_t)b0 * d * e;
+  char* datt = (char*)D.datt.p + (size_t)b0 * d * e;
+  char* dffn = (char*)D.dffn.p + (size_t)b0 * h->d.ffn * e;
   const size_t cache_l = 2 * (size_t)B * H * T * 64;   // elements per layer (K then V)
   const size_t xkv_l = 2 * (size_t)B * H * S * 64;
   for (int l = 0; l < L; ++l) {
     const LayerW& w = h->dec[l];
-    char* cache = (char*)h->kvself.p + (l * cache_l + (size_t)b0 * H * T * 64) * e;
+    char* cache = (char*)D.kvself.p + (l * cache_l + (size_t)b0 * H * T * 64) * e;
     GemmArgs q = rowgemm(x, d, w.qkv_w, nb, 3 * d, d, dq, d);   // LayerNorm fused (f32 A rows)
     q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nbk;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
@@ -725,11 +739,12 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     xa.k = xkv; xa.v = xkv + (size_t)B * H * S * 64 * e;
     xa.k_sb = (long)H * S * 64; xa.k_sh = (long)S * 64; xa.k_sk = 64;
     xa.o = datt; xa.ldo = d; xa.o_Sb = 1; xa.B = nb; xa.H = H; xa.nkeys = S;
-    xa.nsplit = h->xsplit; xa.part = h->xpart.as<float>() + (size_t)b0 * H * kXSplit * 66;
-    xa.ticket = h->xticket.as<int>() + (size_t)b0 * H;
+    xa.nsplit = h->xsplit; xa.part = D.xpart.as<float>() + (size_t)b0 * H * kXSplit * 66;
+    xa.ticket = D.xticket.as<int>() + (size_t)b0 * H;
     xa.variant = h->xvariant;
-    if (h->prof) {
-      xa.stamp.base = h->stamps.as<unsigned long long>(); xa.stamp.pos = pos;
+    if (h->prof_stamps) {
+      xa.stamp.base = h->stamps.as<unsigned long long>() + (size_t)c.buf * h->stamp_slots() * 2 * kStampSub;
+      xa.stamp.pos = pos;
       xa.stamp.stride = L * wcb_handle::kMaxSub; xa.stamp.idx = l * wcb_handle::kMaxSub + chain;
     }
     attention_decode(h->dt, xa, st_);
@@ -750,8 +765,8 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b; lm.st_in = st; lm.st_nb = nbk;
     lm.out_f32 = 1;
     if (c.select) {   // argmax partials with the root boost + EOS mask fused into the LM head
-      lm.sel_val = h->part_val.as<float>() + (size_t)b0 * h->nchunk;
-      lm.sel_idx = h->part_idx.as<int>() + (size_t)b0 * h->nchunk;
+      lm.sel_val = D.part_val.as<float>() + (size_t)b0 * D.nchunk;
+      lm.sel_idx = D.part_idx.as<int>() + (size_t)b0 * D.nchunk;
       lm.sel_root_bits = c.bias->root_bits.as<uint32_t>(); lm.sel_lam = c.lam;
       lm.sel_eos = h->d.eos_token_id; lm.sel_step = ints + I_STEP; lm.sel_min_new = c.min_new;
     }
@@ -764,23 +779,24 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
 // the latency-bound projections of one group overlap the HBM-bound cross-attention of another;
 // token selection (or teacher forcing) joins them.
 void decode_step(wcb_handle* h, const StepCfg& c) {
+  DecCtx& D = h->dc[c.buf];
   const int d = h->d.d_model, B = c.B;
-  int* ints = h->ints.as<int>();
+  int* ints = D.ints.as<int>();
   int* pos = ints + I_POS;
   int* next_ids = ints + I_NEXT;
-  embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, h->dx.as<float>(), h->dstats.as<float>(), B, d, h->hs);
+  embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, D.dx.as<float>(), D.dstats.as<float>(), B, d, D.hs);
   const int ns = std::max(1, std::min(h->n_sub, B));
   if (ns == 1) {
-    decode_rows(h, c, 0, B, 0, h->hs);
+    decode_rows(h, c, 0, B, 0, D.hs);
   } else {
-    HIPCHK(hipEventRecord(h->ev_fork, h->hs));
+    HIPCHK(hipEventRecord(D.ev_fork, D.hs));
     for (int i = 0; i < ns; ++i) {
       const int b0 = (int)((long)B * i / ns), b1 = (int)((long)B * (i + 1) / ns);
-      HIPCHK(hipStreamWaitEvent(h->sub[i], h->ev_fork, 0));
-      decode_rows(h, c, b0, b1 - b0, i, h->sub[i]);
-      HIPCHK(hipEventRecord(h->ev_join[i], h->sub[i]));
+      HIPCHK(hipStreamWaitEvent(D.sub[i], D.ev_fork, 0));
+      decode_rows(h, c, b0, b1 - b0, i, D.sub[i]);
+      HIPCHK(hipEventRecord(D.ev_join[i], D.sub[i]));
     }
-    for (int i = 0; i < ns; ++i) HIPCHK(hipStreamWaitEvent(h->hs, h->ev_join[i], 0));
+    for (int i = 0; i < ns; ++i) HIPCHK(hipStreamWaitEvent(D.hs, D.ev_join[i], 0));
   }
   if (c.select) {
     SelectArgs s;
@@ -792,13 +808,13 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     s.state = next_ids + B; s.finished = next_ids + 2 * B;
     s.eos = h->d.eos_token_id; s.pad = h->d.pad_token_id; s.min_new = c.min_new;
     s.step = ints + I_STEP; s.pos = pos; s.next_ids = next_ids;
-    s.out_ids = h->outbuf.as<int>(); s.out_ld = c.out_ld;
-    s.part_val = h->part_val.as<float>(); s.part_idx = h->part_idx.as<int>(); s.nchunk = h->nchunk;
+    s.out_ids = D.outbuf.as<int>(); s.out_ld = c.out_ld;
+    s.part_val = D.part_val.as<float>(); s.part_idx = D.part_idx.as<int>(); s.nchunk = D.nchunk;
     s.all_done = ints + I_DONE;
     s.ticket = ints + I_TICKET; s.unfinished = ints + I_UNFIN;
-    select_finalize(s, h->hs);
+    select_finalize(s, D.hs);
   } else {
-    advance_forced(next_ids, c.forced, B, c.forced_ld, pos, h->hs);
+    advance_forced(next_ids, c.forced, B, c.forced_ld, pos, D.hs);
   }
 }
 
@@ -853,7 +869,8 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     const int Tc = std::min(T, h->d.n_text_ctx);
     ensure_enc_ws(h, B);
     ensure_dec_ws(h, B, Tc, out_ld);
-    const int buf = h->gen_count++ & 1;
+    const int buf = h->gen_count++ % h->nctx;
+    DecCtx& D = h->dc[buf];
     // ---- encoder stream: front end → encoder → cross-K/V into buffer `buf` once the decode that
     //      last read that buffer has finished. It overlaps the previous call's decode.
     sync_in(h, stream, h->he);
@@ -862,63 +879,64 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     h->timed("xkv_gemm_total", 0, 0, h->he, [&] { cross_kv(h, B, buf); });
     HIPCHK(hipEventRecord(h->ev_xkv[buf], h->he));
     // ---- decode stream
-    HIPCHK(hipStreamWaitEvent(h->hs, h->ev_xkv[buf], 0));
-    int* ints = h->ints.as<int>();
-    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 3 * B) * 4, h->hs));
+    HIPCHK(hipStreamWaitEvent(D.hs, h->ev_xkv[buf], 0));
+    int* ints = D.ints.as<int>();
+    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 3 * B) * 4, D.hs));
     if (prefix) {
-      if ((size_t)B * P * 4 > h->forced.bytes) { quiesce(h); h->forced.ensure((size_t)B * P * 4); }
+      if ((size_t)B * P * 4 > D.forced.bytes) { quiesce(h); D.forced.ensure((size_t)B * P * 4); }
       for (int b = 0; b < B; ++b)
-        HIPCHK(hipMemcpyAsync(h->forced.as<int>() + (size_t)b * P, prefix, (size_t)P * 4, hipMemcpyHostToDevice, h->hs));
-      gather_col(ints + I_NEXT, h->forced.as<int>(), B, P, 0, h->hs);
+        HIPCHK(hipMemcpyAsync(D.forced.as<int>() + (size_t)b * P, prefix, (size_t)P * 4, hipMemcpyHostToDevice, D.hs));
+      gather_col(ints + I_NEXT, D.forced.as<int>(), B, P, 0, D.hs);
     } else {
-      fill_i32(ints + I_NEXT, h->d.decoder_start_token_id, B, h->hs);
+      fill_i32(ints + I_NEXT, h->d.decoder_start_token_id, B, D.hs);
     }
-    StepCfg sc{B, Tc, out_ld, buf, false, false, h->logits.as<float>(), (long)h->d.vocab, bs, cfg->bias_boost,
-               cfg->min_new_tokens, h->forced.as<int>(), P};
+    StepCfg sc{B, Tc, out_ld, buf, false, false, D.logits.as<float>(), (long)h->d.vocab, bs, cfg->bias_boost,
+               cfg->min_new_tokens, D.forced.as<int>(), P};
     for (int p = 0; p + 1 < P; ++p) decode_step(h, sc);   // prompt prefill, teacher-forced
     sc.lm_head = true;
     sc.select = true;
     char key[256];
     snprintf(key, sizeof key, "%d/%d/%d/%p/%a/%d/%d/%d", B, Tc, out_ld, (const void*)bs, cfg->bias_boost,
-             cfg->min_new_tokens, h->n_sub, (int)h->prof);
+             cfg->min_new_tokens, h->n_sub, (int)h->prof_stamps);
     const int max_new = cfg->max_new_tokens;
     const int chunk = 8;
     int done = 0, steps = 0;
-    if (cfg->use_graph && (!h->gexec[buf] || h->gkey[buf] != key)) {
-      if (h->gexec[buf]) { (void)hipGraphExecDestroy(h->gexec[buf]); h->gexec[buf] = nullptr; }
+    if (cfg->use_graph && (!D.gexec || D.gkey != key)) {
+      if (D.gexec) { (void)hipGraphExecDestroy(D.gexec); D.gexec = nullptr; }
       hipGraph_t graph;
-      HIPCHK(hipStreamBeginCapture(h->hs, hipStreamCaptureModeThreadLocal));
+      HIPCHK(hipStreamBeginCapture(D.hs, hipStreamCaptureModeThreadLocal));
       decode_step(h, sc);
-      HIPCHK(hipStreamEndCapture(h->hs, &graph));
-      HIPCHK(hipGraphInstantiate(&h->gexec[buf], graph, nullptr, nullptr, 0));
+      HIPCHK(hipStreamEndCapture(D.hs, &graph));
+      HIPCHK(hipGraphInstantiate(&D.gexec, graph, nullptr, nullptr, 0));
       HIPCHK(hipGraphDestroy(graph));
-      h->gkey[buf] = key;
+      D.gkey = key;
     }
-    h->timed("decode_loop", 0, 0, h->hs, [&] {
+    h->timed("decode_loop", 0, 0, D.hs, [&] {
       while (steps < max_new) {
         const int n = std::min(chunk, max_new - steps);
         for (int i = 0; i < n; ++i) {
-          if (cfg->use_graph) HIPCHK(hipGraphLaunch(h->gexec[buf], h->hs));
+          if (cfg->use_graph) HIPCHK(hipGraphLaunch(D.gexec, D.hs));
           else decode_step(h, sc);
         }
         steps += n;
         if (fixed_len) continue;
-        HIPCHK(hipMemcpyAsync(&done, ints + I_DONE, 4, hipMemcpyDeviceToHost, h->hs));
-        HIPCHK(hipStreamSynchronize(h->hs));
+        HIPCHK(hipMemcpyAsync(&done, ints + I_DONE, 4, hipMemcpyDeviceToHost, D.hs));
+        HIPCHK(hipStreamSynchronize(D.hs));
         if (done > 0) break;
       }
     });
     if (done <= 0) done = steps;
-    if (h->prof) {   // fold this call's cross-attention stamps into the device accumulator
+    if (h->prof_stamps) {   // fold this call's cross-attention stamps into the device accumulator
       const double launches_rows = (double)(P - 1 + steps) * h->d.n_layers * B * h->H() * h->S();
       h->xattn_bytes += launches_rows * 64 * 2 * esize(h->d.dtype);
       h->xattn_flops += launches_rows * 64 * 4;
-      stamp_reduce(h->stamps.as<unsigned long long>(), h->stamp_slots(), h->stamp_acc.as<unsigned long long>(), h->hs);
+      stamp_reduce(h->stamps.as<unsigned long long>() + (size_t)buf * h->stamp_slots() * 2 * kStampSub, h->stamp_slots(),
+                   h->stamp_acc.as<unsigned long long>(), D.hs);
     }
-    HIPCHK(hipMemcpyAsync(out_ids, h->outbuf.p, (size_t)B * out_ld * 4, hipMemcpyDeviceToDevice, h->hs));
-    HIPCHK(hipEventRecord(h->ev_dec[buf], h->hs));
+    HIPCHK(hipMemcpyAsync(out_ids, D.outbuf.p, (size_t)B * out_ld * 4, hipMemcpyDeviceToDevice, D.hs));
+    HIPCHK(hipEventRecord(h->ev_dec[buf], D.hs));
     *out_steps = std::min(done, max_new);
-    if (!cfg->async_out) sync_out(h, stream, h->hs);
+    if (!cfg->async_out) sync_out(h, stream, D.hs);
   });
 }
 
@@ -939,28 +957,29 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
     REQUIRE(T <= h->d.n_text_ctx, "decoder_input_ids longer than max_target_positions");
     ensure_enc_ws(h, B);
     ensure_dec_ws(h, B, T, 1);
-    if ((size_t)B * (T + 1) * 4 > h->forced.bytes) { quiesce(h); h->forced.ensure((size_t)B * (T + 1) * 4); }
-    const int buf = h->gen_count++ & 1;
+    const int buf = h->gen_count++ % h->nctx;
+    DecCtx& D = h->dc[buf];
+    if ((size_t)B * (T + 1) * 4 > D.forced.bytes) { quiesce(h); D.forced.ensure((size_t)B * (T + 1) * 4); }
     sync_in(h, stream, h->he);
     HIPCHK(hipStreamWaitEvent(h->he, h->ev_dec[buf], 0));
     encode_impl(h, mel, B, enc_out);
     cross_kv(h, B, buf);
     HIPCHK(hipEventRecord(h->ev_xkv[buf], h->he));
-    HIPCHK(hipStreamWaitEvent(h->hs, h->ev_xkv[buf], 0));
-    int* ints = h->ints.as<int>();
-    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 3 * B) * 4, h->hs));
-    gather_col(ints + I_NEXT, dec_ids, B, T, 0, h->hs);
+    HIPCHK(hipStreamWaitEvent(D.hs, h->ev_xkv[buf], 0));
+    int* ints = D.ints.as<int>();
+    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 3 * B) * 4, D.hs));
+    gather_col(ints + I_NEXT, dec_ids, B, T, 0, D.hs);
     // forced column T is never read: feed positions 0..T-1 (advance reads column pos+1 < T except last)
-    HIPCHK(hipMemsetAsync(h->forced.p, 0, (size_t)B * (T + 1) * 4, h->hs));
-    HIPCHK(hipMemcpy2DAsync(h->forced.p, (size_t)(T + 1) * 4, dec_ids, (size_t)T * 4, (size_t)T * 4, B,
-                            hipMemcpyDeviceToDevice, h->hs));
+    HIPCHK(hipMemsetAsync(D.forced.p, 0, (size_t)B * (T + 1) * 4, D.hs));
+    HIPCHK(hipMemcpy2DAsync(D.forced.p, (size_t)(T + 1) * 4, dec_ids, (size_t)T * 4, (size_t)T * 4, B,
+                            hipMemcpyDeviceToDevice, D.hs));
     for (int t = 0; t < T; ++t) {
       StepCfg sc{B, T, 1, buf, true, false, logits + (size_t)t * h->d.vocab, (long)T * h->d.vocab, nullptr, 0.f, 0,
-                 h->forced.as<int>(), T + 1};
+                 D.forced.as<int>(), T + 1};
       decode_step(h, sc);
     }
-    HIPCHK(hipEventRecord(h->ev_dec[buf], h->hs));
-    sync_out(h, stream, h->hs);
+    HIPCHK(hipEventRecord(h->ev_dec[buf], D.hs));
+    sync_out(h, stream, D.hs);
   });
 }
 
@@ -1056,13 +1075,14 @@ int wcb_debug_copy(wcb_handle* h, const char* name, void* dst, int64_t bytes, in
     h->dbg_enc_layers = enc_layers;
     const std::map<std::string, DevBuf*> bufs = {{"xt", &h->xt}, {"hbuf", &h->hbuf}, {"x", &h->x}, {"h", &h->h},
                                                  {"qkv", &h->qkv}, {"att", &h->att}, {"ffn", &h->ffn},
-                                                 {"encout", &h->encout}, {"xkv", &h->xkv2[0]}, {"logits", &h->logits}};
+                                                 {"encout", &h->encout}, {"xkv", &h->xkv2[0]},
+                                                 {"logits", &h->dc[0].logits}};
     if (bytes == 0) return;   // only set the layer limit
     REQUIRE(dst, "null dst");
     auto it = bufs.find(name);
     REQUIRE(it != bufs.end(), std::string("unknown buffer ") + name);
     REQUIRE((size_t)bytes <= it->second->bytes, "bytes exceeds buffer size");
-    HIPCHK(hipStreamSynchronize(h->hs));
+    quiesce(h);
     HIPCHK(hipMemcpy(dst, it->second->p, (size_t)bytes, hipMemcpyDeviceToDevice));
   });
 }
@@ -1072,13 +1092,15 @@ int wcb_profile_enable(wcb_handle* h, int enable) {
     REQUIRE(h, "null handle");
     quiesce(h);
     h->prof_collect();
-    h->prof = enable != 0;
+    h->prof = (enable & 1) != 0;          // HIP events around front-end / encoder launches
+    h->prof_stamps = (enable & 2) != 0;   // device stamps in the decode cross-attention (graph nodes)
     h->prof_e.clear();
     h->xattn_bytes = h->xattn_flops = 0;
-    if (h->prof) {
-      h->stamps.ensure((size_t)h->stamp_slots() * 16 * kStampSub);
+    if (h->prof_stamps) {
+      const size_t sb = (size_t)h->nctx * h->stamp_slots() * 16 * kStampSub;   // one region per decode context
+      h->stamps.ensure(sb);
       h->stamp_acc.ensure(16);
-      HIPCHK(hipMemset(h->stamps.p, 0, (size_t)h->stamp_slots() * 16 * kStampSub));
+      HIPCHK(hipMemset(h->stamps.p, 0, sb));
       HIPCHK(hipMemset(h->stamp_acc.p, 0, 16));
     }
   });
@@ -1089,7 +1111,7 @@ int wcb_profile_read(wcb_handle* h, int n, char (*names)[32], int64_t* launches,
   const int rc = guarded(h, [&] {
     REQUIRE(h, "null handle");
     h->prof_collect();
-    if (h->prof && h->stamp_acc.p) {   // decode cross-attention: device-stamped launches
+    if (h->prof_stamps && h->stamp_acc.p) {   // decode cross-attention: device-stamped launches
       quiesce(h);
       unsigned long long acc[2] = {0, 0};
       HIPCHK(hipMemcpy(acc, h->stamp_acc.p, 16, hipMemcpyDeviceToHost));

@@ -298,8 +298,11 @@ class WhisperCB:
     __call__ = forward
 
     # ---------------------------------------------------------------------------- profiling
-    def profile_enable(self, on: bool = True):
-        _lib.check(self._lib.wcb_profile_enable(self._h, int(on)), self._h, "wcb_profile_enable")
+    def profile_enable(self, on: bool = True, events: bool = True, stamps: bool = True):
+        """HIP-event timing of front-end/encoder launches (`events`) and device-stamped timing of the
+        decode cross-attention graph nodes (`stamps`); counters reset."""
+        mode = (int(events) | (int(stamps) << 1)) if on else 0
+        _lib.check(self._lib.wcb_profile_enable(self._h, mode), self._h, "wcb_profile_enable")
 
     def profile_read(self) -> Dict[str, dict]:
         n = 32
