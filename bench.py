@@ -202,7 +202,11 @@ def main():
         avg_ms = p["ms"] / p["launches"]
         bpl = p["bytes"] / p["launches"]
         achieved = bpl / (avg_ms * 1e-3) / 1e9
-        roofs["dec_xattn"] = {"bound": "hbm", "kernel": "attn_decode_kernel (decoder cross-attention, split-KV)",
+        xenc = args.dtype in ("bf16", "f16") and dims.d_model <= 1024 and os.environ.get("WCB_XMODE", "1") != "0"
+        kname = ("attn_xenc_kernel (decoder cross-attention in encoder space: one pass over the encoder "
+                 "output per layer for all heads)") if xenc else \
+            "attn_decode2p_kernel (decoder cross-attention over precomputed per-layer K/V)"
+        roofs["dec_xattn"] = {"bound": "hbm", "kernel": kname,
                               "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                               "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
                               "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": bpl,

@@ -135,6 +135,13 @@ int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, voi
 int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H,
                             int Sk, int nsplit, int variant, void* stream);
 
+/* decoder cross-attention in encoder space (k_xenc.hip), the xmode-1 decode path:
+ * o[B][d] = Σ_h-blocks W_v,h softmax_j(q'_h · enc_j) enc_j + b_v with q'_h = W_k,hᵀ q_h;
+ * q [B][H*64] (pre-scaled by 1/8), enc [B][S][d], wkt = W_k repacked [H][d][64] (element (h,c,i) =
+ * W_k[h*64+i][c]), wv [d][d] (HF layout), bv f32 [d]; nsplit key ranges per row (1..16). 16-bit dtypes. */
+int wcb_op_cross_attention_enc(int dtype, const void* q, const void* enc, const void* wkt, const void* wv,
+                               const float* bv, void* o, int B, int H, int S, int nsplit, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

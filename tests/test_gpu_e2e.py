@@ -137,3 +137,22 @@ def test_prompt_prefix_matches_oracle():
     ids = m.generate(torch.from_numpy(mel), max_length=10, prompt_ids=prompt, min_new_tokens=10).cpu().numpy()
     ref = om.generate(mel, enc=enc, max_length=10, prefix=prompt + [dims.decoder_start_token_id], min_new_tokens=10)
     assert np.array_equal(ids, ref)
+
+
+def test_greedy_bf16_kv_formulation_high_margin_exact():
+    """The precomputed cross-K/V formulation (xmode 0: f32 mode and large-v3 use it) in bf16 gives the
+    same greedy ids as the reference on the high-margin recipe; the default bf16 path is encoder space."""
+    g = np.load(os.path.join(GOLD, "model_tiny.en_margin_s1.npz"))
+    ref = g["greedy_ids"]
+    dims, sd, om, mel, enc = case("tiny.en", 1, "margin", ref.shape[0])
+    old = os.environ.get("WCB_XMODE")
+    os.environ["WCB_XMODE"] = "0"
+    try:
+        m = WhisperCB.from_state_dict(dims, sd, dtype="bf16")
+    finally:
+        if old is None:
+            os.environ.pop("WCB_XMODE")
+        else:
+            os.environ["WCB_XMODE"] = old
+    ids = m.generate(torch.from_numpy(mel), max_length=ref.shape[1]).cpu().numpy()
+    assert np.array_equal(ids, ref)

@@ -57,6 +57,8 @@ SIGNATURES = {
                                           _P]),
     "wcb_op_attention": (C.c_int, [C.c_int, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.c_int, _P]),
+    "wcb_op_cross_attention_enc": (C.c_int, [C.c_int, _P, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int,
+                                             C.c_int, _P]),
 }
 
 

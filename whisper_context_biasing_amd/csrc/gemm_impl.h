@@ -370,7 +370,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
       }
     }
   } else {
-    const T* A = reinterpret_cast<const T*>(g.A);
+    const T* A = reinterpret_cast<const T*>(g.A) + (g.a_grp_n ? (long)(n0 / g.a_grp_n) * g.a_grp_off : 0L);
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
       const int m = min(i * 16 + (lane & 15), g.M - 1);

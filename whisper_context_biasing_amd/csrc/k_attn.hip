@@ -330,42 +330,6 @@ void attention_decode(DType t, const AttnArgs& a, hipStream_t s) {
 }
 
 // --------------------------------------------------------------------------------- flash (MFMA)
-WCB_DEV void glds16a(const void* gptr, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(gptr, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
-}
-WCB_DEV int swz(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
-
-template <typename T>
-WCB_DEV typename DT<T>::frag tr_frag(const char* vt, int r0, int col_chunk2, int lane) {
-  // 16-bit transposed read: group h = lane>>4, lane 4q+p of the group supplies row r0+4h+q,
-  // columns 4p..4p+3 of the 16-column block (chunk pair col_chunk2, col_chunk2+1).
-  const int h = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int r1 = r0 + 4 * h + q, r2 = r1 + 16;
-  const int c = col_chunk2 + (p >> 1), byte = (p & 1) * 8;
-  typedef short s4 __attribute__((ext_vector_type(4)));
-  const s4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(vt + swz(r1, c) + byte));
-  const s4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(vt + swz(r2, c) + byte));
-  typename DT<T>::frag f;
-  if constexpr (__is_same(T, bf16_t)) {
-    f = s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-  } else {
-    const s16x8 t8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-    f = __builtin_bit_cast(h16x8, t8);
-  }
-  return f;
-}
-
-template <typename T>
-WCB_DEV typename DT<T>::frag pack_p(const f32x4& lo, const f32x4& hi) {
-  typename DT<T>::frag f;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if constexpr (__is_same(T, bf16_t)) { f[e] = (short)f_to_bf16(lo[e]); f[e + 4] = (short)f_to_bf16(hi[e]); }
-    else { f[e] = f16_t(lo[e]); f[e + 4] = f16_t(hi[e]); }
-  }
-  return f;
-}
-
 template <typename T, int QW>
 __global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
   using Frag = typename DT<T>::frag;

@@ -1,0 +1,470 @@
+// Decoder cross-attention in encoder space (16-bit model dtypes).
+//
+// Replaces the cross-attention branch of WhisperAttention.forward
+// ([tf] modeling_whisper.py:284-356, is_cross_attention: keys/values from the encoder output, k_proj
+// without bias :279) as the decoder calls it once per layer and generated token
+// (WhisperDecoderLayer.forward :448-505).
+//
+// Algebra (exact in real arithmetic; every Whisper size has k_proj bias = None):
+//   score_j,h = q_h · (W_k,h e_j)        = (W_k,hᵀ q_h) · e_j  =: q'_h · e_j
+//   out_h     = Σ_j p_j,h (W_v,h e_j + b_v,h) = W_v,h (Σ_j p_j,h e_j) + b_v,h      (Σ_j p_j,h = 1)
+// so a decode step streams the encoder output e [1500][d] once per layer for ALL heads, instead of
+// that layer's K and V (2·1500·d per clip): half the bytes of the K/V formulation, and no per-clip
+// cross-K/V precompute (1.36 TFLOP and 1.77 GB of writes per 32-clip whisper-small batch).
+// q'_h = W_k,hᵀ q_h and W_v,h u_h are block-diagonal skinny GEMMs (gemm_impl.h, grouped A).
+//
+// attn_xenc_kernel: workgroup = (key range s, row b), 8 waves. The row's key range streams through a
+//   ring of NS LDS stages, 32 keys × D columns each (global_load_lds, 16 B per lane, source-address
+//   swizzle of common.h), NS-1 chunks in flight. Per chunk each wave computes the 32 × 16 score tile
+//   S = E·q'ᵀ over its share of the D contraction (A = E rows by ds_read_b128, B = q' fragments held
+//   in registers; heads ≥ H are zero); the partials are summed through LDS in a fixed order, so every
+//   wave holds the same S, runs the online softmax per head lane-locally (max over its 4 lane groups
+//   by two shuffles) and accumulates its eighth of Uᵀ = Eᵀ·P (A = Eᵀ by ds_read_b64_tr_b16, B = P
+//   straight from the score accumulators: the k order {4g..4g+3, 16+4g..16+4g+3} of lane group g
+//   matches both).
+//   Output: per (row, range) the range-local (max, Σp) per head and Σ p·e [H][D] in f32.
+// xenc_merge_kernel: workgroup = (head, row): merges the ranges (fixed order: deterministic) and
+//   normalises: u[row][h] = Σ_j p_j,h e_j in the model dtype. W_v,h and b_v are then one block-diagonal
+//   skinny GEMM (gemm_impl.h, grouped A), whose output feeds the out-projection GEMM.
+#include "common.h"
+#include "kernels.h"
+
+namespace wcb {
+
+constexpr int kXencCK = 32;   // keys per chunk
+constexpr int kXencNW = 8;    // waves per workgroup
+
+template <int D> struct XencCfg {
+  static constexpr int NP = D / 64;                       // 64-column panels of a chunk
+  static constexpr int STAGE = kXencCK * D * 2;           // bytes per LDS stage
+  static constexpr int RED = kXencNW * 2 * 64 * 16;       // score partials [wave][tile][lane] f32x4
+  static constexpr int NS = (3 * STAGE + RED <= 160 * 1024) ? 3 : 2;
+  static constexpr int LDS = NS * STAGE + RED;
+  static constexpr int KST = D / 32;                      // k-steps of the score contraction
+  static constexpr int KSW = (KST + kXencNW - 1) / kXencNW;   // k-steps per wave
+  static constexpr int CTW = (D / 16 + kXencNW - 1) / kXencNW;  // 16-column Uᵀ tiles per wave
+  static constexpr int GLW = (4 * NP + kXencNW - 1) / kXencNW;  // glds instructions per wave per chunk
+};
+
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+// ds_read_b64_tr_b16 as inline asm: the builtin form makes hipcc drain every in-flight LDS-DMA
+// (s_waitcnt vmcnt(0)) before it, which serialises the chunk ring. The caller waits lgkmcnt itself.
+WCB_DEV s16x4_t tr_read_asm(const char* p) {
+  s16x4_t r;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+template <typename T>
+WCB_DEV typename DT<T>::frag tr_pair(const s16x4_t& x, const s16x4_t& y) {
+  const s16x8 t8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+  if constexpr (__is_same(T, bf16_t)) return t8;
+  else return __builtin_bit_cast(h16x8, t8);
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(512) void attn_xenc_kernel(XencArgs a) {
+  using Frag = typename DT<T>::frag;
+  using C = XencCfg<D>;
+  constexpr int CK = kXencCK, NW = kXencNW, NP = C::NP, NS = C::NS, KST = C::KST, KSW = C::KSW, CTW = C::CTW;
+  constexpr int GLW = C::GLW;
+  constexpr int PANEL = CK * 128;                         // bytes of one panel in a stage
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  f32x4* red = reinterpret_cast<f32x4*>(lds + NS * C::STAGE);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int split = blockIdx.x, b = blockIdx.y;
+  const unsigned long long t_start = a.stamp.base ? stamp_now() : 0;
+  const int per = ((a.S + a.nsplit - 1) / a.nsplit + CK - 1) / CK * CK;
+  const int k_lo = split * per, k_hi = min(a.S, k_lo + per);
+  const int nch = k_hi > k_lo ? (k_hi - k_lo + CK - 1) / CK : 0;
+  const T* E = reinterpret_cast<const T*>(a.enc) + (long)b * a.enc_sb;
+
+  // q' fragments of this wave's k-steps: lane → head lane&15 (zero for heads >= H)
+  const int hq = lane & 15;
+  Frag qf[KSW];
+  {
+    const T* qrow = reinterpret_cast<const T*>(a.qp) + ((long)b * a.H + min(hq, a.H - 1)) * D + 8 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < KSW; ++i) {
+      const int ks = wave * KSW + i;
+      qf[i] = Frag{};
+      if (ks < KST && hq < a.H) qf[i] = load_frag<T>(qrow + ks * 32);
+    }
+    // retire these plain loads before the LDS-DMA ring starts: a plain load still pending inside the
+    // loop makes hipcc wait vmcnt(0) at its use, i.e. drain the whole ring every chunk
+    __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
+  }
+  // staging: 4·NP wave-instructions of 1 KiB (8 rows × 128 B of one panel) per chunk; wave w issues
+  // instructions w, w+NW, ...: panel q >> 2, row group q & 3
+  int src_off[GLW], src_row[GLW];
+#pragma unroll
+  for (int i = 0; i < GLW; ++i) {
+    const int q = wave + NW * i, p = q >> 2, r = (q & 3) * 8 + (lane >> 3);
+    src_row[i] = r;
+    src_off[i] = p * 64 + ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+  }
+  auto stage = [&](int st, int c) {
+    char* base = lds + st * C::STAGE;
+    const int key0 = k_lo + c * CK;
+#pragma unroll
+    for (int i = 0; i < GLW; ++i) {
+      const int q = wave + NW * i;
+      if (GLW * NW == 4 * NP || q < 4 * NP) {
+        const int key = min(key0 + src_row[i], a.S - 1);
+        glds16a(E + (long)key * D + src_off[i], base + (q >> 2) * PANEL + (q & 3) * 1024);
+      }
+    }
+  };
+
+  f32x4 acc[CTW];
+#pragma unroll
+  for (int t = 0; t < CTW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  const float L2E = 1.4426950408889634f;
+
+  if (nch > 0) stage(0, 0);
+  if (NS > 2 && nch > 1) stage(1, 1);
+  for (int c = 0; c < nch; ++c) {
+    // retire chunk c (this wave's loads; the barrier covers the other waves'), keep c+1 in flight
+    if (NS > 2 && c + 1 < nch) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(GLW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // the stage read in iteration c-1 is free once every wave has passed the barrier above
+    if (c + NS - 1 < nch) stage((c + NS - 1) % NS, c + NS - 1);
+    const char* st = lds + (c % NS) * C::STAGE;
+
+    // partial S = E·q'ᵀ over this wave's k-steps, keys [0,16) and [16,32) of the chunk
+    f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0;
+#pragma unroll
+    for (int i = 0; i < KSW; ++i) {
+      const int ks = wave * KSW + i;
+      if (KSW * NW == KST || ks < KST) {
+        const char* pb = st + (ks >> 1) * PANEL;
+        const int cc = (ks & 1) * 4 + (lane >> 4);
+        const Frag a0 = *reinterpret_cast<const Frag*>(pb + swz(lane & 15, cc));
+        const Frag a1 = *reinterpret_cast<const Frag*>(pb + swz(16 + (lane & 15), cc));
+        s0 = mma16(a0, qf[i], s0);
+        s1 = mma16(a1, qf[i], s1);
+      }
+    }
+    red[(wave * 2 + 0) * 64 + lane] = s0;
+    red[(wave * 2 + 1) * 64 + lane] = s1;
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's partials written
+    __builtin_amdgcn_s_barrier();
+    // every wave sums the partials in the same order: identical S (and P) in all waves
+    s0 = red[lane];
+    s1 = red[64 + lane];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      s0 += red[(w * 2 + 0) * 64 + lane];
+      s1 += red[(w * 2 + 1) * 64 + lane];
+    }
+    // issue this wave's Eᵀ fragment reads (transposed) now; they overlap the softmax
+    s16x4_t tx[CTW], ty[CTW];
+#pragma unroll
+    for (int t = 0; t < CTW; ++t) {
+      const int c0 = (wave * CTW + t) * 16;
+      if (CTW * NW * 16 == D || c0 < D) {
+        const char* vt = st + (c0 >> 6) * PANEL;
+        const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+        const int r1 = 4 * g + q, cch = ((c0 & 63) >> 4) * 2 + (p >> 1), byte = (p & 1) * 8;
+        tx[t] = tr_read_asm(vt + swz(r1, cch) + byte);
+        ty[t] = tr_read_asm(vt + swz(r1 + 16, cch) + byte);
+      }
+    }
+    const int kb = k_lo + c * CK + 4 * (lane >> 4);
+    if (k_lo + (c + 1) * CK > k_hi) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (kb + e >= k_hi) s0[e] = -INFINITY;
+        if (kb + 16 + e >= k_hi) s1[e] = -INFINITY;
+      }
+    }
+    float cm = fmaxf(fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s0[2], s0[3])), fmaxf(fmaxf(s1[0], s1[1]), fmaxf(s1[2], s1[3])));
+    cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+    cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+    const float mnew = fmaxf(m_run, cm);            // finite: every chunk holds >= 1 key of the range
+    const float alpha = exp2f((m_run - mnew) * L2E);
+    m_run = mnew;
+    const float mb = mnew * L2E;
+    float ls = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s0[e] = exp2f(fmaf(s0[e], L2E, -mb));
+      s1[e] = exp2f(fmaf(s1[e], L2E, -mb));
+      ls += s0[e] + s1[e];
+    }
+    l_run = l_run * alpha + ls;
+    const Frag pf = pack_p<T>(s0, s1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // Uᵀ[c][h] += Σ_k E[k][c] P[k][h] over this wave's column tiles
+#pragma unroll
+    for (int t = 0; t < CTW; ++t) {
+      const int c0 = (wave * CTW + t) * 16;
+      if (CTW * NW * 16 == D || c0 < D) acc[t] = mma16(tr_pair<T>(tx[t], ty[t]), pf, acc[t] * alpha);
+    }
+  }
+  // ---- range partials: lane holds Uᵀ[c0 + 4(lane>>4) + e][head lane&15]
+  l_run += __shfl_xor(l_run, 16, 64);
+  l_run += __shfl_xor(l_run, 32, 64);
+  if (hq < a.H) {
+    const long slot = ((long)b * a.nsplit + split) * a.H + hq;
+    float* pp = a.part + slot * D + 4 * (lane >> 4);
+#pragma unroll
+    for (int t = 0; t < CTW; ++t) {
+      const int c0 = (wave * CTW + t) * 16;
+      if (CTW * NW * 16 == D || c0 < D) *reinterpret_cast<f32x4*>(pp + c0) = acc[t];
+    }
+    if (wave == 0 && lane < 16) *reinterpret_cast<float2*>(a.ml + slot * 2) = float2{m_run, l_run};
+  }
+  if (a.stamp.base) {
+    __syncthreads();
+    if (tid == 0) stamp_commit(a.stamp, t_start);
+  }
+}
+
+// ---- register-ring variant (default): the chunk ring lives in VGPRs (512 KiB per CU, against 160 KiB
+// of LDS), so a workgroup needs only its per-wave transpose tiles and the score exchange in LDS
+// (64 KiB at D = 768): two of its workgroups, or one beside a GEMM tile, fit on a CU.
+// Wave w owns columns [w·CW, (w+1)·CW): it loads its 32 × CW slice of each chunk straight into the
+// MFMA A-operand registers (lane → key lane&15 (+16), 8 columns), two chunks ahead; computes its partial
+// scores; writes the slice into its private LDS tile (128-byte-row panels, common.h swizzle) for the
+// transposed Eᵀ reads; the 4 partial score tiles are summed through LDS (double-buffered, one barrier
+// per chunk) in a fixed order.
+template <int D> struct XregCfg {
+  static constexpr int NW = D >= 128 ? 4 : D / 32;        // waves = column slices
+  static constexpr int CW = D / NW;                       // columns per wave
+  static constexpr int KSW = CW / 32;                     // k-steps per wave
+  static constexpr int CTW = CW / 16;                     // 16-column Uᵀ tiles per wave
+  static constexpr int NPW = (CW + 63) / 64;              // 128-byte-row panels per wave tile
+  static constexpr int PANEL = kXencCK * 128;
+  static constexpr int TILE = NPW * PANEL;
+  static constexpr int RED = 2 * NW * 2 * 64 * 16;
+  static constexpr int LDS = NW * TILE + RED;
+};
+
+template <typename T, int D>
+__global__ __launch_bounds__(XregCfg<D>::NW * 64, 2) void attn_xenc_reg_kernel(XencArgs a) {
+  using Frag = typename DT<T>::frag;
+  using C = XregCfg<D>;
+  constexpr int CK = kXencCK, NW = C::NW, CW = C::CW, KSW = C::KSW, CTW = C::CTW, PANEL = C::PANEL;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  char* tile = lds + wave * C::TILE;
+  f32x4* red = reinterpret_cast<f32x4*>(lds + NW * C::TILE);
+  const int split = blockIdx.x, b = blockIdx.y;
+  const unsigned long long t_start = a.stamp.base ? stamp_now() : 0;
+  const int per = ((a.S + a.nsplit - 1) / a.nsplit + CK - 1) / CK * CK;
+  const int k_lo = split * per, k_hi = min(a.S, k_lo + per);
+  const int nch = k_hi > k_lo ? (k_hi - k_lo + CK - 1) / CK : 0;
+  const int cw0 = wave * CW;
+  const T* E = reinterpret_cast<const T*>(a.enc) + (long)b * a.enc_sb + cw0 + 8 * (lane >> 4);
+
+  const int hq = lane & 15;
+  Frag qf[KSW];
+  {
+    const T* qrow = reinterpret_cast<const T*>(a.qp) + ((long)b * a.H + min(hq, a.H - 1)) * D + cw0 + 8 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < KSW; ++i) qf[i] = hq < a.H ? load_frag<T>(qrow + i * 32) : Frag{};
+  }
+  auto load_chunk = [&](Frag (&f)[2][KSW], int c) {
+    const int key0 = k_lo + c * CK + (lane & 15);   // past the range: re-read its last key (L2)
+    const T* r0 = E + (long)min(key0, k_hi - 1) * D;
+    const T* r1 = E + (long)min(key0 + 16, k_hi - 1) * D;
+#pragma unroll
+    for (int ks = 0; ks < KSW; ++ks) {
+      f[0][ks] = load_frag<T>(r0 + ks * 32);
+      f[1][ks] = load_frag<T>(r1 + ks * 32);
+    }
+  };
+
+  f32x4 acc[CTW];
+#pragma unroll
+  for (int t = 0; t < CTW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  const float L2E = 1.4426950408889634f;
+
+  auto body = [&](Frag (&f)[2][KSW], int c) {
+    // partial scores over this wave's columns
+    f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0;
+#pragma unroll
+    for (int ks = 0; ks < KSW; ++ks) {
+      s0 = mma16(f[0][ks], qf[ks], s0);
+      s1 = mma16(f[1][ks], qf[ks], s1);
+    }
+    // the slice into the wave's transpose tile (its reads of the previous chunk precede in order)
+#pragma unroll
+    for (int ks = 0; ks < KSW; ++ks) {
+      char* pb = tile + (ks >> 1) * PANEL;
+      const int cc = (ks & 1) * 4 + (lane >> 4);
+      *reinterpret_cast<Frag*>(pb + swz(lane & 15, cc)) = f[0][ks];
+      *reinterpret_cast<Frag*>(pb + swz(16 + (lane & 15), cc)) = f[1][ks];
+    }
+    load_chunk(f, c + 2);   // the registers are free: refill two chunks ahead (unconditionally: a
+                            // load under a branch makes hipcc drain every load at the loop head)
+    f32x4* rb = red + (c & 1) * NW * 2 * 64;
+    rb[(wave * 2 + 0) * 64 + lane] = s0;
+    rb[(wave * 2 + 1) * 64 + lane] = s1;
+    __syncthreads();
+    s0 = rb[lane];
+    s1 = rb[64 + lane];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      s0 += rb[(w * 2 + 0) * 64 + lane];
+      s1 += rb[(w * 2 + 1) * 64 + lane];
+    }
+    const int kb = k_lo + c * CK + 4 * (lane >> 4);
+    if (k_lo + (c + 1) * CK > k_hi) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (kb + e >= k_hi) s0[e] = -INFINITY;
+        if (kb + 16 + e >= k_hi) s1[e] = -INFINITY;
+      }
+    }
+    float cm = fmaxf(fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s0[2], s0[3])), fmaxf(fmaxf(s1[0], s1[1]), fmaxf(s1[2], s1[3])));
+    cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+    cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+    const float mnew = fmaxf(m_run, cm);
+    const float alpha = exp2f((m_run - mnew) * L2E);
+    m_run = mnew;
+    const float mb = mnew * L2E;
+    float ls = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s0[e] = exp2f(fmaf(s0[e], L2E, -mb));
+      s1[e] = exp2f(fmaf(s1[e], L2E, -mb));
+      ls += s0[e] + s1[e];
+    }
+    l_run = l_run * alpha + ls;
+    const Frag pf = pack_p<T>(s0, s1);
+#pragma unroll
+    for (int t = 0; t < CTW; ++t) {
+      const int c0 = t * 16;
+      const Frag ef = tr_frag<T>(tile + (c0 >> 6) * PANEL, 0, ((c0 & 63) >> 4) * 2, lane);
+      acc[t] = mma16(ef, pf, acc[t] * alpha);
+    }
+  };
+
+  if (nch > 0) {
+    // chunks in pairs; an odd count gets one fully masked chunk (p = 0, running max unchanged)
+    Frag fa[2][KSW], fb[2][KSW];
+    load_chunk(fa, 0);
+    load_chunk(fb, 1);
+    for (int c = 0; c < nch; c += 2) {
+      body(fa, c);
+      body(fb, c + 1);
+    }
+  }
+  // ---- range partials: lane holds Uᵀ[cw0 + 16t + 4(lane>>4) + e][head lane&15]
+  l_run += __shfl_xor(l_run, 16, 64);
+  l_run += __shfl_xor(l_run, 32, 64);
+  if (hq < a.H) {
+    const long slot = ((long)b * a.nsplit + split) * a.H + hq;
+    float* pp = a.part + slot * D + cw0 + 4 * (lane >> 4);
+#pragma unroll
+    for (int t = 0; t < CTW; ++t) *reinterpret_cast<f32x4*>(pp + t * 16) = acc[t];
+    if (wave == 0 && lane < 16) *reinterpret_cast<float2*>(a.ml + slot * 2) = float2{m_run, l_run};
+  }
+  if (a.stamp.base) {
+    __syncthreads();
+    if (tid == 0) stamp_commit(a.stamp, t_start);
+  }
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(256) void xenc_merge_kernel(XencArgs a, T* u, long ldu) {
+  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int ns = a.nsplit;
+  // every load is issued unconditionally (index clamped, weight 0 beyond nsplit): a load under a
+  // run-time condition makes hipcc wait for each one in turn
+  __shared__ float2 sv[kXencMaxSplit];
+  if (tid < kXencMaxSplit)
+    sv[tid] = tid < ns ? *reinterpret_cast<const float2*>(a.ml + (((long)b * ns + tid) * a.H + h) * 2) : float2{0.f, 0.f};
+  __syncthreads();
+  float2 v[kXencMaxSplit];
+#pragma unroll
+  for (int s = 0; s < kXencMaxSplit; ++s) v[s] = sv[s];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < kXencMaxSplit; ++s)
+    if (s < ns && v[s].y > 0.f) mx = fmaxf(mx, v[s].x);
+  float w[kXencMaxSplit];
+  float L = 0.f;
+#pragma unroll
+  for (int s = 0; s < kXencMaxSplit; ++s) {
+    w[s] = (s < ns && v[s].y > 0.f) ? __expf(v[s].x - mx) : 0.f;   // empty ranges publish Σp = 0
+    L += w[s] * v[s].y;
+  }
+  const float inv = 1.f / L;
+  const float* pp = a.part + ((long)b * ns * a.H + h) * D;
+  for (int c = tid * 4; c < D; c += 1024) {
+    f32x4 pv[kXencMaxSplit];
+#pragma unroll
+    for (int s = 0; s < kXencMaxSplit; ++s) pv[s] = *reinterpret_cast<const f32x4*>(pp + (long)min(s, ns - 1) * a.H * D + c);
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < kXencMaxSplit; ++s) acc += w[s] * pv[s];
+    acc *= inv;
+    typedef short s4 __attribute__((ext_vector_type(4)));
+    s4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = __builtin_bit_cast(short, DT<T>::fromf(acc[e]));
+    *reinterpret_cast<s4*>(u + (long)b * ldu + (long)h * D + c) = o;
+  }
+}
+
+bool xenc_supported(DType t, int D) {
+  return (t == kBF16 || t == kF16) && (D == 384 || D == 768 || D == 1024 || D == 64 || D == 128 || D == 256 || D == 512);
+}
+
+template <typename T, int D>
+static void launch_xenc(const XencArgs& a, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)attn_xenc_kernel<T, D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              XencCfg<D>::LDS);
+    (void)hipFuncSetAttribute((const void*)attn_xenc_reg_kernel<T, D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              XregCfg<D>::LDS);
+    attr_set = true;
+  }
+  if (a.variant == 0)
+    hipLaunchKernelGGL((attn_xenc_kernel<T, D>), dim3(a.nsplit, a.rows), dim3(kXencNW * 64), XencCfg<D>::LDS, s, a);
+  else
+    hipLaunchKernelGGL((attn_xenc_reg_kernel<T, D>), dim3(a.nsplit, a.rows), dim3(XregCfg<D>::NW * 64),
+                       XregCfg<D>::LDS, s, a);
+}
+
+template <typename T>
+static void launch_xenc_t(const XencArgs& a, hipStream_t s) {
+  switch (a.D) {
+    case 64: launch_xenc<T, 64>(a, s); break;
+    case 128: launch_xenc<T, 128>(a, s); break;
+    case 256: launch_xenc<T, 256>(a, s); break;
+    case 384: launch_xenc<T, 384>(a, s); break;
+    case 512: launch_xenc<T, 512>(a, s); break;
+    case 768: launch_xenc<T, 768>(a, s); break;
+    case 1024: launch_xenc<T, 1024>(a, s); break;
+    default: break;
+  }
+}
+
+void xenc_attention(DType t, const XencArgs& a, hipStream_t s) {
+  if (t == kBF16) launch_xenc_t<bf16_t>(a, s);
+  else if (t == kF16) launch_xenc_t<f16_t>(a, s);
+}
+
+template <typename T>
+static void launch_merge_t(const XencArgs& a, void* u, long ldu, hipStream_t s) {
+  const dim3 grid(a.H, a.rows);
+#define WCB_XC(DD) case DD: hipLaunchKernelGGL((xenc_merge_kernel<T, DD>), grid, dim3(256), 0, s, a, (T*)u, ldu); break;
+  switch (a.D) { WCB_XC(64) WCB_XC(128) WCB_XC(256) WCB_XC(384) WCB_XC(512) WCB_XC(768) WCB_XC(1024) default: break; }
+#undef WCB_XC
+}
+
+void xenc_merge(DType t, const XencArgs& a, void* u, long ldu, hipStream_t s) {
+  if (t == kBF16) launch_merge_t<bf16_t>(a, u, ldu, s);
+  else if (t == kF16) launch_merge_t<f16_t>(a, u, ldu, s);
+}
+
+}  // namespace wcb

@@ -34,6 +34,9 @@ struct GemmArgs {
   float* sel_val = nullptr; int* sel_idx = nullptr;   // LM head: per-(row, workgroup) argmax partial
   const uint32_t* sel_root_bits = nullptr; float sel_lam = 0.f;
   int sel_eos = -1; const int* sel_step = nullptr; int sel_min_new = 0;
+  // grouped A (skinny path, block-diagonal weights): the A row of output column block n0 starts
+  // (n0 / a_grp_n) · a_grp_off elements further (q'_h = W_k,hᵀ q_h: K = 64 columns of head h)
+  int a_grp_n = 0; long a_grp_off = 0;
 };
 
 void gemm(DType t, const GemmArgs& g, hipStream_t s);
@@ -69,6 +72,25 @@ struct AttnArgs {
 };
 void attention_decode(DType t, const AttnArgs& a, hipStream_t s);   // VALU, any T, any Sq
 bool attention_flash(DType t, const AttnArgs& a, hipStream_t s);    // MFMA encoder (16-bit T)
+
+// Decoder cross-attention in encoder space (k_xenc.hip). Whisper's cross-attention key projection
+// has no bias, so q_h·(enc W_kᵀ)_hᵀ = (W_k,hᵀ q_h)·encᵀ and Σ p·(enc W_vᵀ + b_v) = (Σ p·enc) W_vᵀ + b_v:
+// the step streams the encoder output once per layer instead of the per-layer K and V.
+constexpr int kXencMaxSplit = 16;
+struct XencArgs {
+  const void* enc = nullptr; long enc_sb = 0;   // [rows][S][D] model dtype, enc_sb elements per row
+  const void* qp = nullptr;                     // [rows][H][D] q'_h = W_k,hᵀ q_h (q pre-scaled)
+  int rows = 0, H = 0, D = 0, S = 0;
+  int nsplit = 1;                               // key ranges per row (<= kXencMaxSplit)
+  float* part = nullptr;                        // [rows][nsplit][H][D] Σ_j p_j enc_j (range-local max)
+  float* ml = nullptr;                          // [rows][nsplit][H][2] (max, Σ p)
+  Stamp stamp;
+  int variant = 1;                              // 1 register chunk ring, 0 LDS-DMA chunk ring
+};
+bool xenc_supported(DType t, int D);
+void xenc_attention(DType t, const XencArgs& a, hipStream_t s);
+// u[r][h·D + c] = (Σ_s w_s part[r][s][h][c]) / L  (model dtype; ldu elements per row)
+void xenc_merge(DType t, const XencArgs& a, void* u, long ldu, hipStream_t s);
 
 // log-mel front end
 void logmel_power_mel(const float* pcm, long pcm_stride, int n_samples, int B, const float* dft,

@@ -100,6 +100,8 @@ struct LayerW {
   void* fc1_w = nullptr; float* fc1_b = nullptr;
   void* fc2_w = nullptr; float* fc2_b = nullptr;
   float *ln2_w = nullptr, *ln2_b = nullptr;
+  // encoder-space cross-attention (k_xenc.hip): W_k,hᵀ repacked [H][d][64], W_v [d][d], b_v
+  void* xkt_w = nullptr; void* xv_w = nullptr; float* xv_b = nullptr;
 };
 
 struct ProfEntry {
@@ -125,7 +127,8 @@ struct DecCtx {
   hipStream_t sub[kMaxSub] = {};                // row-group chains (fork/join inside the step graph)
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSub] = {};
   int dec_B = 0, dec_T = 0;
-  DevBuf kvself, dx, dh, dq, datt, dffn, dstats, xpart, xticket, logits, part_val, part_idx, ints, outbuf, forced;
+  DevBuf kvself, dx, dh, dq, dqp, du, datt, dffn, dstats, xpart, xml, xticket, logits, part_val, part_idx, ints, outbuf,
+      forced;
   int nchunk = 64;
   hipGraphExec_t gexec = nullptr;               // captured decode step
   std::string gkey;
@@ -152,6 +155,12 @@ struct wcb_handle {
   // head-major K/V cycling 12 layers): split-KV hand-offs cost more than they hide at 16-32 rows.
   int xsplit = 1;
   int xvariant = 0;  // cross-attention kernel variant (k_attn.hip launch_decode)
+  // Cross-attention formulation: 1 = encoder space (k_xenc.hip: the step streams the encoder output,
+  // no cross-K/V precompute; 16-bit dtypes, d <= 1024), 0 = precomputed per-layer K/V (f32 "exact"
+  // mode, large-v3). Fixed at create (WCB_XMODE overrides where supported).
+  int xmode = 1;
+  int xenc_split = 8;   // key ranges per row of the encoder-space kernel (rows x ranges workgroups)
+  int xenc_variant = 1; // attn_xenc kernel variant (k_xenc.hip)
   std::map<std::string, std::vector<float>> host_w;
   std::vector<DevBuf> owned;
   bool ready = false;
@@ -169,7 +178,8 @@ struct wcb_handle {
   // encoder workspace
   int enc_B = 0;
   DevBuf xt, hbuf, x, h, qkv, att, ffn, encout;
-  // cross-K/V, double-buffered (buffer k is read by decode context k)
+  // per decode context: cross-K/V (xmode 0) or the encoder output (xmode 1); buffer k is read by
+  // decode context k while the encoder stream fills the next one
   DevBuf xkv2[kMaxCtx];
   // default (empty) bias automaton
   std::unique_ptr<wcb_bias> empty_bias;
@@ -342,6 +352,10 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     HIPCHK(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
     if (const char* xs = getenv("WCB_XSPLIT")) h->xsplit = std::max(1, std::min(atoi(xs), kXSplit));
     if (const char* xv = getenv("WCB_XVARIANT")) h->xvariant = atoi(xv);
+    h->xmode = xenc_supported(h->dt, desc->d_model) ? 1 : 0;
+    if (const char* xm = getenv("WCB_XMODE")) h->xmode = (atoi(xm) != 0 && h->xmode) ? 1 : 0;
+    if (const char* xs = getenv("WCB_XENC_SPLIT")) h->xenc_split = std::max(1, std::min(atoi(xs), kXencMaxSplit));
+    if (const char* xv = getenv("WCB_XENC_VARIANT")) h->xenc_variant = atoi(xv);
     // DFT table [416 cols][416 k]: col 2b = win·cos(2πbk/400), col 2b+1 = −win·sin(2πbk/400)
     std::vector<float> dft((size_t)kNCol * kNCol, 0.f);
     for (int c = 0; c < 402; ++c) {
@@ -396,8 +410,8 @@ void wcb_destroy(wcb_handle* h) {
   (void)hipDeviceSynchronize();
   for (DecCtx& D : h->dc) {
     if (D.gexec) (void)hipGraphExecDestroy(D.gexec);
-    for (DevBuf* b : {&D.kvself, &D.dx, &D.dh, &D.dq, &D.datt, &D.dffn, &D.dstats, &D.xpart, &D.xticket, &D.logits,
-                      &D.part_val, &D.part_idx, &D.ints, &D.outbuf, &D.forced})
+    for (DevBuf* b : {&D.kvself, &D.dx, &D.dh, &D.dq, &D.dqp, &D.du, &D.datt, &D.dffn, &D.dstats, &D.xpart, &D.xml, &D.xticket,
+                      &D.logits, &D.part_val, &D.part_idx, &D.ints, &D.outbuf, &D.forced})
       b->release();
     if (D.ev_fork) (void)hipEventDestroy(D.ev_fork);
     for (int i = 0; i < DecCtx::kMaxSub; ++i) {
@@ -506,12 +520,30 @@ int wcb_finalize_weights(wcb_handle* h) {
       const auto& wk = h->W(pd + "encoder_attn.k_proj.weight", dd);
       const auto& wv = h->W(pd + "encoder_attn.v_proj.weight", dd);
       const auto& bv = h->W(pd + "encoder_attn.v_proj.bias", d);
-      std::copy(wk.begin(), wk.end(), xkv_w.begin() + (size_t)(2 * i) * dd);
-      std::copy(wv.begin(), wv.end(), xkv_w.begin() + (size_t)(2 * i + 1) * dd);
-      std::copy(bv.begin(), bv.end(), xkv_b.begin() + (size_t)(2 * i + 1) * d);
+      REQUIRE(h->host_w.count(pd + "encoder_attn.k_proj.bias") == 0 ||
+                  std::all_of(h->host_w[pd + "encoder_attn.k_proj.bias"].begin(),
+                              h->host_w[pd + "encoder_attn.k_proj.bias"].end(), [](float v) { return v == 0.f; }),
+              "encoder_attn.k_proj has no bias in Whisper ([tf] modeling_whisper.py:279)");
+      if (h->xmode == 1) {
+        // W_k,hᵀ: [H][d][64], element (h, c, i) = W_k[h·64 + i][c] (K = 64 contiguous for the MFMA)
+        const int H = h->H();
+        std::vector<float> wkt(dd);
+        for (int hh = 0; hh < H; ++hh)
+          for (int c = 0; c < d; ++c)
+            for (int ii = 0; ii < 64; ++ii) wkt[((size_t)hh * d + c) * 64 + ii] = wk[(size_t)(hh * 64 + ii) * d + c];
+        lw.xkt_w = h->upload_t(wkt);
+        lw.xv_w = h->upload_t(wv);
+        lw.xv_b = h->upload_f(bv);
+      } else {
+        std::copy(wk.begin(), wk.end(), xkv_w.begin() + (size_t)(2 * i) * dd);
+        std::copy(wv.begin(), wv.end(), xkv_w.begin() + (size_t)(2 * i + 1) * dd);
+        std::copy(bv.begin(), bv.end(), xkv_b.begin() + (size_t)(2 * i + 1) * d);
+      }
     }
-    h->xkv_w = h->upload_t(xkv_w);
-    h->xkv_b = h->upload_f(xkv_b);
+    if (h->xmode == 0) {
+      h->xkv_w = h->upload_t(xkv_w);
+      h->xkv_b = h->upload_f(xkv_b);
+    }
     h->enc_ln_w = h->upload_f(h->W("model.encoder.layer_norm.weight", d));
     h->enc_ln_b = h->upload_f(h->W("model.encoder.layer_norm.bias", d));
     h->dec_ln_w = h->upload_f(h->W("model.decoder.layer_norm.weight", d));
@@ -578,7 +610,8 @@ void run_gemm(wcb_handle* h, const char* cls, const GemmArgs& g) {
   h->timed(cls, 2.0 * g.M * g.N * g.K, 0.0, h->he, [&] { gemm(h->dt, g, h->he); });
 }
 
-// WhisperEncoder.forward ([tf] modeling_whisper.py:592-646) on mel f32 [B][n_mel][3000]
+// WhisperEncoder.forward ([tf] modeling_whisper.py:592-646) on mel f32 [B][n_mel][3000]; the final
+// LayerNorm writes [B][1500][d] to enc_out (h->encout when null)
 void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
   ensure_enc_ws(h, B);
   const int d = h->d.d_model, S = h->S(), nm = h->d.n_mel, H = h->H();
@@ -628,8 +661,6 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
   }
   void* dst = enc_out ? enc_out : h->encout.p;
   h->timed("layernorm", 0, M * d * (4.0 + e), h->he, [&] { layernorm(h->dt, h->x.as<float>(), h->enc_ln_w, h->enc_ln_b, dst, (int)M, d, h->he); });
-  if (enc_out && enc_out != h->encout.p)
-    HIPCHK(hipMemcpyAsync(h->encout.p, enc_out, M * d * e, hipMemcpyDeviceToDevice, h->he));
 }
 
 enum { I_STEP = 0, I_POS = 1, I_DONE = 2, I_TICKET = 3, I_UNFIN = 4, I_NEXT = 16 };
@@ -645,7 +676,8 @@ void drop_graphs(wcb_handle* h) {
 void ensure_dec_ws(wcb_handle* h, int B, int T, int out_ld) {
   const size_t e = esize(h->d.dtype), d = h->d.d_model, L = h->d.n_layers, S = h->S();
   const DecCtx& D0 = h->dc[h->nctx - 1];   // every context is sized together
-  const size_t need[] = {2 * L * (size_t)B * S * d * e, 2 * L * (size_t)B * T * d * e, (size_t)B * d * 4,
+  const size_t xbuf = h->xmode ? (size_t)B * S * d * e : 2 * L * (size_t)B * S * d * e;
+  const size_t need[] = {xbuf, 2 * L * (size_t)B * T * d * e, (size_t)B * d * 4,
                          (size_t)B * h->d.ffn * e, (size_t)B * h->d.vocab * 4, (size_t)(I_NEXT + 3 * B + 16) * 4,
                          (size_t)B * out_ld * 4};
   const DevBuf* have[] = {&h->xkv2[h->nctx - 1], &D0.kvself, &D0.dx, &D0.dffn, &D0.logits, &D0.ints, &D0.outbuf};
@@ -666,7 +698,10 @@ void ensure_dec_ws(wcb_handle* h, int B, int T, int out_ld) {
     D.datt.ensure((size_t)B * d * e);
     D.dffn.ensure((size_t)B * h->d.ffn * e);
     D.dstats.ensure((size_t)B * (d / 16) * 2 * 4);
-    D.xpart.ensure((size_t)B * h->H() * kXSplit * 66 * 4);
+    D.xpart.ensure(std::max((size_t)B * h->H() * kXSplit * 66, (size_t)B * h->xenc_split * h->H() * d) * 4);
+    D.xml.ensure((size_t)B * h->xenc_split * h->H() * 2 * 4);
+    D.dqp.ensure((size_t)B * h->H() * d * e);
+    D.du.ensure((size_t)B * h->H() * d * e);
     D.xticket.ensure((size_t)B * h->H() * 4);     // zeroed on allocation; combiners reset their slot
     D.logits.ensure((size_t)B * h->d.vocab * 4);
     D.nchunk = (h->d.vocab + 63) / 64;      // one argmax partial per LM-head workgroup (64 columns)
@@ -679,9 +714,9 @@ void ensure_dec_ws(wcb_handle* h, int B, int T, int out_ld) {
 
 // cross-attention K/V of every decoder layer from the encoder output (A4), once per clip:
 // one GEMM [B·1500, d] × [2·L·d, d]ᵀ written head-split as [L·2][B][H][1500][64]
-void cross_kv(wcb_handle* h, int B, int buf) {
+void cross_kv(wcb_handle* h, int B, int buf, const void* enc) {
   const int d = h->d.d_model, S = h->S(), L = h->d.n_layers;
-  GemmArgs g = rowgemm(h->encout.p, d, h->xkv_w, B * S, 2 * L * d, d, h->xkv2[buf].p, 0);
+  GemmArgs g = rowgemm(enc, d, h->xkv_w, B * S, 2 * L * d, d, h->xkv2[buf].p, 0);
   g.bias = h->xkv_b; g.mode = 1; g.hs_S = S; g.hs_H = h->H(); g.hs_B = B;
   run_gemm(h, "xkv_gemm", g);
 }
@@ -728,26 +763,56 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     GemmArgs o = rowgemm(datt, d, w.o_w, nb, d, d, x, d);
     o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st; o.st_nb = nbk;
     gemm(h->dt, o, st_);
-    // cross attention over the precomputed encoder K/V
-    GemmArgs xq = rowgemm(x, d, w.xq_w, nb, d, d, dq, d);
-    xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk;
-    xq.bias = w.xq_b;
-    gemm(h->dt, xq, st_);
-    AttnArgs xa;
-    const char* xkv = (const char*)h->xkv2[c.buf].p + (l * xkv_l + (size_t)b0 * H * S * 64) * e;
-    xa.q = dq; xa.ldq = d; xa.q_Sb = 1; xa.Sq = 1;
-    xa.k = xkv; xa.v = xkv + (size_t)B * H * S * 64 * e;
-    xa.k_sb = (long)H * S * 64; xa.k_sh = (long)S * 64; xa.k_sk = 64;
-    xa.o = datt; xa.ldo = d; xa.o_Sb = 1; xa.B = nb; xa.H = H; xa.nkeys = S;
-    xa.nsplit = h->xsplit; xa.part = D.xpart.as<float>() + (size_t)b0 * H * kXSplit * 66;
-    xa.ticket = D.xticket.as<int>() + (size_t)b0 * H;
-    xa.variant = h->xvariant;
-    if (h->prof_stamps) {
-      xa.stamp.base = h->stamps.as<unsigned long long>() + (size_t)c.buf * h->stamp_slots() * 2 * kStampSub;
-      xa.stamp.pos = pos;
-      xa.stamp.stride = L * wcb_handle::kMaxSub; xa.stamp.idx = l * wcb_handle::kMaxSub + chain;
+    if (h->xmode == 1) {
+      // cross attention in encoder space: q'_h = W_k,hᵀ q_h (block-diagonal GEMM, K = 64), one pass
+      // over the encoder output per layer for all heads, range combine + W_v,h + b_v
+      GemmArgs xq = rowgemm(x, d, w.xq_w, nb, d, d, dq, d);
+      xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk;
+      xq.bias = w.xq_b;
+      gemm(h->dt, xq, st_);
+      char* dqp = (char*)D.dqp.p + (size_t)b0 * H * d * e;
+      GemmArgs kq = rowgemm(dq, d, w.xkt_w, nb, H * d, 64, dqp, (long)H * d);
+      kq.a_grp_n = d; kq.a_grp_off = 64;
+      gemm(h->dt, kq, st_);
+      XencArgs xa;
+      xa.enc = (const char*)h->xkv2[c.buf].p + (size_t)b0 * S * d * e; xa.enc_sb = (long)S * d;
+      xa.qp = dqp; xa.rows = nb; xa.H = H; xa.D = d; xa.S = S; xa.nsplit = h->xenc_split;
+      xa.variant = h->xenc_variant;
+      xa.part = D.xpart.as<float>() + (size_t)b0 * h->xenc_split * H * d;
+      xa.ml = D.xml.as<float>() + (size_t)b0 * h->xenc_split * H * 2;
+      if (h->prof_stamps) {
+        xa.stamp.base = h->stamps.as<unsigned long long>() + (size_t)c.buf * h->stamp_slots() * 2 * kStampSub;
+        xa.stamp.pos = pos;
+        xa.stamp.stride = L * wcb_handle::kMaxSub; xa.stamp.idx = l * wcb_handle::kMaxSub + chain;
+      }
+      xenc_attention(h->dt, xa, st_);
+      char* du = (char*)D.du.p + (size_t)b0 * H * d * e;
+      xenc_merge(h->dt, xa, du, (long)H * d, st_);
+      GemmArgs vg = rowgemm(du, (long)H * d, w.xv_w, nb, d, d, datt, d);   // o_h = W_v,h u_h + b_v,h
+      vg.a_grp_n = 64; vg.a_grp_off = d; vg.bias = w.xv_b;
+      gemm(h->dt, vg, st_);
+    } else {
+      // cross attention over the precomputed encoder K/V
+      GemmArgs xq = rowgemm(x, d, w.xq_w, nb, d, d, dq, d);
+      xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk;
+      xq.bias = w.xq_b;
+      gemm(h->dt, xq, st_);
+      AttnArgs xa;
+      const char* xkv = (const char*)h->xkv2[c.buf].p + (l * xkv_l + (size_t)b0 * H * S * 64) * e;
+      xa.q = dq; xa.ldq = d; xa.q_Sb = 1; xa.Sq = 1;
+      xa.k = xkv; xa.v = xkv + (size_t)B * H * S * 64 * e;
+      xa.k_sb = (long)H * S * 64; xa.k_sh = (long)S * 64; xa.k_sk = 64;
+      xa.o = datt; xa.ldo = d; xa.o_Sb = 1; xa.B = nb; xa.H = H; xa.nkeys = S;
+      xa.nsplit = h->xsplit; xa.part = D.xpart.as<float>() + (size_t)b0 * H * kXSplit * 66;
+      xa.ticket = D.xticket.as<int>() + (size_t)b0 * H;
+      xa.variant = h->xvariant;
+      if (h->prof_stamps) {
+        xa.stamp.base = h->stamps.as<unsigned long long>() + (size_t)c.buf * h->stamp_slots() * 2 * kStampSub;
+        xa.stamp.pos = pos;
+        xa.stamp.stride = L * wcb_handle::kMaxSub; xa.stamp.idx = l * wcb_handle::kMaxSub + chain;
+      }
+      attention_decode(h->dt, xa, st_);
     }
-    attention_decode(h->dt, xa, st_);
     GemmArgs xo = rowgemm(datt, d, w.xo_w, nb, d, d, x, d);
     xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st; xo.st_nb = nbk;
     gemm(h->dt, xo, st_);
@@ -875,8 +940,12 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     //      last read that buffer has finished. It overlaps the previous call's decode.
     sync_in(h, stream, h->he);
     HIPCHK(hipStreamWaitEvent(h->he, h->ev_dec[buf], 0));
-    encode_impl(h, mel, B, nullptr);
-    h->timed("xkv_gemm_total", 0, 0, h->he, [&] { cross_kv(h, B, buf); });
+    if (h->xmode == 1) {
+      encode_impl(h, mel, B, h->xkv2[buf].p);   // the decode reads the encoder output itself
+    } else {
+      encode_impl(h, mel, B, nullptr);
+      h->timed("xkv_gemm_total", 0, 0, h->he, [&] { cross_kv(h, B, buf, h->encout.p); });
+    }
     HIPCHK(hipEventRecord(h->ev_xkv[buf], h->he));
     // ---- decode stream
     HIPCHK(hipStreamWaitEvent(D.hs, h->ev_xkv[buf], 0));
@@ -928,8 +997,10 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     if (done <= 0) done = steps;
     if (h->prof_stamps) {   // fold this call's cross-attention stamps into the device accumulator
       const double launches_rows = (double)(P - 1 + steps) * h->d.n_layers * B * h->H() * h->S();
-      h->xattn_bytes += launches_rows * 64 * 2 * esize(h->d.dtype);
-      h->xattn_flops += launches_rows * 64 * 4;
+      // algorithmic bytes: K and V (xmode 0) or the encoder output once for all heads (xmode 1)
+      h->xattn_bytes += h->xmode ? launches_rows / h->H() * h->d.d_model * esize(h->d.dtype)
+                                 : launches_rows * 64 * 2 * esize(h->d.dtype);
+      h->xattn_flops += h->xmode ? launches_rows * h->d.d_model * 4 : launches_rows * 64 * 4;
       stamp_reduce(h->stamps.as<unsigned long long>() + (size_t)buf * h->stamp_slots() * 2 * kStampSub, h->stamp_slots(),
                    h->stamp_acc.as<unsigned long long>(), D.hs);
     }
@@ -962,8 +1033,15 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
     if ((size_t)B * (T + 1) * 4 > D.forced.bytes) { quiesce(h); D.forced.ensure((size_t)B * (T + 1) * 4); }
     sync_in(h, stream, h->he);
     HIPCHK(hipStreamWaitEvent(h->he, h->ev_dec[buf], 0));
-    encode_impl(h, mel, B, enc_out);
-    cross_kv(h, B, buf);
+    const size_t enc_bytes = (size_t)B * h->S() * h->d.d_model * esize(h->d.dtype);
+    if (h->xmode == 1) {
+      encode_impl(h, mel, B, h->xkv2[buf].p);
+      if (enc_out) HIPCHK(hipMemcpyAsync(enc_out, h->xkv2[buf].p, enc_bytes, hipMemcpyDeviceToDevice, h->he));
+    } else {
+      void* eo = enc_out ? enc_out : h->encout.p;
+      encode_impl(h, mel, B, eo);
+      cross_kv(h, B, buf, eo);
+    }
     HIPCHK(hipEventRecord(h->ev_xkv[buf], h->he));
     HIPCHK(hipStreamWaitEvent(D.hs, h->ev_xkv[buf], 0));
     int* ints = D.ints.as<int>();
@@ -1187,6 +1265,35 @@ int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void*
       a.ticket = ticket.as<int>();
     }
     attention_decode(DType(dtype), a, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+int wcb_op_cross_attention_enc(int dtype, const void* q, const void* enc, const void* wkt, const void* wv,
+                               const float* bv, void* o, int B, int H, int S, int nsplit, void* stream) {
+  return guarded(nullptr, [&] {
+    const int d = H * 64;
+    REQUIRE(q && enc && wkt && wv && bv && o && B > 0 && B <= 64 && H > 0 && S > 0 && nsplit >= 1 &&
+                nsplit <= kXencMaxSplit, "bad argument");
+    REQUIRE(xenc_supported(DType(dtype), d), "encoder-space cross-attention needs a 16-bit dtype and d <= 1024");
+    static DevBuf qp, u, part, ml;   // workspaces of this test entry point
+    const size_t e = esize(dtype);
+    qp.ensure((size_t)B * H * d * e);
+    u.ensure((size_t)B * H * d * e);
+    part.ensure((size_t)B * nsplit * H * d * 4);
+    ml.ensure((size_t)B * nsplit * H * 2 * 4);
+    GemmArgs kq = rowgemm(q, d, wkt, B, H * d, 64, qp.p, (long)H * d);
+    kq.a_grp_n = d; kq.a_grp_off = 64;
+    gemm(DType(dtype), kq, (hipStream_t)stream);
+    XencArgs xa;
+    xa.enc = enc; xa.enc_sb = (long)S * d; xa.qp = qp.p; xa.rows = B; xa.H = H; xa.D = d; xa.S = S;
+    xa.nsplit = nsplit; xa.part = part.as<float>(); xa.ml = ml.as<float>();
+    if (const char* v = getenv("WCB_XENC_VARIANT")) xa.variant = atoi(v);
+    xenc_attention(DType(dtype), xa, (hipStream_t)stream);
+    xenc_merge(DType(dtype), xa, u.p, (long)H * d, (hipStream_t)stream);
+    GemmArgs vg = rowgemm(u.p, (long)H * d, wv, B, d, d, o, d);
+    vg.a_grp_n = 64; vg.a_grp_off = d; vg.bias = bv;
+    gemm(DType(dtype), vg, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
   });
 }
