@@ -214,3 +214,27 @@ def test_cross_attention_encoder_space(dt, d, B, S, nsplit, variant, monkeypatch
     err = (o.double() - ref).abs().max().item()
     assert err < tol * max(1.0, ref.abs().max().item()), err
     assert torch.equal(_xattn_enc(dt, q, enc, wk, wv, bv, nsplit), o)   # deterministic
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("M,N,K,act,resid", [(4096, 768, 768, 0, False), (6000, 2304, 768, 0, False),
+                                             (5000, 768, 3072, 0, True), (4100, 3072, 768, 1, False),
+                                             (4097, 256, 2304, 1, True)])
+def test_gemm_ring_encoder_shapes(dt, M, N, K, act, resid):
+    """The LDS-ring tile kernel (16-bit, M >= 4096, N % 128 == 0: the encoder GEMMs) with the encoder's
+    epilogues, ragged M, vs fp64."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(DT[dt][0]).cuda()
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(DT[dt][0]).cuda()
+    bias = torch.randn(N, generator=g).float().cuda()
+    R = torch.randn(M, N, generator=g).float().cuda() if resid else None
+    out = _gemm(dt, A, W, bias=bias, act=act, resid=R.clone() if resid else None, out_f32=resid)
+    ref = A.double() @ W.double().T + bias.double()
+    if act:
+        ref = torch.nn.functional.gelu(ref)
+    if resid:
+        ref = ref + R.double()
+    # f32 accumulation; 16-bit output rounding (2^-8 bf16, 2^-11 f16 relative) when not f32
+    tol = 1e-4 if resid else (8e-3 if dt == "bf16" else 1e-3)
+    err = ((out.double() - ref).abs() - tol * ref.abs()).max().item()
+    assert err < 2e-4, err

@@ -77,6 +77,29 @@ def test_teacher_forced_logits_match_reference(model_case):
     np.testing.assert_allclose(top5, g["tf_logits_top5_val"], atol=5e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("size", ["micro", "tiny.en"])
+def test_beam5_ids_match_reference(golden_dir, size):
+    """HF beam search (num_beams = 5, max_length = 24) of the reference model: token-exact."""
+    from oracle.beam_np import generate_beam
+    g = np.load(os.path.join(golden_dir, f"model_{size}_diverse_s0.npz"))
+    ref = g["beam5_ids"]
+    dims = get_dims(size)
+    om = W.OracleModel.from_dims(dims, make_weights(dims, seed=0, recipe="diverse"))
+    mel = W.log_mel(synth_batch(ref.shape[0]), dims.n_mel)
+    ids = generate_beam(om, mel, num_beams=5, max_length=24)
+    assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
+
+
+def test_whisper_trim_semantics():
+    """[tf] generation_whisper.py:1063-1086 + :213-225 with pad == eos (every Whisper config)."""
+    from oracle.beam_np import whisper_trim
+    E = 50256
+    ids = np.array([[1, 2, E, E, E], [3, 4, 5, E, E]])
+    assert np.array_equal(whisper_trim(ids, E, E), [[1, 2, E], [3, 4, 5]])
+    ids = np.array([[1, 2, 3, 4], [5, E, E, E]])
+    assert np.array_equal(whisper_trim(ids, E, E), [[1, 2, 3, 4], [5, E, E, E]])
+
+
 def test_greedy_ids_match_reference(model_case):
     """Token-exact greedy (integer argmax) against the reference's generate()."""
     dims, om, mel, g = model_case

@@ -17,6 +17,7 @@
 #include "kernels.h"
 
 #include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 namespace wcb {
@@ -243,6 +244,183 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(GemmArgs g) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) { v[e] = lo[e]; v[e + 4] = hi[e]; }
     epi_store8<T, EPI>(g, m, n, v);
+  }
+}
+
+// gemm_ring_kernel (16-bit types, the encoder / conv-stem GEMMs): BMxBN tile per workgroup of
+// WMxWN waves, K tiles of 64 staged HBM/L2 → LDS by global_load_lds into a ring of NS stages, so
+// NS-1 tiles stay in flight while one is multiplied. One barrier per K tile: each wave retires its own
+// loads of tile k with a COUNTED s_waitcnt vmcnt (the younger tiles stay in flight across the
+// barrier), the raw s_barrier makes every wave's tile-k bytes visible and tells the issuers that the
+// stage of tile k-1 is free, then tile k+NS-1 is issued into it. No plain global loads inside the
+// loop (hipcc would drain the DMA ring at their use); __syncthreads only after it.
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int BK = 64, CE = 8;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int STAGE = (BM + BN) * 128;
+  constexpr int IA = BM / 8 / NW, IB = BN / 8 / NW, GL = IA + IB;   // glds per wave per K tile
+  static_assert(IA * NW * 8 == BM && IB * NW * 8 == BN, "tile rows must split over waves");
+  using Frag = typename DT<T>::frag;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (wg / tiles_n) * BM, n0 = (wg % tiles_n) * BN;
+
+  const T* A = reinterpret_cast<const T*>(g.A);
+  const T* W = reinterpret_cast<const T*>(g.W);
+  const T* a_src[IA];
+  const T* b_src[IB];
+#pragma unroll
+  for (int i = 0; i < IA; ++i) {
+    const int r = (wave + i * NW) * 8 + (lane >> 3);
+    const int m = min(m0 + r, g.M - 1);
+    a_src[i] = A + a_row(g, m) + ((lane & 7) ^ ((r >> 1) & 7)) * CE;
+  }
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    const int r = (wave + i * NW) * 8 + (lane >> 3);
+    const long n = min(n0 + r, g.N - 1);
+    b_src[i] = W + n * g.ldw + ((lane & 7) ^ ((r >> 1) & 7)) * CE;
+  }
+  auto stage = [&](int st, int k0) {
+    char* base = smem + st * STAGE;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) glds16(a_src[i] + k0, base + (wave + i * NW) * 1024);
+#pragma unroll
+    for (int i = 0; i < IB; ++i) glds16(b_src[i] + k0, base + BM * 128 + (wave + i * NW) * 1024);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = g.K / BK;
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) stage(p, p * BK);
+  int st = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // tiles issued so far: kt .. min(nk, kt + NS - 1) - 1; keep the ones after kt in flight
+    const int ahead = min(nk - 1 - kt, NS - 2);
+    if constexpr (NS >= 4) {
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * GL) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(GL) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (NS == 3) {
+      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(GL) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    {
+      const int nxt = kt + NS - 1;
+      int sn = st + NS - 1;
+      if (sn >= NS) sn -= NS;
+      if (nxt < nk) stage(sn, nxt * BK);
+    }
+    const char* base = smem + st * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      Frag a[FM], b[FN];
+      const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * TM + i * 16 + (lane & 15);
+        a[i] = *reinterpret_cast<const Frag*>(base + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * TN + j * 16 + (lane & 15);
+        b[j] = *reinterpret_cast<const Frag*>(base + BM * 128 + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mma16(a[i], b[j], acc[i][j]);
+    }
+    st = st + 1 == NS ? 0 : st + 1;
+  }
+  __syncthreads();   // every wave is done with the ring: the epilogue reuses its LDS
+
+  // epilogue: f32 tile through LDS (in WM passes of TM rows when the whole tile does not fit), then
+  // 8 columns per lane per store
+  constexpr int LDC = BN + 4;
+  constexpr int PASSES = (BM * LDC * 4 <= 160 * 1024) ? 1 : WM;
+  constexpr int PR = BM / PASSES;
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int ps = 0; ps < PASSES; ++ps) {
+    if (PASSES == 1 || wm == ps) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * TN + j * 16 + (lane & 15);
+        const int n = min(n0 + col, g.N - 1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = wm * TM + i * 16 + (lane >> 4) * 4 + e;
+            const int m = min(m0 + row, g.M - 1);
+            ct[(row - ps * PR) * LDC + col] = epi_pointwise<T, EPI>(g, m, n, acc[i][j][e]);
+          }
+      }
+    }
+    __syncthreads();
+    constexpr int C8 = BN / 8;
+#pragma unroll 2
+    for (int idx = tid; idx < PR * C8; idx += NT) {
+      const int row = idx / C8, c8 = idx % C8;
+      const int m = m0 + ps * PR + row;
+      const int n = n0 + c8 * 8;
+      if (m >= g.M || n >= g.N) continue;
+      float v[8];
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(ct + row * LDC + c8 * 8);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(ct + row * LDC + c8 * 8 + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[e] = lo[e]; v[e + 4] = hi[e]; }
+      epi_store8<T, EPI>(g, m, n, v);
+    }
+    if (PASSES > 1) __syncthreads();
+  }
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI>
+static void launch_ring_e(const GemmArgs& g, hipStream_t s) {
+  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  constexpr int stage_bytes = NS * (BM + BN) * 128;
+  constexpr int epi_full = BM * (BN + 4) * 4;
+  constexpr int epi_bytes = epi_full <= 160 * 1024 ? epi_full : epi_full / WM;
+  constexpr int lds = stage_bytes > epi_bytes ? stage_bytes : epi_bytes;
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int NS>
+static void launch_ring(const GemmArgs& g, hipStream_t s) {
+  const int bits = (g.bias ? E_BIAS : 0) | (g.act == 1 ? E_GELU : 0) | (g.resid ? E_RESID : 0) |
+                   (g.out_f32 ? E_F32 : 0) | (g.addrow ? E_ADDROW : 0) | (g.mode == 1 ? E_HEAD : 0);
+  switch (bits) {
+    case E_BIAS: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS>(g, s); break;
+    case E_BIAS | E_GELU: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_GELU>(g, s); break;
+    case E_BIAS | E_RESID | E_F32: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_RESID | E_F32>(g, s); break;
+    case E_BIAS | E_GELU | E_F32 | E_ADDROW:
+      launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_GELU | E_F32 | E_ADDROW>(g, s); break;
+    case E_BIAS | E_HEAD: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_HEAD>(g, s); break;
+    default: launch_ring_e<T, BM, BN, WM, WN, NS, E_RUNTIME>(g, s); break;
   }
 }
 
@@ -526,7 +704,22 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
     if (!ok) fprintf(stderr, "wcb: no skinny GEMM instance for K=%d\n", g.K);
     return;
   }
-  // Tile choice: 128x128 (4 waves 2x2) when N fills it, else 128x64.
+  // 16-bit encoder-size GEMMs: the LDS-ring kernel (tile by WCB_GEMM_TILE for experiments);
+  // f32 ("exact" mode) and small shapes: the two-stage tile kernel, 128x128 (4 waves 2x2) when N
+  // fills it, else 128x64.
+  // Default: 256x256 (2 stages) when N allows it (measured 1128 vs 990 TFLOP/s at 48000x2304x768
+  // class shapes), else 256x128 (3 stages).
+  static const int variant = [] { const char* v = getenv("WCB_GEMM_TILE"); return v ? atoi(v) : -1; }();
+  if constexpr (sizeof(T) == 2) {
+    if (variant != 0 && g.N % 128 == 0 && g.M >= 4096) {
+      switch (variant < 0 ? (g.N % 256 == 0 ? 2 : 1) : variant) {
+        case 2: launch_ring<T, 256, 256, 2, 4, 2>(g, s); return;
+        case 3: launch_ring<T, 128, 128, 2, 2, 4>(g, s); return;
+        case 4: launch_ring<T, 128, 256, 2, 4, 3>(g, s); return;
+        default: launch_ring<T, 256, 128, 4, 2, 3>(g, s); return;
+      }
+    }
+  }
   if (g.N % 128 == 0) launch_tile<T, 128, 128, 2, 2>(g, s);
   else launch_tile<T, 128, 64, 2, 2>(g, s);
 }
