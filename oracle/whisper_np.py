@@ -16,6 +16,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 from scipy.special import erf
 
+from .beam_np import whisper_trim
 from .bias_ref import AhoCorasick
 
 N_SAMPLES, N_FFT, HOP, N_FRAMES = 480000, 400, 160, 3000
@@ -256,13 +257,14 @@ class OracleModel:
     def generate(self, mel=None, max_length: int = 225, enc=None, min_new_tokens: int = 0,
                  bias: Optional[Sequence[Sequence[int]]] = None, bias_boost: float = 0.0,
                  prefix: Optional[Sequence[int]] = None, return_logits: bool = False,
-                 use_cache: bool = True):
+                 use_cache: bool = True, trim: bool = True):
         """Greedy decode with the reference's eval semantics:
         init = [decoder_start] ([tf] generation_whisper.py:1489,1591-1606); ≤ max_length new
         tokens (max_length+1 total incl. SOT, [tf] generation_whisper.py:1932-1940); fp32
         logits; argmax, lowest index on ties ([tf] generation/utils.py:2894,2925); finished rows
         emit pad; stop when all rows finished ([tf] :2928-2936); output excludes SOT and is right-
-        padded with pad ([tf] generation_whisper.py:936-943,1141-1144).
+        padded with pad ([tf] generation_whisper.py:936-943,1141-1144); with `trim` the trailing EOS
+        and pads are dropped per row as Whisper does ([tf] generation_whisper.py:1063-1086).
         `min_new_tokens` masks EOS (benchmark mode); `bias`/`bias_boost` apply
         the A8 boost (oracle/bias_ref.py). `use_cache=False` recomputes the whole prefix every
         step exactly like `scripts/evaluation.py:178`.
@@ -315,4 +317,6 @@ class OracleModel:
                 h = self.decode_tokens(seq, 0, {}, xkv)
             logits_last = self.lm_head(h[:, -1])
         ids = np.stack(out, axis=1)
+        if trim:   # Whisper's post-processing of the generate() output (oracle/beam_np.py)
+            ids = whisper_trim(ids, self.eos, self.pad)
         return (ids, np.stack(all_logits, axis=1)) if return_logits else ids

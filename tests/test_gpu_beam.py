@@ -1,0 +1,110 @@
+"""GPU: beam search (A9) through the C ABI (k_beam.hip, key-map self-attention, shared encoder rows).
+
+* f32 mode: token-exact against the reference's own beam-5 goldens (HF generate, num_beams = 5).
+* boost / MinNewTokens / prompt prefix / more than 64 rows (row groups): identical to the oracle
+  (oracle/beam_np.py) in f32 mode — parity vs the reference unpinned for the boost (no reference code).
+* bf16 (encoder-space cross-attention, rows_per_enc = beams): batch invariance (every utterance
+  decoded alone gives the same beams as in the batch: the row maps and the shared encoder rows are
+  exact) and identical to the oracle on the high-margin recipe.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import whisper_np as W  # noqa: E402
+from oracle.beam_np import generate_beam  # noqa: E402
+from whisper_context_biasing_amd.config import get_dims  # noqa: E402
+from whisper_context_biasing_amd.model import WhisperCB  # noqa: E402
+from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list  # noqa: E402
+from whisper_context_biasing_amd.weights import make_weights  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+_CASES, _MODELS = {}, {}
+
+
+def case(size, seed, recipe, B):
+    key = (size, seed, recipe, B)
+    if key not in _CASES:
+        dims = get_dims(size)
+        sd = make_weights(dims, seed=seed, recipe=recipe)
+        om = W.OracleModel.from_dims(dims, sd)
+        mel = W.log_mel(synth_batch(B), dims.n_mel)
+        _CASES[key] = (dims, om, mel, om.encode(mel))
+    return _CASES[key]
+
+
+def model(size, seed, recipe, dtype):
+    key = (size, seed, recipe, dtype)
+    if key not in _MODELS:
+        dims = get_dims(size)
+        _MODELS[key] = WhisperCB.from_state_dict(dims, make_weights(dims, seed=seed, recipe=recipe), dtype=dtype)
+    return _MODELS[key]
+
+
+@pytest.mark.parametrize("size", ["micro", "tiny.en"])
+def test_beam5_f32_matches_reference_golden(size):
+    g = np.load(os.path.join(GOLD, f"model_{size}_diverse_s0.npz"))
+    ref = g["beam5_ids"]
+    dims, om, mel, enc = case(size, 0, "diverse", ref.shape[0])
+    m = model(size, 0, "diverse", "f32")
+    for use_graph in (True, False):
+        ids = m.generate(torch.from_numpy(mel), max_length=24, num_beams=5, use_graph=use_graph).cpu().numpy()
+        assert ids.shape == ref.shape and np.array_equal(ids, ref), (use_graph, ids, ref)
+
+
+@pytest.mark.parametrize("nb,lam,min_new,n_phr", [(2, 0.0, 0, 0), (3, 2.0, 0, 200), (5, 2.0, 12, 1000),
+                                                  (8, 8.0, 0, 50)])
+def test_beam_boost_matches_oracle_f32(nb, lam, min_new, n_phr):
+    dims, om, mel, enc = case("micro", 0, "diverse", 2)
+    m = model("micro", 0, "diverse", "f32")
+    plain = om.generate(mel, enc=enc, max_length=24, min_new_tokens=24)
+    phrases = synth_bias_list(n_phr, eot=dims.eos_token_id) if n_phr else []
+    phrases = phrases + [list(map(int, plain[0, 2:5])), list(map(int, plain[1, 1:3])) + [7, 8]]
+    ids = m.generate(torch.from_numpy(mel), max_length=24, num_beams=nb, bias_list=phrases, bias_boost=lam,
+                     min_new_tokens=min_new).cpu().numpy()
+    ref = generate_beam(om, enc=enc, num_beams=nb, max_length=24, bias=phrases, bias_boost=lam,
+                        min_new_tokens=min_new)
+    assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
+
+
+def test_beam_natural_eos_matches_oracle_f32():
+    """Long decode (beams finish on EOS, early-stop heuristic, Whisper trim)."""
+    dims, om, mel, enc = case("micro", 0, "diverse", 2)
+    m = model("micro", 0, "diverse", "f32")
+    ids = m.generate(torch.from_numpy(mel), max_length=120, num_beams=4).cpu().numpy()
+    ref = generate_beam(om, enc=enc, num_beams=4, max_length=120)
+    assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
+
+
+def test_beam_row_groups_match_oracle_f32():
+    """16 clips x 5 beams = 80 decoder rows: two row groups of the skinny decode GEMMs."""
+    dims, om, mel, enc = case("micro", 0, "diverse", 16)
+    m = model("micro", 0, "diverse", "f32")
+    ids = m.generate(torch.from_numpy(mel), max_length=16, num_beams=5).cpu().numpy()
+    ref = generate_beam(om, enc=enc, num_beams=5, max_length=16)
+    assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
+
+
+def test_beam_prompt_prefix_matches_oracle_f32():
+    dims, om, mel, enc = case("micro", 0, "diverse", 2)
+    m = model("micro", 0, "diverse", "f32")
+    prompt = [50361, 100, 200, 300]
+    ids = m.generate(torch.from_numpy(mel), max_length=10, num_beams=3, prompt_ids=prompt).cpu().numpy()
+    ref = generate_beam(om, enc=enc, num_beams=3, max_length=10, prefix=prompt + [dims.decoder_start_token_id])
+    assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
+
+
+def test_beam_bf16_batch_invariant_and_high_margin():
+    dims, om, mel, enc = case("tiny.en", 1, "margin", 4)
+    m = model("tiny.en", 1, "margin", "bf16")
+    x = torch.from_numpy(mel)
+    ids = m.generate(x, max_length=24, num_beams=5).cpu().numpy()
+    for b in range(x.shape[0]):
+        one = m.generate(x[b:b + 1], max_length=24, num_beams=5).cpu().numpy()
+        assert np.array_equal(one[0], ids[b, :one.shape[1]]), (b, one, ids[b])
+    ref = generate_beam(om, enc=enc, num_beams=5, max_length=24)
+    assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)

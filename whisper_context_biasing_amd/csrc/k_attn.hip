@@ -29,7 +29,8 @@ namespace wcb {
 // an agent-scope ticket; the chunk that draws the last ticket reads every partial with sc1 loads,
 // combines them in chunk order (deterministic) and resets the ticket (cdna_hip_programming.md §6
 // Guideline 16, first row of the measured hand-off table).
-template <typename T, int NW, int U>
+// PHYS (beam search): key j of row b lives in cache row phys[(row0 + b)·phys_ld + j] (k_beam.hip).
+template <typename T, int NW, int U, bool PHYS = false>
 __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(AttnArgs a) {
   __shared__ float wo[NW][64];
   __shared__ float wm[NW], wl[NW];
@@ -44,8 +45,11 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(AttnArgs a) {
   const int j_lo = chunk * per, j_hi = min(nk_all, j_lo + per);
   const int nk = max(j_hi - j_lo, 0);
   const T* q = reinterpret_cast<const T*>(a.q) + ((long)b * a.q_Sb + i) * a.ldq + h * 64;
-  const T* kb = reinterpret_cast<const T*>(a.k) + (long)b * a.k_sb + (long)h * a.k_sh + (long)j_lo * a.k_sk + seg * 8;
-  const T* vb = reinterpret_cast<const T*>(a.v) + (long)b * a.k_sb + (long)h * a.k_sh + (long)j_lo * a.k_sk + seg * 8;
+  const long krow = PHYS ? 0L : (long)((a.row0 + b) / a.b_div) * a.k_sb;
+  const int* prow = PHYS ? a.phys + (long)(a.row0 + b) * a.phys_ld + j_lo : nullptr;
+  const T* kb = reinterpret_cast<const T*>(a.k) + krow + (long)h * a.k_sh + (long)j_lo * a.k_sk + seg * 8;
+  const T* vb = reinterpret_cast<const T*>(a.v) + krow + (long)h * a.k_sh + (long)j_lo * a.k_sk + seg * 8;
+  auto koff = [&](int j) -> long { return (long)j * a.k_sk + (PHYS ? (long)prow[j] * a.k_sb : 0L); };
   float qv[8];
   load8f<T>(q + seg * 8, qv);
 
@@ -56,9 +60,9 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(AttnArgs a) {
   for (int j0 = wave * WSPAN; j0 < nk; j0 += GSPAN) {
     float kv[U][8], vv[U][8];
 #pragma unroll
-    for (int u = 0; u < U; ++u) load8f<T>(kb + (long)min(j0 + u * 8 + kg, nk - 1) * a.k_sk, kv[u]);
+    for (int u = 0; u < U; ++u) load8f<T>(kb + koff(min(j0 + u * 8 + kg, nk - 1)), kv[u]);
 #pragma unroll
-    for (int u = 0; u < U; ++u) load8f<T>(vb + (long)min(j0 + u * 8 + kg, nk - 1) * a.k_sk, vv[u]);
+    for (int u = 0; u < U; ++u) load8f<T>(vb + koff(min(j0 + u * 8 + kg, nk - 1)), vv[u]);
     float sc[U];
     float mx = -INFINITY;
 #pragma unroll
@@ -181,8 +185,9 @@ __global__ __launch_bounds__(NW * 64) void attn_decode2p_kernel(AttnArgs a) {
   const int j_lo = chunk * per, j_hi = min(nk_all, j_lo + per);
   const int nk = max(j_hi - j_lo, 0);
   const T* q = reinterpret_cast<const T*>(a.q) + ((long)b * a.q_Sb + i) * a.ldq + h * 64;
-  const T* kb = reinterpret_cast<const T*>(a.k) + (long)b * a.k_sb + (long)h * a.k_sh + (long)j_lo * a.k_sk + seg * 8;
-  const T* vb = reinterpret_cast<const T*>(a.v) + (long)b * a.k_sb + (long)h * a.k_sh + (long)j_lo * a.k_sk + seg * 8;
+  const long krow = (long)((a.row0 + b) / a.b_div) * a.k_sb;
+  const T* kb = reinterpret_cast<const T*>(a.k) + krow + (long)h * a.k_sh + (long)j_lo * a.k_sk + seg * 8;
+  const T* vb = reinterpret_cast<const T*>(a.v) + krow + (long)h * a.k_sh + (long)j_lo * a.k_sk + seg * 8;
   float qv[8];
   load8f<T>(q + seg * 8, qv);
 
@@ -307,6 +312,10 @@ __global__ __launch_bounds__(NW * 64) void attn_decode2p_kernel(AttnArgs a) {
 
 template <typename T>
 static void launch_decode(const AttnArgs& b, dim3 grid, int variant, hipStream_t s) {
+  if (b.phys) {   // beam-search self-attention: keys through the row map
+    hipLaunchKernelGGL((attn_decode_kernel<T, 4, 8, true>), grid, dim3(256), 0, s, b);
+    return;
+  }
   switch (variant) {
     case 0: hipLaunchKernelGGL((attn_decode2p_kernel<T, 8>), grid, dim3(512), 0, s, b); break;
     case 1: hipLaunchKernelGGL((attn_decode_kernel<T, 4, 8>), grid, dim3(256), 0, s, b); break;

@@ -1,0 +1,337 @@
+// Beam search (A9) on the device: HF `_beam_search` ([tf] generation/utils.py:3208-3524, helpers
+// :3008-3204) with the A8 bias boost and the MinNewTokens EOS mask as log-prob processors
+// ([tf] utils.py:3388-3389). Oracle: oracle/beam_np.py.
+//
+// Rows r = b·nb + i (utterance b, running beam i). Per decode step:
+//   beam_topk_kernel  one workgroup per row over the f32 logits row: log_softmax (max, Σexp), the
+//                     boost (root bitmap ∪ trans(state) in an LDS bitmap) and EOS mask, plus the
+//                     beam's running score, then the row's top-K (K = 2·nb) by (score desc, token
+//                     asc). HBM-bound: 4·V bytes per row (the later passes hit L2).
+//   beam_step_kernel  one workgroup per utterance: the top-K of its nb·K row candidates (the global
+//                     top-K over nb·V lies in their union, and per-row token order equals the
+//                     flat-index order beam·V + token), running / finished updates (length penalty,
+//                     -1e9 masks, early-stop heuristic), sequences, AC states, the self-attention key
+//                     map, and the batch-wide stop test by the last arriving utterance.
+// KV-cache reorder without copies (K9): row i's key/value at position t lives in cache row
+// phys[i][t] (the row that computed it). A step writes position `pos` of every row in its own cache
+// row, so choosing parents is a gather of nb·T ints per utterance instead of moving 2·L·t·d
+// elements per row; the self-attention kernel reads each key through the map.
+#include "common.h"
+#include "kernels.h"
+
+namespace wcb {
+
+namespace {
+constexpr int kTopK = 16;                     // per-thread candidate list; K = 2·nb <= 16
+constexpr int kBitWords = kBeamMaxVocab / 32;
+constexpr float kNeg = -1.0e9f;
+
+WCB_DEV bool beam_better(float v, int i, float bv, int bi) { return v > bv || (v == bv && i < bi); }
+
+// δ(s, tok): trans(s) entry if present, else the root child, else the root (k_select.hip)
+WCB_DEV int ac_delta(const BeamArgs& a, int s, int tok) {
+  for (int t = a.trans_off[s]; t < a.trans_off[s + 1]; ++t)
+    if (a.trans_tok[t] == tok) return a.trans_dst[t];
+  const int c = (tok >= 0 && tok < a.V) ? a.root_child[tok] : -1;
+  return c >= 0 ? c : 0;
+}
+
+WCB_DEV float block_max4(float v, float* red) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float r = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  return r;
+}
+WCB_DEV float block_sum4(float v, float* red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float r = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return r;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void beam_init_kernel(BeamArgs a) {
+  const int r = blockIdx.x, i = r % a.nb;
+  const int Lg = a.Lt - a.P;
+  for (int t = threadIdx.x; t < a.T; t += blockDim.x) a.phys[(long)r * a.T + t] = r;
+  for (int t = threadIdx.x; t < Lg; t += blockDim.x) {
+    a.run_seq[(long)r * Lg + t] = a.pad;
+    a.fin_seq[(long)r * Lg + t] = a.pad;
+  }
+  if (threadIdx.x == 0) {
+    a.run_sc[r] = i == 0 ? 0.f : kNeg;        // only beam 0 seeds the first step
+    a.fin_sc[r] = kNeg;
+    a.fin_done[r] = 0;
+    a.fin_len[r] = 0;
+    a.state[r] = 0;
+    if (i == 0) { a.flags[2 * (r / a.nb)] = 1; a.flags[2 * (r / a.nb) + 1] = 0; }
+  }
+}
+
+__global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
+  if (*a.all_done) return;                    // frozen once the search has stopped
+  __shared__ uint32_t bits[kBitWords];
+  __shared__ float red[4];
+  __shared__ float cv[256][kTopK + 1];
+  __shared__ int ci[256][kTopK + 1];
+  __shared__ float wv[4];
+  __shared__ int wi[4], wt[4];
+  const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* row = a.logits + (long)r * a.ld;
+  float m = -INFINITY;
+  for (int v = tid; v < a.V; v += 256) m = fmaxf(m, row[v]);
+  m = block_max4(m, red);
+  float s = 0.f;
+  for (int v = tid; v < a.V; v += 256) s += expf(row[v] - m);
+  const float lsum = logf(block_sum4(s, red));
+  const bool boost = a.lam != 0.f;
+  if (boost) {
+    const int nw = (a.V + 31) >> 5;
+    for (int k = tid; k < nw; k += 256) bits[k] = a.root_bits[k];
+    __syncthreads();
+    const int st = a.state[r];
+    for (int t = a.trans_off[st] + tid; t < a.trans_off[st + 1]; t += 256) {
+      const int v = a.trans_tok[t];
+      atomicOr(&bits[v >> 5], 1u << (v & 31));
+    }
+    __syncthreads();
+  }
+  const bool mask_eos = *a.step < a.min_new;
+  const float rsc = a.run_sc[r];
+  float lv[kTopK];
+  int li[kTopK];
+#pragma unroll
+  for (int k = 0; k < kTopK; ++k) { lv[k] = -INFINITY; li[k] = 0x7fffffff; }
+  for (int v = tid; v < a.V; v += 256) {
+    float x = (row[v] - m) - lsum;                                    // log_softmax
+    if (boost && ((bits[v >> 5] >> (v & 31)) & 1u)) x = x + a.lam;    // bias boost processor
+    if (mask_eos && v == a.eos) x = -INFINITY;                         // MinNewTokens processor
+    x = x + rsc;                                                       // + running beam score
+    if (beam_better(x, v, lv[kTopK - 1], li[kTopK - 1])) {
+      float pv = x;
+      int pi = v;
+#pragma unroll
+      for (int k = 0; k < kTopK; ++k) {
+        if (beam_better(pv, pi, lv[k], li[k])) {
+          const float tv = lv[k];
+          const int ti = li[k];
+          lv[k] = pv; li[k] = pi; pv = tv; pi = ti;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kTopK; ++k) { cv[tid][k] = lv[k]; ci[tid][k] = li[k]; }
+  int head = 0;
+  __syncthreads();
+  for (int k = 0; k < a.K; ++k) {   // K rounds: block argmax over the threads' list heads
+    float hv = head < kTopK ? cv[tid][head] : -INFINITY;
+    int hi = head < kTopK ? ci[tid][head] : 0x7fffffff;
+    int ht = tid;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(hv, o, 64);
+      const int oi = __shfl_xor(hi, o, 64), ot = __shfl_xor(ht, o, 64);
+      if (beam_better(ov, oi, hv, hi)) { hv = ov; hi = oi; ht = ot; }
+    }
+    if (lane == 0) { wv[w] = hv; wi[w] = hi; wt[w] = ht; }
+    __syncthreads();
+    float bv = wv[0];
+    int bi = wi[0], bt = wt[0];
+#pragma unroll
+    for (int q = 1; q < 4; ++q)
+      if (beam_better(wv[q], wi[q], bv, bi)) { bv = wv[q]; bi = wi[q]; bt = wt[q]; }
+    if (tid == bt) ++head;
+    if (tid == 0) { a.cand_val[(long)r * a.K + k] = bv; a.cand_tok[(long)r * a.K + k] = bi; }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void beam_step_kernel(BeamArgs a) {
+  if (*a.all_done) return;
+  __shared__ float tv[kTopK], rlp[kTopK], flv[kTopK];
+  __shared__ int tb[kTopK], tt[kTopK], hit[kTopK];
+  __shared__ int sel[kMaxBeams], fsrc[kMaxBeams], st_old[kMaxBeams];
+  __shared__ float fsc_old[kMaxBeams];
+  __shared__ int fdone_old[kMaxBeams], flen_old[kMaxBeams];
+  __shared__ int seq_old[kMaxBeams][kBeamMaxLen];
+  __shared__ int fin_old[kMaxBeams][kBeamMaxLen];
+  __shared__ int phys_old[kMaxBeams][kBeamMaxLen];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int nb = a.nb, K = a.K, R0 = b * nb;
+  const int step = *a.step;
+  const int cur = a.P + step;                 // tokens in every running sequence before this one
+  const int Lg = a.Lt - a.P;
+  const int unsat_old = a.flags[2 * b];
+  // ---- phase 1 (wave 0): top-K of the nb·K candidates by (score desc, beam·V + token asc)
+  if (tid < 64) {
+    const int nc = nb * K;   // <= 128: two per lane
+    float v0 = -INFINITY, v1 = -INFINITY;
+    int f0 = 0x7fffffff, f1 = 0x7fffffff;
+    if (lane < nc) {
+      const int rr = lane / K, k = lane % K;
+      v0 = a.cand_val[(long)(R0 + rr) * K + k];
+      f0 = rr * a.V + a.cand_tok[(long)(R0 + rr) * K + k];
+    }
+    if (lane + 64 < nc) {
+      const int rr = (lane + 64) / K, k = (lane + 64) % K;
+      v1 = a.cand_val[(long)(R0 + rr) * K + k];
+      f1 = rr * a.V + a.cand_tok[(long)(R0 + rr) * K + k];
+    }
+    for (int k = 0; k < K; ++k) {
+      float bv = v0;
+      int bf = f0;
+      if (beam_better(v1, f1, bv, bf)) { bv = v1; bf = f1; }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int of = __shfl_xor(bf, o, 64);
+        if (beam_better(ov, of, bv, bf)) { bv = ov; bf = of; }
+      }
+      if (f0 == bf) { v0 = -INFINITY; f0 = 0x7fffffff; }
+      else if (f1 == bf) { v1 = -INFINITY; f1 = 0x7fffffff; }
+      if (lane == 0) { tv[k] = bv; tb[k] = bf / a.V; tt[k] = bf % a.V; }
+    }
+  }
+  // old state of the utterance into LDS (new rows are gathers of old rows)
+  for (int e = tid; e < nb * step; e += 256) {
+    const int i = e / step, t = e % step;
+    seq_old[i][t] = a.run_seq[(long)(R0 + i) * Lg + t];
+    fin_old[i][t] = a.fin_seq[(long)(R0 + i) * Lg + t];
+  }
+  for (int e = tid; e < nb * cur; e += 256) {
+    const int i = e / cur, t = e % cur;
+    phys_old[i][t] = a.phys[(long)(R0 + i) * a.T + t];
+  }
+  if (tid < nb) {
+    st_old[tid] = a.state[R0 + tid];
+    fsc_old[tid] = a.fin_sc[R0 + tid];
+    fdone_old[tid] = a.fin_done[R0 + tid];
+    flen_old[tid] = a.fin_len[R0 + tid];
+  }
+  __syncthreads();
+  // ---- phase 2: stopping criteria, running scores, finished-candidate scores
+  if (tid < K) {
+    const int k = tid;
+    const bool h = tt[k] == a.eos || cur + 1 >= a.Lt;
+    hit[k] = h;
+    rlp[k] = h ? tv[k] + kNeg : tv[k];
+    const float den = (float)pow((double)(cur + 1 - a.P), (double)a.len_pen);
+    float fl = tv[k] / den;
+    if (!unsat_old) fl = fl + kNeg;
+    const bool did = h && k < nb;
+    if (!did) fl = fl + kNeg;
+    flv[k] = fl;
+  }
+  __syncthreads();
+  if (tid < K) {   // running beams: rank among the K by (rlp desc, k asc)
+    const int k = tid;
+    int rank = 0;
+    for (int q = 0; q < K; ++q) rank += beam_better(rlp[q], q, rlp[k], k);
+    if (rank < nb) sel[rank] = k;
+  } else if (tid >= 64 && tid < 64 + nb + K) {   // finished: merge old nb and new K, keep nb
+    const int m = tid - 64;
+    const float vm = m < nb ? fsc_old[m] : flv[m - nb];
+    int rank = 0;
+    for (int q = 0; q < nb + K; ++q) {
+      const float vq = q < nb ? fsc_old[q] : flv[q - nb];
+      rank += beam_better(vq, q, vm, m);
+    }
+    if (rank < nb) fsrc[rank] = m;
+  }
+  __syncthreads();
+  // ---- phase 3: write the new running and finished beams
+  for (int e = tid; e < nb * (step + 1); e += 256) {
+    const int i = e / (step + 1), t = e % (step + 1);
+    const int k = sel[i];
+    a.run_seq[(long)(R0 + i) * Lg + t] = t < step ? seq_old[tb[k]][t] : tt[k];
+    const int m = fsrc[i];
+    int fv;
+    if (m < nb) fv = t < step ? fin_old[m][t] : a.pad;   // old finished sequences end before `step`
+    else fv = t < step ? seq_old[tb[m - nb]][t] : tt[m - nb];
+    a.fin_seq[(long)(R0 + i) * Lg + t] = fv;
+  }
+  for (int e = tid; e < nb * cur; e += 256) {
+    const int i = e / cur, t = e % cur;
+    a.phys[(long)(R0 + i) * a.T + t] = phys_old[tb[sel[i]]][t];
+  }
+  if (tid < nb) {
+    const int i = tid, k = sel[i];
+    if (cur < a.T) a.phys[(long)(R0 + i) * a.T + cur] = R0 + i;   // the next step writes its own row
+    a.next_ids[R0 + i] = tt[k];
+    a.run_sc[R0 + i] = rlp[k];
+    a.state[R0 + i] = a.lam != 0.f ? ac_delta(a, st_old[tb[k]], tt[k]) : 0;
+    const int m = fsrc[i];
+    if (m < nb) {
+      a.fin_sc[R0 + i] = fsc_old[m];
+      a.fin_done[R0 + i] = fdone_old[m];
+      a.fin_len[R0 + i] = flen_old[m];
+    } else {
+      a.fin_sc[R0 + i] = flv[m - nb];
+      a.fin_done[R0 + i] = (hit[m - nb] && (m - nb) < nb) ? 1 : 0;
+      a.fin_len[R0 + i] = step + 1;
+    }
+  }
+  __syncthreads();
+  // ---- phase 4: early-stop heuristic (early_stopping = False) and the batch-wide stop test
+  if (tid == 0) {
+    const float den = (float)pow((double)(cur + 1 - a.P), (double)a.len_pen);
+    const float best = rlp[sel[0]] / den;
+    float mn = INFINITY;
+    for (int j = 0; j < nb; ++j) {
+      const int m = fsrc[j];
+      mn = fminf(mn, m < nb ? fsc_old[m] : flv[m - nb]);
+    }
+    bool any = false;
+    for (int j = 0; j < nb; ++j) {
+      const int m = fsrc[j];
+      const bool done = m < nb ? fdone_old[m] != 0 : (hit[m - nb] && (m - nb) < nb);
+      any |= best > (done ? mn : kNeg);
+    }
+    bool allhit = true;
+    for (int k = 0; k < K; ++k) allhit &= hit[k] != 0;
+    __hip_atomic_store(a.flags + 2 * b, (unsat_old && any) ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.flags + 2 * b + 1, allhit ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();
+    if (atomicAdd(a.ticket, 1) == a.B - 1) {    // every utterance has arrived
+      __threadfence();
+      bool any_unsat = false, all_hit = true;
+      for (int u = 0; u < a.B; ++u) {
+        any_unsat |= __hip_atomic_load(a.flags + 2 * u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        all_hit &= __hip_atomic_load(a.flags + 2 * u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+      }
+      *a.step = step + 1;
+      *a.pos = *a.pos + 1;
+      if ((!any_unsat || all_hit) && *a.all_done == 0) *a.all_done = step + 1;
+      *a.ticket = 0;
+      __threadfence();
+    }
+  }
+}
+
+// out[b][t] = best finished sequence of utterance b (pad after its length); *out_len = max length
+__global__ __launch_bounds__(256) void beam_output_kernel(BeamArgs a) {
+  const int b = blockIdx.x, r = b * a.nb;
+  const int Lg = a.Lt - a.P;
+  const int len = a.fin_len[r];
+  for (int t = threadIdx.x; t < a.out_ld; t += blockDim.x)
+    a.out_ids[(long)b * a.out_ld + t] = (t < len && t < Lg) ? a.fin_seq[(long)r * Lg + t] : a.pad;
+  if (threadIdx.x == 0) atomicMax(a.out_len, len);
+}
+
+void beam_init(const BeamArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(beam_init_kernel, dim3(a.B * a.nb), dim3(256), 0, s, a);
+}
+void beam_select(const BeamArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(beam_topk_kernel, dim3(a.B * a.nb), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(beam_step_kernel, dim3(a.B), dim3(256), 0, s, a);
+}
+void beam_output(const BeamArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(beam_output_kernel, dim3(a.B), dim3(256), 0, s, a);
+}
+
+}  // namespace wcb

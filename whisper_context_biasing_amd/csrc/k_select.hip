@@ -133,6 +133,19 @@ void gather_col(int* dst, const int* src, int M, int ld, int col, hipStream_t s)
   hipLaunchKernelGGL(gather_col_kernel, dim3(1), dim3(256), 0, s, dst, src, M, ld, col);
 }
 
+struct IntChunk { int n; int v[256]; };
+__global__ void write_i32_kernel(int* dst, IntChunk c) {
+  for (int i = threadIdx.x; i < c.n; i += blockDim.x) dst[i] = c.v[i];
+}
+void write_i32(int* dst, const int* host_src, int n, hipStream_t s) {
+  for (int o = 0; o < n; o += 256) {
+    IntChunk c;
+    c.n = n - o < 256 ? n - o : 256;
+    for (int i = 0; i < c.n; ++i) c.v[i] = host_src[o + i];
+    hipLaunchKernelGGL(write_i32_kernel, dim3(1), dim3(256), 0, s, dst + o, c);
+  }
+}
+
 void select_finalize(const SelectArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(select_finalize_kernel, dim3(a.M), dim3(64), 0, s, a);
 }

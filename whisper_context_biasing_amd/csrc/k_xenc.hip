@@ -77,7 +77,7 @@ __global__ __launch_bounds__(512) void attn_xenc_kernel(XencArgs a) {
   const int per = ((a.S + a.nsplit - 1) / a.nsplit + CK - 1) / CK * CK;
   const int k_lo = split * per, k_hi = min(a.S, k_lo + per);
   const int nch = k_hi > k_lo ? (k_hi - k_lo + CK - 1) / CK : 0;
-  const T* E = reinterpret_cast<const T*>(a.enc) + (long)b * a.enc_sb;
+  const T* E = reinterpret_cast<const T*>(a.enc) + (long)((a.row0 + b) / a.rows_per_enc) * a.enc_sb;
 
   // q' fragments of this wave's k-steps: lane → head lane&15 (zero for heads >= H)
   const int hq = lane & 15;
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(XregCfg<D>::NW * 64, 2) void attn_xenc_reg_kernel(X
   const int k_lo = split * per, k_hi = min(a.S, k_lo + per);
   const int nch = k_hi > k_lo ? (k_hi - k_lo + CK - 1) / CK : 0;
   const int cw0 = wave * CW;
-  const T* E = reinterpret_cast<const T*>(a.enc) + (long)b * a.enc_sb + cw0 + 8 * (lane >> 4);
+  const T* E = reinterpret_cast<const T*>(a.enc) + (long)((a.row0 + b) / a.rows_per_enc) * a.enc_sb + cw0 + 8 * (lane >> 4);
 
   const int hq = lane & 15;
   Frag qf[KSW];

@@ -69,6 +69,10 @@ struct AttnArgs {
   int nsplit = 1; float* part = nullptr; int* ticket = nullptr;
   Stamp stamp;   // profiling (decode graph): per-launch start/end stamps
   int variant = 1;   // decode kernel variant (k_attn.hip launch_decode)
+  // K/V row of query row b (decode kernels): phys ? phys[(row0 + b)·phys_ld + j] (beam search: the
+  // cache row that computed key j) : (row0 + b) / b_div (beams sharing one clip's cross K/V)
+  int row0 = 0, b_div = 1;
+  const int* phys = nullptr; long phys_ld = 0;
 };
 void attention_decode(DType t, const AttnArgs& a, hipStream_t s);   // VALU, any T, any Sq
 bool attention_flash(DType t, const AttnArgs& a, hipStream_t s);    // MFMA encoder (16-bit T)
@@ -86,6 +90,7 @@ struct XencArgs {
   float* ml = nullptr;                          // [rows][nsplit][H][2] (max, Σ p)
   Stamp stamp;
   int variant = 1;                              // 1 register chunk ring, 0 LDS-DMA chunk ring
+  int row0 = 0, rows_per_enc = 1;               // row b reads encoder output (row0 + b) / rows_per_enc
 };
 bool xenc_supported(DType t, int D);
 void xenc_attention(DType t, const XencArgs& a, hipStream_t s);
@@ -120,7 +125,36 @@ void select_finalize(const SelectArgs& a, hipStream_t s);        // partials alr
 void advance_forced(int* next_ids, const int* forced, int M, int ld, int* pos, hipStream_t s);
 void gather_col(int* dst, const int* src, int M, int ld, int col, hipStream_t s);
 
+// Beam search (k_beam.hip): HF _beam_search with the A8 boost / MinNewTokens as log-prob processors.
+// Rows r = b·nb + i (utterance b, running beam i); sequences hold generated tokens only.
+constexpr int kMaxBeams = 8;
+constexpr int kBeamMaxLen = 448;       // max_target_positions of every Whisper size
+constexpr int kBeamMaxVocab = 53248;   // LDS boost bitmap
+struct BeamArgs {
+  const float* logits = nullptr; long ld = 0; int V = 0;
+  int B = 0, nb = 0, K = 0;            // utterances, beams, candidates kept per step (2·nb)
+  int P = 0, Lt = 0, T = 0;            // prefix length, max total length, cache positions (phys row)
+  int eos = 0, pad = 0, min_new = 0;
+  float lam = 0.f, len_pen = 1.f;
+  const uint32_t* root_bits = nullptr; const int* root_child = nullptr;
+  const int* trans_off = nullptr; const int* trans_tok = nullptr; const int* trans_dst = nullptr;
+  int* step = nullptr; int* pos = nullptr; int* all_done = nullptr; int* ticket = nullptr;
+  int* next_ids = nullptr; int* state = nullptr;        // [R]
+  float* run_sc = nullptr; int* run_seq = nullptr;      // [R], [R][Lt-P]
+  int* phys = nullptr;                                  // [R][T] cache row of every key position
+  float* cand_val = nullptr; int* cand_tok = nullptr;   // [R][K] per-row top-K
+  float* fin_sc = nullptr; int* fin_done = nullptr; int* fin_len = nullptr; int* fin_seq = nullptr;  // [B·nb](·(Lt-P))
+  int* flags = nullptr;                                 // [B][2]: heuristic unsatisfied, all K hit
+  int* out_ids = nullptr; int out_ld = 0; int* out_len = nullptr;
+};
+void beam_init(const BeamArgs& a, hipStream_t s);
+void beam_select(const BeamArgs& a, hipStream_t s);   // per-row top-K + per-utterance step
+void beam_output(const BeamArgs& a, hipStream_t s);   // best finished sequence per utterance
+
 void fill_i32(int* p, int v, long n, hipStream_t s);
+// dst[0..n) = host values, passed by value in the kernel arguments (stream-ordered, no host buffer
+// lifetime or pageable-copy ordering to worry about)
+void write_i32(int* dst, const int* host_src, int n, hipStream_t s);
 // Per launch slot (kStampSub sub-slots each): add max(end) − min(start) to acc[0] (ticks) and 1 to
 // acc[1] if the slot was used; then zero the n launch slots.
 void stamp_reduce(unsigned long long* slots, long n, unsigned long long* acc, hipStream_t s);

@@ -122,13 +122,13 @@ struct wcb_bias {
 // i+1 decode on its own stream while call i is still decoding: two latency-bound step chains share
 // the GPU instead of one.
 struct DecCtx {
-  static constexpr int kMaxSub = 4;
+  static constexpr int kMaxSub = 8;             // row groups of <= 64 rows (beam search: B·nb rows)
   hipStream_t hs = nullptr;                     // decode stream of this context
   hipStream_t sub[kMaxSub] = {};                // row-group chains (fork/join inside the step graph)
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSub] = {};
   int dec_B = 0, dec_T = 0;
   DevBuf kvself, dx, dh, dq, dqp, du, datt, dffn, dstats, xpart, xml, xticket, logits, part_val, part_idx, ints, outbuf,
-      forced;
+      forced, beam;
   int nchunk = 64;
   hipGraphExec_t gexec = nullptr;               // captured decode step
   std::string gkey;
@@ -411,7 +411,7 @@ void wcb_destroy(wcb_handle* h) {
   for (DecCtx& D : h->dc) {
     if (D.gexec) (void)hipGraphExecDestroy(D.gexec);
     for (DevBuf* b : {&D.kvself, &D.dx, &D.dh, &D.dq, &D.dqp, &D.du, &D.datt, &D.dffn, &D.dstats, &D.xpart, &D.xml, &D.xticket,
-                      &D.logits, &D.part_val, &D.part_idx, &D.ints, &D.outbuf, &D.forced})
+                      &D.logits, &D.part_val, &D.part_idx, &D.ints, &D.outbuf, &D.forced, &D.beam})
       b->release();
     if (D.ev_fork) (void)hipEventDestroy(D.ev_fork);
     for (int i = 0; i < DecCtx::kMaxSub; ++i) {
@@ -673,10 +673,11 @@ void drop_graphs(wcb_handle* h) {
   }
 }
 
-void ensure_dec_ws(wcb_handle* h, int B, int T, int out_ld) {
+// decode workspace: B decoder rows (clips x beams) reading `clips` encoder outputs
+void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld) {
   const size_t e = esize(h->d.dtype), d = h->d.d_model, L = h->d.n_layers, S = h->S();
   const DecCtx& D0 = h->dc[h->nctx - 1];   // every context is sized together
-  const size_t xbuf = h->xmode ? (size_t)B * S * d * e : 2 * L * (size_t)B * S * d * e;
+  const size_t xbuf = h->xmode ? (size_t)clips * S * d * e : 2 * L * (size_t)clips * S * d * e;
   const size_t need[] = {xbuf, 2 * L * (size_t)B * T * d * e, (size_t)B * d * 4,
                          (size_t)B * h->d.ffn * e, (size_t)B * h->d.vocab * 4, (size_t)(I_NEXT + 3 * B + 16) * 4,
                          (size_t)B * out_ld * 4};
@@ -722,11 +723,14 @@ void cross_kv(wcb_handle* h, int B, int buf, const void* enc) {
 }
 
 struct StepCfg {
-  int B, T, out_ld, buf;   // buf: which cross-K/V buffer the step reads
+  int B, T, out_ld, buf;   // B: decoder rows (clips x beams); buf: which cross-K/V buffer the step reads
   bool lm_head, select;
   float* logits_out; long logits_ld;   // LM head destination
   const wcb_bias* bias; float lam; int min_new;
   const int* forced; int forced_ld;    // advance_forced source when !select
+  int clips = 0, nb = 1;               // encoder outputs (0: B) and decoder rows per encoder output
+  const int* phys = nullptr;           // beam search: cache row of every key position [B][T]
+  const BeamArgs* beam = nullptr;      // beam search selection (replaces the greedy select)
 };
 
 // Decoder layers + LM head for rows [b0, b0 + nb) of the batch on stream `st_`: WhisperDecoder.forward
@@ -746,7 +750,8 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
   char* datt = (char*)D.datt.p + (size_t)b0 * d * e;
   char* dffn = (char*)D.dffn.p + (size_t)b0 * h->d.ffn * e;
   const size_t cache_l = 2 * (size_t)B * H * T * 64;   // elements per layer (K then V)
-  const size_t xkv_l = 2 * (size_t)B * H * S * 64;
+  const int clips = c.clips ? c.clips : B;
+  const size_t xkv_l = 2 * (size_t)clips * H * S * 64;
   for (int l = 0; l < L; ++l) {
     const LayerW& w = h->dec[l];
     char* cache = (char*)D.kvself.p + (l * cache_l + (size_t)b0 * H * T * 64) * e;
@@ -756,8 +761,10 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     gemm(h->dt, q, st_);
     AttnArgs a;
     a.q = dq; a.ldq = d; a.q_Sb = 1; a.Sq = 1;
-    a.k = cache; a.v = cache + (size_t)B * H * T * 64 * e;
+    const char* cache0 = (char*)D.kvself.p + l * cache_l * e;   // K/V rows addressed absolutely
+    a.k = cache0; a.v = cache0 + (size_t)B * H * T * 64 * e;
     a.k_sb = (long)H * T * 64; a.k_sh = (long)T * 64; a.k_sk = 64;
+    a.row0 = b0; a.phys = c.phys; a.phys_ld = T;
     a.o = datt; a.ldo = d; a.o_Sb = 1; a.B = nb; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1;
     attention_decode(h->dt, a, st_);
     GemmArgs o = rowgemm(datt, d, w.o_w, nb, d, d, x, d);
@@ -775,7 +782,8 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       kq.a_grp_n = d; kq.a_grp_off = 64;
       gemm(h->dt, kq, st_);
       XencArgs xa;
-      xa.enc = (const char*)h->xkv2[c.buf].p + (size_t)b0 * S * d * e; xa.enc_sb = (long)S * d;
+      xa.enc = h->xkv2[c.buf].p; xa.enc_sb = (long)S * d;
+      xa.row0 = b0; xa.rows_per_enc = c.nb;   // beams of a clip share its encoder output
       xa.qp = dqp; xa.rows = nb; xa.H = H; xa.D = d; xa.S = S; xa.nsplit = h->xenc_split;
       xa.variant = h->xenc_variant;
       xa.part = D.xpart.as<float>() + (size_t)b0 * h->xenc_split * H * d;
@@ -798,9 +806,10 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       xq.bias = w.xq_b;
       gemm(h->dt, xq, st_);
       AttnArgs xa;
-      const char* xkv = (const char*)h->xkv2[c.buf].p + (l * xkv_l + (size_t)b0 * H * S * 64) * e;
+      const char* xkv = (const char*)h->xkv2[c.buf].p + l * xkv_l * e;
       xa.q = dq; xa.ldq = d; xa.q_Sb = 1; xa.Sq = 1;
-      xa.k = xkv; xa.v = xkv + (size_t)B * H * S * 64 * e;
+      xa.k = xkv; xa.v = xkv + (size_t)clips * H * S * 64 * e;
+      xa.row0 = b0; xa.b_div = c.nb;           // beams of a clip share its cross K/V
       xa.k_sb = (long)H * S * 64; xa.k_sh = (long)S * 64; xa.k_sk = 64;
       xa.o = datt; xa.ldo = d; xa.o_Sb = 1; xa.B = nb; xa.H = H; xa.nkeys = S;
       xa.nsplit = h->xsplit; xa.part = D.xpart.as<float>() + (size_t)b0 * H * kXSplit * 66;
@@ -829,7 +838,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     GemmArgs lm = rowgemm(x, d, h->tok_emb, nb, h->d.vocab, d, c.logits_out + (size_t)b0 * c.logits_ld, c.logits_ld);
     lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b; lm.st_in = st; lm.st_nb = nbk;
     lm.out_f32 = 1;
-    if (c.select) {   // argmax partials with the root boost + EOS mask fused into the LM head
+    if (c.select && !c.beam) {   // argmax partials with the root boost + EOS mask fused into the LM head
       lm.sel_val = D.part_val.as<float>() + (size_t)b0 * D.nchunk;
       lm.sel_idx = D.part_idx.as<int>() + (size_t)b0 * D.nchunk;
       lm.sel_root_bits = c.bias->root_bits.as<uint32_t>(); lm.sel_lam = c.lam;
@@ -850,9 +859,13 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
   int* pos = ints + I_POS;
   int* next_ids = ints + I_NEXT;
   embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, D.dx.as<float>(), D.dstats.as<float>(), B, d, D.hs);
-  const int ns = std::max(1, std::min(h->n_sub, B));
-  if (ns == 1) {
-    decode_rows(h, c, 0, B, 0, D.hs);
+  const int ngrp = (B + 63) / 64;   // the skinny decode GEMMs take <= 64 rows
+  const int ns = std::max(ngrp, std::max(1, std::min(h->n_sub, B)));
+  if (ns == 1 || !D.sub[0]) {        // one stream: row groups back to back
+    for (int i = 0; i < ns; ++i) {
+      const int b0 = (int)((long)B * i / ns), b1 = (int)((long)B * (i + 1) / ns);
+      decode_rows(h, c, b0, b1 - b0, i, D.hs);
+    }
   } else {
     HIPCHK(hipEventRecord(D.ev_fork, D.hs));
     for (int i = 0; i < ns; ++i) {
@@ -863,7 +876,9 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     }
     for (int i = 0; i < ns; ++i) HIPCHK(hipStreamWaitEvent(D.hs, D.ev_join[i], 0));
   }
-  if (c.select) {
+  if (c.select && c.beam) {
+    beam_select(*c.beam, D.hs);
+  } else if (c.select) {
     SelectArgs s;
     s.logits = c.logits_out; s.ld = c.logits_ld; s.M = B; s.V = h->d.vocab;
     s.lam = c.lam;
@@ -918,8 +933,11 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
   return guarded(h, [&] {
     REQUIRE(h && cfg && out_ids && out_steps && B > 0, "bad argument");
     if (!h->ready) throw WcbError(WCB_ERR_STATE, "weights not finalized");
-    REQUIRE(cfg->num_beams == 1, "num_beams > 1 is not implemented in this build");
-    REQUIRE(B <= 64, "batch > 64 per handle: split the batch (decode GEMMs are the skinny M<=64 path)");
+    const int nb = cfg->num_beams;
+    REQUIRE(nb >= 1 && nb <= kMaxBeams, "num_beams must be in [1, 8]");
+    const int R = B * nb;   // decoder rows: utterance b, beam i -> row b*nb + i
+    REQUIRE(B <= 64, "batch > 64 per handle: split the batch");
+    REQUIRE(R <= 64 * DecCtx::kMaxSub, "batch x num_beams > 512 rows per call: split the batch");
     REQUIRE(cfg->bias_boost >= 0.f, "bias_boost must be >= 0");
     REQUIRE(cfg->max_new_tokens >= 1, "max_new_tokens must be >= 1");
     REQUIRE(mel != nullptr, "mel is required");
@@ -932,10 +950,21 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     const bool fixed_len = cfg->min_new_tokens >= cfg->max_new_tokens;   // EOS masked: no host polling
     const int out_ld = cfg->max_new_tokens;
     const int Tc = std::min(T, h->d.n_text_ctx);
+    if (nb > 1) {
+      REQUIRE(cfg->max_new_tokens <= kBeamMaxLen && Tc <= kBeamMaxLen, "beam search: more than 448 positions");
+      REQUIRE(cfg->bias_boost == 0.f || h->d.vocab <= kBeamMaxVocab, "beam search boost: vocabulary too large");
+    }
     ensure_enc_ws(h, B);
-    ensure_dec_ws(h, B, Tc, out_ld);
+    ensure_dec_ws(h, B, R, Tc, out_ld);
     const int buf = h->gen_count++ % h->nctx;
     DecCtx& D = h->dc[buf];
+    // beam state [R] / [R][max_new] / [R][Tc] / [R][K] / [B][2] in one buffer
+    const int K = 2 * nb, Lg = cfg->max_new_tokens;
+    const size_t beam_words[] = {(size_t)R, (size_t)R, (size_t)R, (size_t)R, (size_t)R * Lg, (size_t)R * Lg,
+                                 (size_t)R * Tc, (size_t)R * K, (size_t)R * K, (size_t)B * 2};
+    size_t beam_bytes = 0;
+    for (size_t w : beam_words) beam_bytes += (w * 4 + 255) / 256 * 256;
+    if (nb > 1 && beam_bytes > D.beam.bytes) { quiesce(h); D.beam.ensure(beam_bytes); }
     // ---- encoder stream: front end → encoder → cross-K/V into buffer `buf` once the decode that
     //      last read that buffer has finished. It overlaps the previous call's decode.
     sync_in(h, stream, h->he);
@@ -950,23 +979,43 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     // ---- decode stream
     HIPCHK(hipStreamWaitEvent(D.hs, h->ev_xkv[buf], 0));
     int* ints = D.ints.as<int>();
-    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 3 * B) * 4, D.hs));
-    if (prefix) {
-      if ((size_t)B * P * 4 > D.forced.bytes) { quiesce(h); D.forced.ensure((size_t)B * P * 4); }
-      for (int b = 0; b < B; ++b)
-        HIPCHK(hipMemcpyAsync(D.forced.as<int>() + (size_t)b * P, prefix, (size_t)P * 4, hipMemcpyHostToDevice, D.hs));
-      gather_col(ints + I_NEXT, D.forced.as<int>(), B, P, 0, D.hs);
+    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 3 * R) * 4, D.hs));
+    if (prefix) {   // one prefix row shared by every decoder row (forced_ld = 0 below)
+      if ((size_t)P * 4 > D.forced.bytes) { quiesce(h); D.forced.ensure((size_t)P * 4); }
+      write_i32(D.forced.as<int>(), prefix, P, D.hs);
+      gather_col(ints + I_NEXT, D.forced.as<int>(), R, 0, 0, D.hs);
     } else {
-      fill_i32(ints + I_NEXT, h->d.decoder_start_token_id, B, D.hs);
+      fill_i32(ints + I_NEXT, h->d.decoder_start_token_id, R, D.hs);
     }
-    StepCfg sc{B, Tc, out_ld, buf, false, false, D.logits.as<float>(), (long)h->d.vocab, bs, cfg->bias_boost,
-               cfg->min_new_tokens, D.forced.as<int>(), P};
+    BeamArgs bm;
+    if (nb > 1) {
+      char* p = (char*)D.beam.p;
+      auto take = [&](int i) { char* q = p; p += (beam_words[i] * 4 + 255) / 256 * 256; return q; };
+      bm.run_sc = (float*)take(0); bm.fin_sc = (float*)take(1); bm.fin_done = (int*)take(2); bm.fin_len = (int*)take(3);
+      bm.run_seq = (int*)take(4); bm.fin_seq = (int*)take(5); bm.phys = (int*)take(6);
+      bm.cand_val = (float*)take(7); bm.cand_tok = (int*)take(8); bm.flags = (int*)take(9);
+      bm.logits = D.logits.as<float>(); bm.ld = h->d.vocab; bm.V = h->d.vocab;
+      bm.B = B; bm.nb = nb; bm.K = K; bm.P = P; bm.Lt = T; bm.T = Tc;
+      bm.eos = h->d.eos_token_id; bm.pad = h->d.pad_token_id; bm.min_new = cfg->min_new_tokens;
+      bm.lam = cfg->bias_boost; bm.len_pen = 1.f;
+      bm.root_bits = bs->root_bits.as<uint32_t>(); bm.root_child = bs->root_child.as<int>();
+      bm.trans_off = bs->trans_off.as<int>(); bm.trans_tok = bs->trans_tok.as<int>(); bm.trans_dst = bs->trans_dst.as<int>();
+      bm.step = ints + I_STEP; bm.pos = ints + I_POS; bm.all_done = ints + I_DONE; bm.ticket = ints + I_TICKET;
+      bm.next_ids = ints + I_NEXT; bm.state = ints + I_NEXT + R;
+      bm.out_ids = D.outbuf.as<int>(); bm.out_ld = out_ld; bm.out_len = ints + I_UNFIN;
+      beam_init(bm, D.hs);   // before the prefill: the self-attention reads keys through bm.phys
+    }
+    StepCfg sc{R, Tc, out_ld, buf, false, false, D.logits.as<float>(), (long)h->d.vocab, bs, cfg->bias_boost,
+               cfg->min_new_tokens, D.forced.as<int>(), 0};
+    sc.clips = B;
+    sc.nb = nb;
+    if (nb > 1) { sc.phys = bm.phys; sc.beam = &bm; }
     for (int p = 0; p + 1 < P; ++p) decode_step(h, sc);   // prompt prefill, teacher-forced
     sc.lm_head = true;
     sc.select = true;
     char key[256];
-    snprintf(key, sizeof key, "%d/%d/%d/%p/%a/%d/%d/%d", B, Tc, out_ld, (const void*)bs, cfg->bias_boost,
-             cfg->min_new_tokens, h->n_sub, (int)h->prof_stamps);
+    snprintf(key, sizeof key, "%d/%d/%d/%d/%p/%a/%d/%d/%d/%d", B, nb, Tc, out_ld, (const void*)bs, cfg->bias_boost,
+             cfg->min_new_tokens, h->n_sub, (int)h->prof_stamps, P);
     const int max_new = cfg->max_new_tokens;
     const int chunk = 8;
     int done = 0, steps = 0;
@@ -996,13 +1045,24 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     });
     if (done <= 0) done = steps;
     if (h->prof_stamps) {   // fold this call's cross-attention stamps into the device accumulator
-      const double launches_rows = (double)(P - 1 + steps) * h->d.n_layers * B * h->H() * h->S();
+      const double launches_rows = (double)(P - 1 + steps) * h->d.n_layers * R * h->H() * h->S();
       // algorithmic bytes: K and V (xmode 0) or the encoder output once for all heads (xmode 1)
       h->xattn_bytes += h->xmode ? launches_rows / h->H() * h->d.d_model * esize(h->d.dtype)
                                  : launches_rows * 64 * 2 * esize(h->d.dtype);
       h->xattn_flops += h->xmode ? launches_rows * h->d.d_model * 4 : launches_rows * 64 * 4;
       stamp_reduce(h->stamps.as<unsigned long long>() + (size_t)buf * h->stamp_slots() * 2 * kStampSub, h->stamp_slots(),
                    h->stamp_acc.as<unsigned long long>(), D.hs);
+    }
+    if (nb > 1) {   // best finished sequence of every utterance; its columns = the longest of them
+      beam_output(bm, D.hs);
+      int olen = 0;
+      HIPCHK(hipMemcpyAsync(out_ids, D.outbuf.p, (size_t)B * out_ld * 4, hipMemcpyDeviceToDevice, D.hs));
+      HIPCHK(hipMemcpyAsync(&olen, ints + I_UNFIN, 4, hipMemcpyDeviceToHost, D.hs));
+      HIPCHK(hipEventRecord(h->ev_dec[buf], D.hs));
+      HIPCHK(hipStreamSynchronize(D.hs));
+      *out_steps = std::min(olen, max_new);
+      sync_out(h, stream, D.hs);
+      return;
     }
     HIPCHK(hipMemcpyAsync(out_ids, D.outbuf.p, (size_t)B * out_ld * 4, hipMemcpyDeviceToDevice, D.hs));
     HIPCHK(hipEventRecord(h->ev_dec[buf], D.hs));
@@ -1027,7 +1087,7 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
     REQUIRE(B <= 64, "batch > 64 per handle");
     REQUIRE(T <= h->d.n_text_ctx, "decoder_input_ids longer than max_target_positions");
     ensure_enc_ws(h, B);
-    ensure_dec_ws(h, B, T, 1);
+    ensure_dec_ws(h, B, B, T, 1);
     const int buf = h->gen_count++ % h->nctx;
     DecCtx& D = h->dc[buf];
     if ((size_t)B * (T + 1) * 4 > D.forced.bytes) { quiesce(h); D.forced.ensure((size_t)B * (T + 1) * 4); }

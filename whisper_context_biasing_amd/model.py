@@ -219,7 +219,11 @@ class WhisperCB:
                  num_beams: Optional[int] = None, bias_list=None, bias_boost: float = 0.0,
                  min_new_tokens: int = 0, prompt_ids=None, return_dict_in_generate: bool = False,
                  generation_config=None, use_graph: bool = True, block: bool = True, **kwargs):
-        """Greedy decode with the reference's eval semantics.
+        """Greedy (num_beams = 1, the reference's eval setting) or HF beam
+        search (num_beams = 2..8, [tf] generation/utils.py:3208) on the device.
+
+        Returns Whisper's post-processed ids ([tf] generation_whisper.py:1063-1086, 213-225): per row
+        the trailing pads and the final EOS dropped, right-padded with pad to the longest row.
 
         `labels` / `bias_spans` are accepted and ignored for token selection exactly like the
         reference (`[tf] trainer_seq2seq.py:310-329`), unless `bias_boost > 0` and no explicit
@@ -235,19 +239,24 @@ class WhisperCB:
         gc = generation_config or self.generation_config
         max_length = int(max_length if max_length is not None else getattr(gc, "max_length", 448))
         num_beams = int(num_beams if num_beams is not None else getattr(gc, "num_beams", 1) or 1)
-        if num_beams != 1:
-            raise NotImplementedError("beam search is not implemented in this build (greedy only)")
+        if not 1 <= num_beams <= 8:
+            raise ValueError("num_beams must be in [1, 8]")
         x = self._features(input_features)
         B = x.shape[0]
         prefix = [self.dims.decoder_start_token_id]
         if prompt_ids is not None:
             prefix = [int(t) for t in prompt_ids] + prefix
-        max_new = min(max_length, self.dims.n_text_ctx + 1 - len(prefix))
+        # HF: max_length + prompt tokens, capped at max_target_positions ([tf] generation_whisper.py:1932-1940)
+        max_new = min(max_length, self.dims.n_text_ctx - len(prefix))
+        if max_new < 1:
+            raise ValueError("prompt leaves no room for new tokens")
+        if num_beams > 1:
+            block = True                           # the best-sequence length is read back on the host
         phrases = bias_list
         if phrases is None and bias_boost > 0 and bias_spans is not None:
             phrases = self._spans_to_phrases(bias_spans)
         bl = self.bias_list(phrases) if (phrases and bias_boost > 0) else None
-        cfg = _lib.WcbGenCfg(max_new, int(min_new_tokens), 1, float(bias_boost), int(use_graph), int(not block))
+        cfg = _lib.WcbGenCfg(max_new, int(min_new_tokens), num_beams, float(bias_boost), int(use_graph), int(not block))
         out = torch.empty(B, max_new, dtype=torch.int32, device=self.device)
         steps = C.c_int32(0)
         pre = np.asarray(prefix, dtype=np.int32)
@@ -261,7 +270,28 @@ class WhisperCB:
         if return_dict_in_generate:
             sot = torch.tensor(prefix, dtype=torch.int64, device=self.device)[None].expand(B, -1)
             return GenerateOutput(sequences=torch.cat([sot, ids], dim=1))
-        return ids
+        return self._whisper_trim(ids)
+
+    def _whisper_trim(self, ids: torch.Tensor) -> torch.Tensor:
+        """Whisper's short-form post-processing ([tf] generation_whisper.py:1063-1086, then
+        _pad_to_max_length :213-225): per row drop the pads (all but one when pad == eos) and the
+        final EOS, then right-pad every row with pad to the longest one."""
+        eos, pad = self.dims.eos_token_id, self.dims.pad_token_id
+        rows = ids.cpu().numpy()
+        lens = []
+        for r in rows:
+            n = len(r)
+            if n and r[-1] == pad:
+                n -= int((r == pad).sum()) - (1 if pad == eos else 0)
+            if n and r[n - 1] == eos:
+                n -= 1
+            lens.append(n)
+        W = max(lens, default=0)
+        out = ids[:, :W].clone()
+        for i, n in enumerate(lens):
+            if n < W:
+                out[i, n:] = pad
+        return out
 
     def synchronize(self):
         """Wait for every queued front-end / encoder / decode operation of this model."""
