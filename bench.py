@@ -189,7 +189,9 @@ def main():
         avg_ms = p["ms"] / p["launches"]
         achieved = p["flops"] / p["launches"] / (avg_ms * 1e-3) / 1e12
         peak = {"bf16": PEAK_BF16_TFLOPS, "f16": PEAK_F16_TFLOPS}.get(args.dtype, PEAK_F32_TFLOPS)
-        roofs["enc_gemm"] = {"bound": "mfma", "kernel": "gemm_tile_kernel (encoder conv/QKV/out/fc1/fc2)",
+        kn = ("gemm_ring_kernel (encoder QKV/out/fc1/fc2/conv2, LDS-DMA ring; conv1 gemm_tile_kernel)"
+              if args.dtype in ("bf16", "f16") else "gemm_tile_kernel (encoder conv/QKV/out/fc1/fc2)")
+        roofs["enc_gemm"] = {"bound": "mfma", "kernel": kn,
                              "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                              "frac": round(achieved / peak, 4), "traffic": None,
                              "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": p["flops"] / p["launches"],

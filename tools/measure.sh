@@ -12,8 +12,10 @@ timeout -k 10 300 python bench.py --no-cpu-baseline --no-profile > "$O/bench_nop
 cat "$O/bench_noprof.json"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/trace" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$O/trace_bench.json" 2> "$O/trace_bench.err" || exit 1
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run --output-format csv -- python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-profile > /dev/null 2> "$O/pmc_fetch.err" || exit 1
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write" -o run --output-format csv -- python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-profile > /dev/null 2> "$O/pmc_write.err" || exit 1
+# PMC passes on a light run of the same launches (4 tokens, serialised batches): one counter group each
+PMC_ARGS="--steps 1 --warmup 1 --new-tokens 4 --no-overlap --no-cpu-baseline --no-profile"
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run --output-format csv -- python3 "$R/bench.py" $PMC_ARGS > "$O/pmc_fetch.out" 2> "$O/pmc_fetch.err" || { tail -5 "$O/pmc_fetch.err"; exit 1; }
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write" -o run --output-format csv -- python3 "$R/bench.py" $PMC_ARGS > "$O/pmc_write.out" 2> "$O/pmc_write.err" || { tail -5 "$O/pmc_write.err"; exit 1; }
 cd "$R"
 python tools/prof_summary.py "$(ls "$O"/trace/*kernel_trace.csv "$O"/trace/*/*kernel_trace.csv 2>/dev/null | head -1)" 40 > "$O/kernel_summary.txt"
 cat "$O/kernel_summary.txt" | head -25

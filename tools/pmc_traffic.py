@@ -2,9 +2,9 @@
 
 MI355X_MICROARCH.md (HBM, gfx950): FETCH_SIZE counts half the bytes of wide coalesced streaming reads
 (double it); WRITE_SIZE is exact for 16-B/lane stores. Kernel classes follow bench.py's roofline names:
-  dec_xattn  attn_decode_kernel launches with the largest grid (the split-KV cross-attention:
-             nsplit x rows x heads workgroups; the self-attention has rows x heads)
-  enc_gemm   gemm_tile_kernel launches (encoder conv / QKV / out / fc1 / fc2 and the cross-K/V GEMM)
+  dec_xattn  attn_xenc_* launches (encoder-space cross-attention, 16-bit modes), else the
+             attn_decode* launches with the largest grid (cross-attention over precomputed K/V)
+  enc_gemm   gemm_ring_kernel / gemm_tile_kernel launches (encoder conv / QKV / out / fc1 / fc2)
 
 usage: python tools/pmc_traffic.py <fetch_pass_dir> <write_pass_dir> <out.json> [algorithmic bytes/launch json]
 """
@@ -17,9 +17,11 @@ import sys
 
 
 def classify(name: str, grid: int, xattn_grid: int):
-    if "attn_decode_kernel" in name and grid == xattn_grid:
+    if "attn_xenc" in name:
         return "dec_xattn"
-    if "gemm_tile_kernel" in name:
+    if "attn_decode" in name and grid == xattn_grid and xattn_grid > 0:
+        return "dec_xattn"
+    if "gemm_tile_kernel" in name or "gemm_ring_kernel" in name:
         return "enc_gemm"
     return None
 
@@ -37,7 +39,8 @@ def load(pass_dir: str, counter: str):
             key = (f, r.get("Dispatch_Id") or r.get("Correlation_Id"))
             per[key] += float(r["Counter_Value"])
             meta[key] = (r["Kernel_Name"], int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0))
-    xattn_grid = max([g for n, g in meta.values() if "attn_decode_kernel" in n] or [0])
+    has_xenc = any("attn_xenc" in n for n, g in meta.values())
+    xattn_grid = 0 if has_xenc else max([g for n, g in meta.values() if "attn_decode" in n] or [0])
     out = collections.defaultdict(list)
     for k, v in per.items():
         cls = classify(*meta[k], xattn_grid)
@@ -49,7 +52,7 @@ def load(pass_dir: str, counter: str):
 def main():
     fetch = load(sys.argv[1], "FETCH_SIZE")
     write = load(sys.argv[2], "WRITE_SIZE")
-    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py --steps 1 --warmup 1",
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py --steps 1 --warmup 1 --new-tokens 4 --no-overlap (batch 32: same launches as the bench)",
            "correction": "FETCH_SIZE(KB) x 1024 x 2 (gfx950 wide-read undercount) + WRITE_SIZE(KB) x 1024",
            "kernels": {}}
     for cls in sorted(set(fetch) | set(write)):
