@@ -76,9 +76,11 @@ int wcb_log_mel(wcb_handle* h, const float* pcm, int B, int n_samples, int64_t p
 int wcb_encode(wcb_handle* h, const float* mel, int B, void* enc_out, void* stream);
 
 /* replaces model.generate(input_features, max_length=...) as called by
- * [tf] trainer_seq2seq.py:329: greedy from [decoder_start] (+ optional prefix), bias boost,
- * out_ids int32 DEVICE [B][cfg->max_new_tokens] (finished rows padded with pad_token_id),
- * *out_steps = number of generated columns (all rows finished or max_new_tokens).
+ * [tf] trainer_seq2seq.py:329: greedy (num_beams = 1) or HF beam search (num_beams 2..8,
+ * [tf] generation/utils.py:3208) from [decoder_start] (+ optional prefix), bias boost,
+ * out_ids int32 DEVICE [B][cfg->max_new_tokens] (finished rows padded with pad_token_id; beams: the
+ * best finished sequence of each clip), *out_steps = number of generated columns (greedy: all rows
+ * finished or max_new_tokens; beams: the longest best sequence). Beam search always blocks.
  * The front end/encoder run on one library stream and the decode on another, with two cross-K/V
  * buffers: call i+1's encoder overlaps call i's decode (async_out = 1 keeps `stream` free). */
 int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg, const wcb_bias* bias,

@@ -88,6 +88,10 @@ WCB_DEV void epi_store8(const GemmArgs& g, int m, int n, float* v) {
     const f32x4 r1 = *reinterpret_cast<const f32x4*>(g.resid + off + 4);
 #pragma unroll
     for (int j = 0; j < 4; ++j) { v[j] += r0[j]; v[j + 4] += r1[j]; }
+    if (g.clamp != 0.f) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fminf(fmaxf(v[j], -g.clamp), g.clamp);
+    }
   }
   if (has<EPI>(g, E_F32)) store8<float>(reinterpret_cast<float*>(g.out) + off, v);
   else store8<T>(reinterpret_cast<T*>(g.out) + off, v);

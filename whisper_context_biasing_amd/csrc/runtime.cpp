@@ -657,6 +657,7 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
     run_gemm(h, "enc_gemm", f1);
     GemmArgs f2 = rowgemm(h->ffn.p, h->d.ffn, w.fc2_w, (int)M, d, h->d.ffn, h->x.p, d);
     f2.bias = w.fc2_b; f2.resid = h->x.as<float>(); f2.out_f32 = 1;
+    if (h->dt == kF16) f2.clamp = 65504.f - 1000.f;   // fp16 layer-output clamp (large-v3 fp16 config)
     run_gemm(h, "enc_gemm", f2);
   }
   void* dst = enc_out ? enc_out : h->encout.p;
