@@ -108,3 +108,43 @@ def test_beam_bf16_batch_invariant_and_high_margin():
         assert np.array_equal(one[0], ids[b, :one.shape[1]]), (b, one, ids[b])
     ref = generate_beam(om, enc=enc, num_beams=5, max_length=24)
     assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
+
+
+def _one_layer(size, seed, recipe, B, dtype):
+    dims = get_dims(size, n_layers=1)
+    sd = make_weights(dims, seed=seed, recipe=recipe)
+    om = W.OracleModel.from_dims(dims, sd)
+    mel = W.log_mel(synth_batch(B), dims.n_mel)
+    return dims, om, mel, WhisperCB.from_state_dict(dims, sd, dtype=dtype)
+
+
+def _batch_invariant(m, x, **kw):
+    ids = m.generate(x, **kw).cpu().numpy()
+    for b in range(x.shape[0]):
+        one = m.generate(x[b:b + 1], **kw).cpu().numpy()[0]
+        assert np.array_equal(one, ids[b, :len(one)]), (b, one, ids[b])
+        assert (ids[b, len(one):] == m.dims.pad_token_id).all()
+    return ids
+
+
+def test_beam_c5_shape_f16_kv_mode():
+    """C5 shape (large-v3 layer: d = 1280, 20 heads, 128 mels, V = 51866) in fp16: the precomputed
+    cross-K/V path shared by the beams of a clip (b_div), the f16 encoder clamp epilogue, a 5000-phrase
+    boost. Batch-invariant; identical to the oracle without boost on the high-margin recipe."""
+    dims, om, mel, m = _one_layer("large-v3", 1, "margin", 3, "f16")
+    x = torch.from_numpy(mel)
+    phrases = synth_bias_list(5000, eot=dims.eos_token_id)
+    _batch_invariant(m, x, max_length=12, num_beams=5, bias_list=phrases, bias_boost=2.0)
+    ids = m.generate(x, max_length=12, num_beams=5).cpu().numpy()
+    ref = generate_beam(om, mel=mel, num_beams=5, max_length=12)
+    assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
+
+
+def test_beam_c3_shape_bf16_row_groups():
+    """C3 shape (medium layer: d = 1024, encoder-space cross-attention) with 13 clips x 5 beams = 65
+    decoder rows (two row groups): batch-invariant, and identical to the oracle on the high-margin recipe."""
+    dims, om, mel, m = _one_layer("medium", 1, "margin", 13, "bf16")
+    x = torch.from_numpy(mel)
+    ids = _batch_invariant(m, x, max_length=8, num_beams=5)
+    ref = generate_beam(om, mel=mel, num_beams=5, max_length=8)
+    assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)

@@ -48,7 +48,7 @@ def model(size, seed, recipe, dtype):
     return _MODELS[key]
 
 
-@pytest.mark.parametrize("dtype,tol", [("f32", 2e-4), ("bf16", 6e-2)])
+@pytest.mark.parametrize("dtype,tol", [("f32", 2e-4), ("bf16", 6e-2), ("f16", 1.5e-2)])
 @pytest.mark.parametrize("size", ["micro", "tiny.en"])
 def test_encoder_matches_oracle(size, dtype, tol):
     dims, sd, om, mel, enc = case(size, 0, "diverse", 2)

@@ -244,8 +244,9 @@ template <int D> struct XregCfg {
   static constexpr int LDS = NW * TILE + RED;
 };
 
-template <typename T, int D>
-__global__ __launch_bounds__(XregCfg<D>::NW * 64, 2) void attn_xenc_reg_kernel(XencArgs a) {
+// NR = chunks in flight per wave (register ring depth): 2 (two workgroups per CU) or 3 (one).
+template <typename T, int D, int NR>
+__global__ __launch_bounds__(XregCfg<D>::NW * 64, NR == 2 ? 2 : 1) void attn_xenc_reg_kernel(XencArgs a) {
   using Frag = typename DT<T>::frag;
   using C = XregCfg<D>;
   constexpr int CK = kXencCK, NW = C::NW, CW = C::CW, KSW = C::KSW, CTW = C::CTW, PANEL = C::PANEL;
@@ -301,7 +302,7 @@ __global__ __launch_bounds__(XregCfg<D>::NW * 64, 2) void attn_xenc_reg_kernel(X
       *reinterpret_cast<Frag*>(pb + swz(lane & 15, cc)) = f[0][ks];
       *reinterpret_cast<Frag*>(pb + swz(16 + (lane & 15), cc)) = f[1][ks];
     }
-    load_chunk(f, c + 2);   // the registers are free: refill two chunks ahead (unconditionally: a
+    load_chunk(f, c + NR);  // the registers are free: refill NR chunks ahead (unconditionally: a
                             // load under a branch makes hipcc drain every load at the loop head)
     f32x4* rb = red + (c & 1) * NW * 2 * 64;
     rb[(wave * 2 + 0) * 64 + lane] = s0;
@@ -347,13 +348,25 @@ __global__ __launch_bounds__(XregCfg<D>::NW * 64, 2) void attn_xenc_reg_kernel(X
   };
 
   if (nch > 0) {
-    // chunks in pairs; an odd count gets one fully masked chunk (p = 0, running max unchanged)
-    Frag fa[2][KSW], fb[2][KSW];
-    load_chunk(fa, 0);
-    load_chunk(fb, 1);
-    for (int c = 0; c < nch; c += 2) {
-      body(fa, c);
-      body(fb, c + 1);
+    // chunks in groups of NR; a short last group gets fully masked chunks (p = 0, running max kept)
+    if constexpr (NR == 2) {
+      Frag fa[2][KSW], fb[2][KSW];
+      load_chunk(fa, 0);
+      load_chunk(fb, 1);
+      for (int c = 0; c < nch; c += 2) {
+        body(fa, c);
+        body(fb, c + 1);
+      }
+    } else {
+      Frag fa[2][KSW], fb[2][KSW], fc[2][KSW];
+      load_chunk(fa, 0);
+      load_chunk(fb, 1);
+      load_chunk(fc, 2);
+      for (int c = 0; c < nch; c += 3) {
+        body(fa, c);
+        body(fb, c + 1);
+        body(fc, c + 2);
+      }
     }
   }
   // ---- range partials: lane holds Uᵀ[cw0 + 16t + 4(lane>>4) + e][head lane&15]
@@ -424,14 +437,19 @@ static void launch_xenc(const XencArgs& a, hipStream_t s) {
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)attn_xenc_kernel<T, D>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               XencCfg<D>::LDS);
-    (void)hipFuncSetAttribute((const void*)attn_xenc_reg_kernel<T, D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)attn_xenc_reg_kernel<T, D, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              XregCfg<D>::LDS);
+    (void)hipFuncSetAttribute((const void*)attn_xenc_reg_kernel<T, D, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               XregCfg<D>::LDS);
     attr_set = true;
   }
   if (a.variant == 0)
     hipLaunchKernelGGL((attn_xenc_kernel<T, D>), dim3(a.nsplit, a.rows), dim3(kXencNW * 64), XencCfg<D>::LDS, s, a);
+  else if (a.variant == 2)
+    hipLaunchKernelGGL((attn_xenc_reg_kernel<T, D, 3>), dim3(a.nsplit, a.rows), dim3(XregCfg<D>::NW * 64),
+                       XregCfg<D>::LDS, s, a);
   else
-    hipLaunchKernelGGL((attn_xenc_reg_kernel<T, D>), dim3(a.nsplit, a.rows), dim3(XregCfg<D>::NW * 64),
+    hipLaunchKernelGGL((attn_xenc_reg_kernel<T, D, 2>), dim3(a.nsplit, a.rows), dim3(XregCfg<D>::NW * 64),
                        XregCfg<D>::LDS, s, a);
 }
 

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <thread>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -102,6 +103,8 @@ struct LayerW {
   float *ln2_w = nullptr, *ln2_b = nullptr;
   // encoder-space cross-attention (k_xenc.hip): W_k,hᵀ repacked [H][d][64], W_v [d][d], b_v
   void* xkt_w = nullptr; void* xv_w = nullptr; float* xv_b = nullptr;
+  // q'_h straight from the normalised residual: W_qk,h = W_k,hᵀ W_q,h ([H·d][d]), b_qk,h = W_k,hᵀ b_q,h
+  void* xqk_w = nullptr; float* xqk_b = nullptr;
 };
 
 struct ProfEntry {
@@ -161,6 +164,7 @@ struct wcb_handle {
   int xmode = 1;
   int xenc_split = 8;   // key ranges per row of the encoder-space kernel (rows x ranges workgroups)
   int xenc_variant = 1; // attn_xenc kernel variant (k_xenc.hip)
+  int xqk = 0;          // 1: one GEMM LN(x) → q' with W_k,hᵀW_q,h precombined (WCB_XQK; measured slower: 14 MB per layer)
   std::map<std::string, std::vector<float>> host_w;
   std::vector<DevBuf> owned;
   bool ready = false;
@@ -356,6 +360,7 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     if (const char* xm = getenv("WCB_XMODE")) h->xmode = (atoi(xm) != 0 && h->xmode) ? 1 : 0;
     if (const char* xs = getenv("WCB_XENC_SPLIT")) h->xenc_split = std::max(1, std::min(atoi(xs), kXencMaxSplit));
     if (const char* xv = getenv("WCB_XENC_VARIANT")) h->xenc_variant = atoi(xv);
+    if (const char* xq = getenv("WCB_XQK")) h->xqk = atoi(xq);
     // DFT table [416 cols][416 k]: col 2b = win·cos(2πbk/400), col 2b+1 = −win·sin(2πbk/400)
     std::vector<float> dft((size_t)kNCol * kNCol, 0.f);
     for (int c = 0; c < 402; ++c) {
@@ -534,6 +539,28 @@ int wcb_finalize_weights(wcb_handle* h) {
         lw.xkt_w = h->upload_t(wkt);
         lw.xv_w = h->upload_t(wv);
         lw.xv_b = h->upload_f(bv);
+        if (h->xqk) {
+          // W_qk[h·d + c][n] = Σ_i W_k[h·64 + i][c] · W_q[h·64 + i][n] (q rows pre-scaled), one head per
+          // host thread; rounded to the model dtype once
+          std::vector<float> wqk((size_t)H * dd, 0.f), bqk((size_t)H * d, 0.f);
+          std::vector<std::thread> th;
+          for (int hh = 0; hh < H; ++hh)
+            th.emplace_back([&, hh] {
+              for (int ii = 0; ii < 64; ++ii) {
+                const float* qr = wq.data() + (size_t)(hh * 64 + ii) * d;
+                const float* kr = wk.data() + (size_t)(hh * 64 + ii) * d;
+                for (int c = 0; c < d; ++c) {
+                  const float a = kr[c];
+                  float* o = wqk.data() + ((size_t)hh * d + c) * d;
+                  for (int n = 0; n < d; ++n) o[n] += a * qr[n];
+                  bqk[(size_t)hh * d + c] += a * bq[hh * 64 + ii];
+                }
+              }
+            });
+          for (auto& t : th) t.join();
+          lw.xqk_w = h->upload_t(wqk);
+          lw.xqk_b = h->upload_f(bqk);
+        }
       } else {
         std::copy(wk.begin(), wk.end(), xkv_w.begin() + (size_t)(2 * i) * dd);
         std::copy(wv.begin(), wv.end(), xkv_w.begin() + (size_t)(2 * i + 1) * dd);
@@ -774,14 +801,21 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     if (h->xmode == 1) {
       // cross attention in encoder space: q'_h = W_k,hᵀ q_h (block-diagonal GEMM, K = 64), one pass
       // over the encoder output per layer for all heads, range combine + W_v,h + b_v
-      GemmArgs xq = rowgemm(x, d, w.xq_w, nb, d, d, dq, d);
-      xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk;
-      xq.bias = w.xq_b;
-      gemm(h->dt, xq, st_);
       char* dqp = (char*)D.dqp.p + (size_t)b0 * H * d * e;
-      GemmArgs kq = rowgemm(dq, d, w.xkt_w, nb, H * d, 64, dqp, (long)H * d);
-      kq.a_grp_n = d; kq.a_grp_off = 64;
-      gemm(h->dt, kq, st_);
+      if (w.xqk_w) {   // q' = (W_k,hᵀ W_q,h) LN(x) + W_k,hᵀ b_q,h: one GEMM
+        GemmArgs xq = rowgemm(x, d, w.xqk_w, nb, H * d, d, dqp, (long)H * d);
+        xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk;
+        xq.bias = w.xqk_b;
+        gemm(h->dt, xq, st_);
+      } else {
+        GemmArgs xq = rowgemm(x, d, w.xq_w, nb, d, d, dq, d);
+        xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk;
+        xq.bias = w.xq_b;
+        gemm(h->dt, xq, st_);
+        GemmArgs kq = rowgemm(dq, d, w.xkt_w, nb, H * d, 64, dqp, (long)H * d);
+        kq.a_grp_n = d; kq.a_grp_off = 64;
+        gemm(h->dt, kq, st_);
+      }
       XencArgs xa;
       xa.enc = h->xkv2[c.buf].p; xa.enc_sb = (long)S * d;
       xa.row0 = b0; xa.rows_per_enc = c.nb;   // beams of a clip share its encoder output
