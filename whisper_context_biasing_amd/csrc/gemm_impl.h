@@ -448,6 +448,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float red[SL][MF * 16][BNC + 1];
   __shared__ float st_mean[MF * 16], st_rstd[MF * 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int mb = blockIdx.y * MF * 16;   // row block (M split over grid.y: more workgroups, less A per CU)
   // LN statistics partials first: the oldest loads retire first (in-order vmcnt), so the row
   // statistics are ready while the weight stream is still in flight
   constexpr int NB = NW * KS * 2;                          // 16-column blocks per row (K / 16)
@@ -458,7 +459,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
   if constexpr (LN) {
 #pragma unroll
     for (int ps = 0; ps < PASSES; ++ps) {
-      const int m = min(ps * RPP + tid / TPR, g.M - 1);
+      const int m = min(mb + ps * RPP + tid / TPR, g.M - 1);
       s1[ps] = 0.f;
       s2[ps] = 0.f;
       float2 pv[NB / TPR];
@@ -485,7 +486,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
   float pf_bias[EP], pf_res[EP];
 #pragma unroll
   for (int ep = 0; ep < EP; ++ep) {
-    const int t = ep * NT + tid, row = t / BNC, nn = n0 + t % BNC;
+    const int t = ep * NT + tid, row = mb + t / BNC, nn = n0 + t % BNC;
     const bool ok = t < MF * 16 * BNC && row < g.M && nn < g.N;
     pf_bias[ep] = (ok && g.bias) ? g.bias[nn] : 0.f;
     pf_res[ep] = (ok && g.resid && g.mode == 0) ? g.resid[c_row(g, row) + nn] : 0.f;
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
     float xv[MF][KS][8];
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
-      const int m = min(i * 16 + (lane & 15), g.M - 1);
+      const int m = min(mb + i * 16 + (lane & 15), g.M - 1);
       const float* xr = X + a_row(g, m) + kb;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -555,7 +556,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
     const T* A = reinterpret_cast<const T*>(g.A) + (g.a_grp_n ? (long)(n0 / g.a_grp_n) * g.a_grp_off : 0L);
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
-      const int m = min(i * 16 + (lane & 15), g.M - 1);
+      const int m = min(mb + i * 16 + (lane & 15), g.M - 1);
       const T* ap = A + a_row(g, m) + kb;
       Frag a[KS];
 #pragma unroll
@@ -587,13 +588,13 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
 #pragma unroll
   for (int ep = 0; ep < EP; ++ep) {
     const int t = ep * NT + tid;
-    const int row = t / BNC, col = t % BNC;
+    const int lrow = t / BNC, col = t % BNC, row = mb + lrow;
     const int nn = n0 + col;
     const bool valid = t < MF * 16 * BNC && row < g.M && nn < g.N;
     float v = 0.f;
     if (valid) {
 #pragma unroll
-      for (int w = 0; w < SL; ++w) v += red[w][row][col];
+      for (int w = 0; w < SL; ++w) v += red[w][lrow][col];
       v += pf_bias[ep];
       if (g.act == 1) v = gelu_t<T>(v);
       if (g.addrow) v += g.addrow[(long)(g.c_Mb ? row % g.c_Mb : row) * g.N + nn];
@@ -677,15 +678,20 @@ static void launch_tile(const GemmArgs& g, hipStream_t s) {
 
 template <typename T, int MF, int NF, int NW, int KS>
 static void launch_skinny_k(const GemmArgs& g, hipStream_t s) {
-  const int grid = (g.N + NF * 16 - 1) / (NF * 16);
-  if (g.ln_w) hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NF, NW, KS, true>), dim3(grid), dim3(NW * 64), 0, s, g);
-  else hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NF, NW, KS, false>), dim3(grid), dim3(NW * 64), 0, s, g);
+  const dim3 grid((g.N + NF * 16 - 1) / (NF * 16), (g.M + MF * 16 - 1) / (MF * 16));
+  if (g.ln_w) hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NF, NW, KS, true>), grid, dim3(NW * 64), 0, s, g);
+  else hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NF, NW, KS, false>), grid, dim3(NW * 64), 0, s, g);
 }
 
 // K = NW waves x KS steps x 32: pick the wave count first, then the (compile-time) steps per wave.
 template <typename T, int MF, int NF>
 static bool launch_skinny_mf(const GemmArgs& g, hipStream_t s) {
   const int K = g.K;
+  // WCB_SK_NW: preferred waves per workgroup where an instance exists for K (experiments)
+  static const int sk_nw = [] { const char* v = getenv("WCB_SK_NW"); return v ? atoi(v) : 0; }();
+#define WCB_SKP(nw, ks) if (sk_nw == nw && K == nw * ks * 32) { launch_skinny_k<T, MF, NF, nw, ks>(g, s); return true; }
+  WCB_SKP(4, 6) WCB_SKP(12, 2) WCB_SKP(8, 12) WCB_SKP(12, 8) WCB_SKP(4, 24)
+#undef WCB_SKP
 #define WCB_SK(nw, ks) if (K == nw * ks * 32) { launch_skinny_k<T, MF, NF, nw, ks>(g, s); return true; }
   WCB_SK(1, 1) WCB_SK(1, 2) WCB_SK(2, 2) WCB_SK(4, 2) WCB_SK(4, 3) WCB_SK(4, 4) WCB_SK(8, 2)
   WCB_SK(8, 3) WCB_SK(8, 4) WCB_SK(8, 5) WCB_SK(8, 6) WCB_SK(16, 4) WCB_SK(16, 5) WCB_SK(16, 6)
@@ -697,13 +703,17 @@ static bool launch_skinny_mf(const GemmArgs& g, hipStream_t s) {
 template <typename T>
 static void gemm_t(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 64 || g.mode == 2 || g.ln_w) {
+    // rows per workgroup: up to 16·sk_mf; larger M is split over grid.y (more workgroups, less A
+    // traffic per CU) — WCB_SK_MF = 1, 2 or 4
+    static const int sk_mf = [] { const char* v = getenv("WCB_SK_MF"); return v ? atoi(v) : 1; }();
+    const int mf = g.M <= 16 || sk_mf <= 1 ? 1 : (g.M <= 32 || sk_mf == 2) ? 2 : 4;
     bool ok;
     if (g.sel_val) {   // LM head: 64 columns per workgroup (A re-read 4x less), fused argmax partial
-      if (g.M <= 16) ok = launch_skinny_mf<T, 1, 4>(g, s);
-      else if (g.M <= 32) ok = launch_skinny_mf<T, 2, 4>(g, s);
+      if (mf == 1) ok = launch_skinny_mf<T, 1, 4>(g, s);
+      else if (mf == 2) ok = launch_skinny_mf<T, 2, 4>(g, s);
       else ok = launch_skinny_mf<T, 4, 4>(g, s);
-    } else if (g.M <= 16) ok = launch_skinny_mf<T, 1, 1>(g, s);
-    else if (g.M <= 32) ok = launch_skinny_mf<T, 2, 1>(g, s);
+    } else if (mf == 1) ok = launch_skinny_mf<T, 1, 1>(g, s);
+    else if (mf == 2) ok = launch_skinny_mf<T, 2, 1>(g, s);
     else ok = launch_skinny_mf<T, 4, 1>(g, s);
     if (!ok) fprintf(stderr, "wcb: no skinny GEMM instance for K=%d\n", g.K);
     return;
