@@ -144,6 +144,19 @@ int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void*
 int wcb_op_cross_attention_enc(int dtype, const void* q, const void* enc, const void* wkt, const void* wv,
                                const float* bv, void* o, int B, int H, int S, int nsplit, void* stream);
 
+/* Bias-weighted cross entropy — replaces the loss block of
+ * WhisperForConditionalGenerationWeightCE.forward (models/whisper_medical.py:113-156): weight
+ * bias_weight on every label token covered by a contiguous match of one of its utterance's spans
+ * (:118-133), −log_softmax(logits)[label]·w over labels ≠ −100, summed / (valid count + 1e-8)
+ * (:136-151). spans == NULL: nn.CrossEntropyLoss(ignore_index=−100) mean (:152-155).
+ * logits f32 [B·T][ld] (device), labels [B][T], spans [B][N][Lmax] with span_len [B][N] (0 = empty
+ * span, skipped — :122-127); per_token [B·T] (device, caller-owned) receives −logp·w·valid;
+ * loss (device f32 scalar) and count (device, nullable) the mean and the valid-label count.
+ * Labels must be −100 or in [0, V). Async on `stream`; deterministic (fixed-order reduction). */
+int wcb_op_weighted_ce(const float* logits, long ld, int B, int T, int V, const int32_t* labels,
+                       const int32_t* spans, const int32_t* span_len, int N, int Lmax, float bias_weight,
+                       float* per_token, float* loss, int32_t* count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -8,6 +8,7 @@ Contents (each function cites the reference / [tf] file:line it restates):
   * `whisper_np`  — numpy float32 restatement of log-mel, encoder, KV-cached decoder, greedy
                     generate (HF semantics), bias-list Aho-Corasick boost, beam search.
   * `bias_ref`    — pure-Python Aho-Corasick automaton defining the boost operator (A8).
+  * `wce_ref`     — numpy restatement of the bias-weighted cross entropy (`whisper_medical.py:113-156`).
   * `metric_ref`  — pure-Python WER / bias-WER restatement of `utils/compute_metric.py`.
 
 Pinning: `whisper_np` is checked against golden vectors produced by importing the reference model

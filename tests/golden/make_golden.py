@@ -161,7 +161,51 @@ def metric_fixture():
     print("metric fixtures written")
 
 
+def wce_fixture(seed=0, T=10):
+    """Weighted-CE loss of the reference forward (`models/whisper_medical.py:113-156`) on the micro
+    model: labels with planted bias spans (list form with an empty span, the collator's padded
+    tensor form, the zeros[B,1,1] "no spans" form) and bias_spans=None (plain CE). Stores the
+    labels, spans and the reference's loss for each form (bias_weight = 10)."""
+    dims = get_dims("micro")
+    sd = make_weights(dims, seed=seed, recipe="diverse")
+    from transformers import WhisperFeatureExtractor
+    fe = WhisperFeatureExtractor(feature_size=dims.n_mel)
+    B = 2
+    pcm = synth_batch(B)
+    mel = np.stack([fe(c, sampling_rate=16000).input_features[0] for c in pcm]).astype(np.float32)
+    rng = np.random.default_rng(seed + 99)
+    labels = rng.integers(0, dims.eos_token_id, size=(B, T)).astype(np.int64)
+    eos = dims.eos_token_id
+    # planted spans: row 0 holds [11, 22, 33] at 2 and [44] at 7; row 1 holds [55, 66] twice and
+    # the padded-form match [77, 88, eos] at the end (span followed by EOS, SURVEY.md §9.5)
+    labels[0, 2:5] = [11, 22, 33]; labels[0, 7] = 44; labels[0, 0] = -100
+    labels[1, 1:3] = [55, 66]; labels[1, 4:6] = [55, 66]; labels[1, 7:10] = [77, 88, eos]
+    labels[1, 3] = 0
+    spans_list = [[[11, 22, 33], [44], []], [[55, 66], [77, 88], [99, 98, 97]]]
+    Lmax = 3
+    padded = np.full((B, 3, Lmax), eos, dtype=np.int64)
+    for i, row in enumerate(spans_list):
+        for n, sp in enumerate(row):
+            padded[i, n, :len(sp)] = sp
+    m = ref_model(dims, sd)
+    x = torch.from_numpy(mel)
+    lab = torch.from_numpy(labels)
+    out = {"labels": labels, "spans_padded": padded, "bias_weight": np.float64(10.0)}
+    out["spans_list_len"] = np.array([[len(sp) for sp in row] for row in spans_list], dtype=np.int64)
+    with torch.no_grad():
+        out["loss_list"] = np.float64(m(input_features=x, labels=lab, bias_spans=spans_list).loss)
+        out["loss_padded"] = np.float64(m(input_features=x, labels=lab, bias_spans=torch.from_numpy(padded)).loss)
+        out["loss_zeros"] = np.float64(m(input_features=x, labels=lab,
+                                         bias_spans=torch.zeros(B, 1, 1, dtype=torch.long)).loss)
+        out["loss_none"] = np.float64(m(input_features=x, labels=lab).loss)
+    np.savez_compressed(os.path.join(HERE, "wce_micro_s0.npz"), **out)
+    print("wce", {k: float(v) for k, v in out.items() if k.startswith("loss")})
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["wce"]:
+        wce_fixture()
+        sys.exit(0)
     metric_fixture()
     torch.set_num_threads(8)
     mel_fixture()

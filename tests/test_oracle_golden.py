@@ -118,3 +118,36 @@ def test_use_cache_false_mode_equals_cached(model_case):
         pytest.skip("quadratic recompute only checked on the micro config")
     ids = om.generate(mel, max_length=12, use_cache=False)
     assert np.array_equal(ids, g["greedy_ids"][:, :12])
+
+
+def test_weighted_ce_matches_reference(golden_dir):
+    """The weighted-CE oracle on the oracle's teacher-forced logits reproduces the reference
+    forward's loss (models/whisper_medical.py:113-156) for every bias_spans form."""
+    from oracle import wce_ref
+    g = np.load(os.path.join(golden_dir, "wce_micro_s0.npz"))
+    dims = get_dims("micro")
+    om = W.OracleModel.from_dims(dims, make_weights(dims, seed=0, recipe="diverse"))
+    labels = g["labels"]
+    B, T = labels.shape
+    # shift_tokens_right ([tf] modeling_whisper.py:67-80), as the reference forward does
+    dec = np.full_like(labels, dims.pad_token_id)
+    dec[:, 1:] = labels[:, :-1]
+    dec[:, 0] = dims.decoder_start_token_id
+    dec[dec == -100] = dims.pad_token_id
+    logits, _ = om.forward_logits(W.log_mel(synth_batch(B), dims.n_mel), dec)
+    bw = float(g["bias_weight"])
+    pad = g["spans_padded"]
+    lens = g["spans_list_len"]
+    spans_list = [[list(pad[i, n, :lens[i, n]]) for n in range(pad.shape[1])] for i in range(B)]
+    cases = {
+        "loss_list": spans_list,
+        "loss_padded": wce_ref.spans_from_padded(pad),
+        "loss_zeros": [[[0]] for _ in range(B)],
+        "loss_none": None,
+    }
+    for key, spans in cases.items():
+        loss, _ = wce_ref.weighted_ce(logits, labels, spans, bw)
+        # logits agree with the reference to 5e-4 (test_teacher_forced_logits_match_reference)
+        assert abs(loss - float(g[key])) < 2e-6 * abs(float(g[key])) + 1e-5, key   # measured ≤ 5e-6
+    # the forms really differ (padding quirk, zeros matching label 0, weighting on/off)
+    assert len({round(float(g[k]), 3) for k in cases}) == 4

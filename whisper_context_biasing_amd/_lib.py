@@ -52,6 +52,8 @@ SIGNATURES = {
                               C.c_int, _P]),
     "wcb_op_gemm_ln": (C.c_int, [C.c_int, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P,
                                  C.c_int, _P]),
+    "wcb_op_weighted_ce": (C.c_int, [_P, C.c_long, C.c_int, C.c_int, C.c_int, _P, _P, _P, C.c_int, C.c_int,
+                                     C.c_float, _P, _P, _P, _P]),
     "wcb_op_layernorm": (C.c_int, [C.c_int, _P, _P, _P, _P, C.c_int, C.c_int, _P]),
     "wcb_op_attention_decode": (C.c_int, [C.c_int, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                           _P]),

@@ -154,6 +154,19 @@ void beam_init(const BeamArgs& a, hipStream_t s);
 void beam_select(const BeamArgs& a, hipStream_t s);   // per-row top-K + per-utterance step
 void beam_output(const BeamArgs& a, hipStream_t s);   // best finished sequence per utterance
 
+// Bias-weighted cross entropy (k_loss.hip; models/whisper_medical.py:113-156).
+struct WceArgs {
+  const float* logits = nullptr; long ld = 0;          // [B·T][ld] f32, V columns used
+  int B = 0, T = 0, V = 0;
+  const int* labels = nullptr;                         // [B][T], -100 = ignore
+  const int* spans = nullptr; const int* span_len = nullptr;   // [B][N][Lmax], [B][N] (0 = empty)
+  int N = 0, Lmax = 0, use_spans = 0;
+  float bias_weight = 1.f;
+  float* per_token = nullptr;                          // [B·T] −logp[label]·w·valid
+  float* loss = nullptr; int* count = nullptr;         // scalar loss, valid-label count (nullable)
+};
+void weighted_ce(const WceArgs& a, hipStream_t s);
+
 void fill_i32(int* p, int v, long n, hipStream_t s);
 // dst[0..n) = host values, passed by value in the kernel arguments (stream-ordered, no host buffer
 // lifetime or pageable-copy ordering to worry about)

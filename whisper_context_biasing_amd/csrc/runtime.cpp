@@ -1393,6 +1393,22 @@ int wcb_op_cross_attention_enc(int dtype, const void* q, const void* enc, const 
   });
 }
 
+int wcb_op_weighted_ce(const float* logits, long ld, int B, int T, int V, const int32_t* labels,
+                       const int32_t* spans, const int32_t* span_len, int N, int Lmax, float bias_weight,
+                       float* per_token, float* loss, int32_t* count, void* stream) {
+  return guarded(nullptr, [&] {
+    REQUIRE(logits && labels && per_token && loss && B > 0 && T > 0 && V > 0 && ld >= V, "bad argument");
+    REQUIRE(!spans || (span_len && N > 0 && Lmax > 0), "spans need span_len, N > 0 and Lmax > 0");
+    WceArgs a;
+    a.logits = logits; a.ld = ld; a.B = B; a.T = T; a.V = V; a.labels = labels;
+    a.spans = spans; a.span_len = span_len; a.N = spans ? N : 0; a.Lmax = spans ? Lmax : 0;
+    a.use_spans = spans ? 1 : 0; a.bias_weight = bias_weight;
+    a.per_token = per_token; a.loss = loss; a.count = count;
+    weighted_ce(a, (hipStream_t)stream);
+    HIPCHK(hipGetLastError());
+  });
+}
+
 int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk,
                      int flash, void* stream) {
   return guarded(nullptr, [&] {

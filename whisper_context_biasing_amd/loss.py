@@ -1,36 +1,74 @@
 """Bias-weighted cross entropy of the reference forward (`models/whisper_medical.py:113-156`).
 
-Training-loss path (not the inference hot path): computed with torch ops on
-the logits libwcb returns, so `WhisperCB.forward(labels=..., bias_spans=...)` reports the same
-`.loss` as the reference. Semantics kept exactly, including the quirk that padded spans are
-compared with their 50256 padding.
+SURVEY.md §8(f) rank 3. Runs on the device through `wcb_op_weighted_ce` (csrc/k_loss.hip): span
+coverage, one streaming log-sum-exp pass over each logits row, label gather, weighting and a
+fixed-order mean, fused — the [B·T, V] log_softmax the reference materialises is never written.
+This module only packs `bias_spans` into int32 device arrays. Semantics kept exactly, including
+the quirk that a padded span tensor is compared with its padding: the list form
+keeps each span's own length, the tensor form gives every span the padded length.
 """
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
+
+from . import _lib
 
 
-def weighted_ce(logits: torch.Tensor, labels: torch.Tensor, bias_spans, bias_weight: float) -> torch.Tensor:
+def _pack_spans(bias_spans, B: int):
+    """→ (spans int32 [B][N][Lmax], lengths int32 [B][N]) on the CPU, reference span semantics
+    (`models/whisper_medical.py:120-127`: an empty list / zero-element tensor is skipped)."""
+    if isinstance(bias_spans, torch.Tensor):
+        t = bias_spans.to(torch.int64)
+        if t.dim() != 3 or t.shape[0] != B:
+            raise ValueError(f"bias_spans tensor must be [B, N, L], got {tuple(t.shape)}")
+        N, L = t.shape[1], t.shape[2]
+        lens = torch.full((B, N), L, dtype=torch.int32)
+        return t.to(torch.int32).contiguous(), lens
+    if len(bias_spans) != B:
+        raise ValueError(f"bias_spans has {len(bias_spans)} utterances, labels have {B}")
+    rows = []
+    for spans in bias_spans:
+        rows.append([sp.reshape(-1).tolist() if isinstance(sp, torch.Tensor) else list(sp) for sp in spans])
+    N = max(1, max(len(r) for r in rows))
+    L = max([1] + [len(sp) for r in rows for sp in r])
+    packed = torch.zeros((B, N, L), dtype=torch.int32)
+    lens = torch.zeros((B, N), dtype=torch.int32)
+    for i, r in enumerate(rows):
+        for n, sp in enumerate(r):
+            if sp:
+                packed[i, n, :len(sp)] = torch.tensor(sp, dtype=torch.int32)
+                lens[i, n] = len(sp)
+    return packed, lens
+
+
+def weighted_ce(logits: torch.Tensor, labels: torch.Tensor, bias_spans, bias_weight: float,
+                return_per_token: bool = False):
+    """logits f32 [B, T, V] on the GPU, labels [B, T] (−100 = ignore). Returns the scalar loss
+    (device f32), and the per-token −logp·w·valid terms when `return_per_token`."""
+    if not logits.is_cuda:
+        raise _lib.WcbError("weighted_ce runs on the GPU only (no CPU fallback)")
     B, T, V = logits.shape
-    labels = labels.to(logits.device)
+    if logits.dtype != torch.float32 or logits.stride(2) != 1 or logits.stride(0) != T * logits.stride(1):
+        logits = logits.float().contiguous()
+    dev = logits.device
+    lab = labels.to(dev, torch.int32).contiguous()
+    if lab.shape != (B, T):
+        raise ValueError(f"labels {tuple(lab.shape)} do not match logits {tuple(logits.shape)}")
+    bad = (lab != -100) & ((lab < 0) | (lab >= V))
+    if bool(bad.any()):
+        raise IndexError("label id out of range [0, V)")
+    per = torch.empty(B * T, dtype=torch.float32, device=dev)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    lib = _lib.load()
+    stream = torch.cuda.current_stream(dev).cuda_stream
     if bias_spans is None:
-        return F.cross_entropy(logits.reshape(-1, V), labels.reshape(-1), ignore_index=-100)
-    weights = torch.ones_like(labels, dtype=torch.float32)
-    lab = labels.tolist()
-    for i in range(B):
-        for span in bias_spans[i]:
-            span = span.tolist() if isinstance(span, torch.Tensor) else list(span)
-            if not span:
-                continue
-            n = len(span)
-            for j in range(T - n + 1):
-                if lab[i][j:j + n] == span:
-                    weights[i, j:j + n] = bias_weight
-    logp = F.log_softmax(logits.float(), dim=-1).view(-1, V)
-    flat = labels.view(-1)
-    w = weights.view(-1)
-    valid = flat != -100
-    per_tok = -logp[torch.arange(logp.size(0), device=logp.device), flat.clamp(min=0)]
-    per_tok = per_tok * valid.float()
-    return (per_tok * w * valid.float()).sum() / (valid.sum() + 1e-8)
+        rc = lib.wcb_op_weighted_ce(logits.data_ptr(), logits.stride(1), B, T, V, lab.data_ptr(),
+                                    None, None, 0, 0, 1.0, per.data_ptr(), loss.data_ptr(), None, stream)
+    else:
+        sp, ln = _pack_spans(bias_spans, B)
+        sp, ln = sp.to(dev), ln.to(dev)
+        rc = lib.wcb_op_weighted_ce(logits.data_ptr(), logits.stride(1), B, T, V, lab.data_ptr(),
+                                    sp.data_ptr(), ln.data_ptr(), sp.shape[1], sp.shape[2], float(bias_weight),
+                                    per.data_ptr(), loss.data_ptr(), None, stream)
+    _lib.check(rc, None, "wcb_op_weighted_ce")
+    return (loss, per.view(B, T)) if return_per_token else loss
