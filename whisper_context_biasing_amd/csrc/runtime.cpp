@@ -1081,9 +1081,11 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     if (done <= 0) done = steps;
     if (h->prof_stamps) {   // fold this call's cross-attention stamps into the device accumulator
       const double launches_rows = (double)(P - 1 + steps) * h->d.n_layers * R * h->H() * h->S();
-      // algorithmic bytes: K and V (xmode 0) or the encoder output once for all heads (xmode 1)
-      h->xattn_bytes += h->xmode ? launches_rows / h->H() * h->d.d_model * esize(h->d.dtype)
-                                 : launches_rows * 64 * 2 * esize(h->d.dtype);
+      // algorithmic bytes: K and V (xmode 0) or the encoder output once for all heads (xmode 1), of
+      // every distinct clip once (the beams of a clip share its rows: counted per clip, not per row)
+      const double launches_clips = launches_rows / nb;
+      h->xattn_bytes += h->xmode ? launches_clips / h->H() * h->d.d_model * esize(h->d.dtype)
+                                 : launches_clips * 64 * 2 * esize(h->d.dtype);
       h->xattn_flops += h->xmode ? launches_rows * h->d.d_model * 4 : launches_rows * 64 * 4;
       stamp_reduce(h->stamps.as<unsigned long long>() + (size_t)buf * h->stamp_slots() * 2 * kStampSub, h->stamp_slots(),
                    h->stamp_acc.as<unsigned long long>(), D.hs);
