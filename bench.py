@@ -214,7 +214,8 @@ def main():
         avg_ms = p["ms"] / p["launches"]
         bpl = p["bytes"] / p["launches"]
         achieved = bpl / (avg_ms * 1e-3) / 1e9
-        xenc = args.dtype in ("bf16", "f16") and dims.d_model <= 1024 and os.environ.get("WCB_XMODE", "1") != "0"
+        xenc = args.dtype in ("bf16", "f16") and dims.d_model <= 1024 and os.environ.get("WCB_XMODE", "1") != "0" \
+            and (args.num_beams == 1 or os.environ.get("WCB_BEAM_XMODE", "0") == "1")
         kname = ("attn_xenc_kernel (decoder cross-attention in encoder space: one pass over the encoder "
                  "output per layer for all heads)") if xenc else \
             "attn_decode2p_kernel (decoder cross-attention over precomputed per-layer K/V)"

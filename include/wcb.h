@@ -157,6 +157,17 @@ int wcb_op_weighted_ce(const float* logits, long ld, int B, int T, int V, const 
                        const int32_t* spans, const int32_t* span_len, int N, int Lmax, float bias_weight,
                        float* per_token, float* loss, int32_t* count, void* stream);
 
+/* Host-side scoring (csrc/metric.cpp, no GPU): the arithmetic of utils/compute_metric.py on
+ * already-normalised text. wcb_wer_counts: per utterance i, errors[i] = word-level Levenshtein
+ * distance between refs[i] and hyps[i] (whitespace-separated words) and ref_words[i] = |words(refs[i])|
+ * — corpus WER = Σerrors / Σref_words, as evaluate's "wer" (jiwer) computes it at
+ * compute_metric.py:159. n_threads <= 0: all hardware threads. wcb_bias_counts: compute_bias_wer's
+ * per-utterance tallies (compute_metric.py:200-230): non-overlapping phrase counts in ref / pred. */
+int wcb_wer_counts(const char* const* refs, const char* const* hyps, int n, int64_t* errors, int64_t* ref_words,
+                   int n_threads);
+int wcb_bias_counts(const char* ref, const char* pred, const char* const* phrases, int n_phrases,
+                    int64_t* distance, int64_t* tokens);
+
 #ifdef __cplusplus
 }
 #endif

@@ -3,7 +3,8 @@
 * f32 mode: token-exact against the reference's own beam-5 goldens (HF generate, num_beams = 5).
 * boost / MinNewTokens / prompt prefix / more than 64 rows (row groups): identical to the oracle
   (oracle/beam_np.py) in f32 mode — parity vs the reference unpinned for the boost (no reference code).
-* bf16 (encoder-space cross-attention, rows_per_enc = beams): batch invariance (every utterance
+* bf16, both cross-attention formulations for beams (default: precomputed per-clip cross-K/V shared by
+  the beams, b_div; WCB_BEAM_XMODE=1: encoder space, rows_per_enc = beams): batch invariance (every utterance
   decoded alone gives the same beams as in the batch: the row maps and the shared encoder rows are
   exact) and identical to the oracle on the high-margin recipe.
 """
@@ -37,11 +38,30 @@ def case(size, seed, recipe, B):
     return _CASES[key]
 
 
-def model(size, seed, recipe, dtype):
-    key = (size, seed, recipe, dtype)
+class _env:
+    """Set environment variables the library reads when a handle is created."""
+    def __init__(self, **kv):
+        self.kv, self.old = kv, {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = os.environ.get(k)
+            os.environ[k] = v
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def model(size, seed, recipe, dtype, beam_xmode="0"):
+    key = (size, seed, recipe, dtype, beam_xmode)
     if key not in _MODELS:
         dims = get_dims(size)
-        _MODELS[key] = WhisperCB.from_state_dict(dims, make_weights(dims, seed=seed, recipe=recipe), dtype=dtype)
+        with _env(WCB_BEAM_XMODE=beam_xmode):
+            _MODELS[key] = WhisperCB.from_state_dict(dims, make_weights(dims, seed=seed, recipe=recipe), dtype=dtype)
     return _MODELS[key]
 
 
@@ -98,9 +118,10 @@ def test_beam_prompt_prefix_matches_oracle_f32():
     assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
 
 
-def test_beam_bf16_batch_invariant_and_high_margin():
+@pytest.mark.parametrize("beam_xmode", ["0", "1"])
+def test_beam_bf16_batch_invariant_and_high_margin(beam_xmode):
     dims, om, mel, enc = case("tiny.en", 1, "margin", 4)
-    m = model("tiny.en", 1, "margin", "bf16")
+    m = model("tiny.en", 1, "margin", "bf16", beam_xmode)
     x = torch.from_numpy(mel)
     ids = m.generate(x, max_length=24, num_beams=5).cpu().numpy()
     for b in range(x.shape[0]):
@@ -110,12 +131,13 @@ def test_beam_bf16_batch_invariant_and_high_margin():
     assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
 
 
-def _one_layer(size, seed, recipe, B, dtype):
+def _one_layer(size, seed, recipe, B, dtype, beam_xmode="0"):
     dims = get_dims(size, n_layers=1)
     sd = make_weights(dims, seed=seed, recipe=recipe)
     om = W.OracleModel.from_dims(dims, sd)
     mel = W.log_mel(synth_batch(B), dims.n_mel)
-    return dims, om, mel, WhisperCB.from_state_dict(dims, sd, dtype=dtype)
+    with _env(WCB_BEAM_XMODE=beam_xmode):
+        return dims, om, mel, WhisperCB.from_state_dict(dims, sd, dtype=dtype)
 
 
 def _batch_invariant(m, x, **kw):
@@ -140,11 +162,29 @@ def test_beam_c5_shape_f16_kv_mode():
     assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
 
 
-def test_beam_c3_shape_bf16_row_groups():
-    """C3 shape (medium layer: d = 1024, encoder-space cross-attention) with 13 clips x 5 beams = 65
-    decoder rows (two row groups): batch-invariant, and identical to the oracle on the high-margin recipe."""
-    dims, om, mel, m = _one_layer("medium", 1, "margin", 13, "bf16")
+@pytest.mark.parametrize("beam_xmode", ["0", "1"])
+def test_beam_c3_shape_bf16_row_groups(beam_xmode):
+    """C3 shape (medium layer: d = 1024; per-clip cross-K/V or encoder-space cross-attention) with 13
+    clips x 5 beams = 65 decoder rows (two row groups): batch-invariant, and identical to the oracle on
+    the high-margin recipe."""
+    dims, om, mel, m = _one_layer("medium", 1, "margin", 13, "bf16", beam_xmode)
     x = torch.from_numpy(mel)
     ids = _batch_invariant(m, x, max_length=8, num_beams=5)
     ref = generate_beam(om, mel=mel, num_beams=5, max_length=8)
     assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
+
+
+def test_greedy_and_beam_calls_interleave_on_one_handle():
+    """One bf16 handle alternates greedy (encoder-space cross-attention) and beam (per-clip cross-K/V)
+    calls: the decode workspaces regrow / graphs are re-captured, and every call returns what a fresh
+    sequence of the same call returns."""
+    dims, om, mel, enc = case("tiny.en", 1, "margin", 4)
+    m = model("tiny.en", 1, "margin", "bf16")
+    x = torch.from_numpy(mel)
+    g1 = m.generate(x, max_length=20).cpu().numpy()
+    b1 = m.generate(x, max_length=20, num_beams=5).cpu().numpy()
+    g2 = m.generate(x, max_length=20).cpu().numpy()
+    b2 = m.generate(x, max_length=20, num_beams=3).cpu().numpy()
+    b3 = m.generate(x, max_length=20, num_beams=5).cpu().numpy()
+    assert np.array_equal(g1, g2) and np.array_equal(b1, b3)
+    assert np.array_equal(b2, generate_beam(om, enc=enc, num_beams=3, max_length=20))

@@ -54,6 +54,10 @@ SIGNATURES = {
                                  C.c_int, _P]),
     "wcb_op_weighted_ce": (C.c_int, [_P, C.c_long, C.c_int, C.c_int, C.c_int, _P, _P, _P, C.c_int, C.c_int,
                                      C.c_float, _P, _P, _P, _P]),
+    "wcb_wer_counts": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_int,
+                                 C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_int]),
+    "wcb_bias_counts": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(C.c_char_p), C.c_int,
+                                  C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "wcb_op_layernorm": (C.c_int, [C.c_int, _P, _P, _P, _P, C.c_int, C.c_int, _P]),
     "wcb_op_attention_decode": (C.c_int, [C.c_int, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                           _P]),

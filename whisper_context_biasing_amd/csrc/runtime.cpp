@@ -162,6 +162,10 @@ struct wcb_handle {
   // no cross-K/V precompute; 16-bit dtypes, d <= 1024), 0 = precomputed per-layer K/V (f32 "exact"
   // mode, large-v3). Fixed at create (WCB_XMODE overrides where supported).
   int xmode = 1;
+  // beam search (num_beams > 1) reads precomputed per-clip cross-K/V (xmode 0) even when greedy uses
+  // the encoder-space kernel: its per-row work is smaller and the beams of a clip share the K/V
+  // (measured on C3, medium beam 5: 1805 vs 1414 audio-s/s). WCB_BEAM_XMODE=1 keeps encoder space.
+  int beam_xmode = 0;
   int xenc_split = 8;   // key ranges per row of the encoder-space kernel (rows x ranges workgroups)
   int xenc_variant = 1; // attn_xenc kernel variant (k_xenc.hip)
   int xqk = 0;          // 1: one GEMM LN(x) → q' with W_k,hᵀW_q,h precombined (WCB_XQK; measured slower: 14 MB per layer)
@@ -358,6 +362,8 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     if (const char* xv = getenv("WCB_XVARIANT")) h->xvariant = atoi(xv);
     h->xmode = xenc_supported(h->dt, desc->d_model) ? 1 : 0;
     if (const char* xm = getenv("WCB_XMODE")) h->xmode = (atoi(xm) != 0 && h->xmode) ? 1 : 0;
+    h->beam_xmode = 0;
+    if (const char* bx = getenv("WCB_BEAM_XMODE")) h->beam_xmode = (atoi(bx) != 0 && h->xmode) ? 1 : 0;
     if (const char* xs = getenv("WCB_XENC_SPLIT")) h->xenc_split = std::max(1, std::min(atoi(xs), kXencMaxSplit));
     if (const char* xv = getenv("WCB_XENC_VARIANT")) h->xenc_variant = atoi(xv);
     if (const char* xq = getenv("WCB_XQK")) h->xqk = atoi(xq);
@@ -561,13 +567,14 @@ int wcb_finalize_weights(wcb_handle* h) {
           lw.xqk_w = h->upload_t(wqk);
           lw.xqk_b = h->upload_f(bqk);
         }
-      } else {
+      }
+      if (h->xmode == 0 || h->beam_xmode == 0) {
         std::copy(wk.begin(), wk.end(), xkv_w.begin() + (size_t)(2 * i) * dd);
         std::copy(wv.begin(), wv.end(), xkv_w.begin() + (size_t)(2 * i + 1) * dd);
         std::copy(bv.begin(), bv.end(), xkv_b.begin() + (size_t)(2 * i + 1) * d);
       }
     }
-    if (h->xmode == 0) {
+    if (h->xmode == 0 || h->beam_xmode == 0) {
       h->xkv_w = h->upload_t(xkv_w);
       h->xkv_b = h->upload_f(xkv_b);
     }
@@ -702,10 +709,10 @@ void drop_graphs(wcb_handle* h) {
 }
 
 // decode workspace: B decoder rows (clips x beams) reading `clips` encoder outputs
-void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld) {
+void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode) {
   const size_t e = esize(h->d.dtype), d = h->d.d_model, L = h->d.n_layers, S = h->S();
   const DecCtx& D0 = h->dc[h->nctx - 1];   // every context is sized together
-  const size_t xbuf = h->xmode ? (size_t)clips * S * d * e : 2 * L * (size_t)clips * S * d * e;
+  const size_t xbuf = xmode ? (size_t)clips * S * d * e : 2 * L * (size_t)clips * S * d * e;
   const size_t need[] = {xbuf, 2 * L * (size_t)B * T * d * e, (size_t)B * d * 4,
                          (size_t)B * h->d.ffn * e, (size_t)B * h->d.vocab * 4, (size_t)(I_NEXT + 3 * B + 16) * 4,
                          (size_t)B * out_ld * 4};
@@ -757,6 +764,7 @@ struct StepCfg {
   const wcb_bias* bias; float lam; int min_new;
   const int* forced; int forced_ld;    // advance_forced source when !select
   int clips = 0, nb = 1;               // encoder outputs (0: B) and decoder rows per encoder output
+  int xmode = 1;                       // cross-attention formulation of this call (wcb_handle::xmode)
   const int* phys = nullptr;           // beam search: cache row of every key position [B][T]
   const BeamArgs* beam = nullptr;      // beam search selection (replaces the greedy select)
 };
@@ -798,7 +806,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     GemmArgs o = rowgemm(datt, d, w.o_w, nb, d, d, x, d);
     o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st; o.st_nb = nbk;
     gemm(h->dt, o, st_);
-    if (h->xmode == 1) {
+    if (c.xmode == 1) {
       // cross attention in encoder space: q'_h = W_k,hᵀ q_h (block-diagonal GEMM, K = 64), one pass
       // over the encoder output per layer for all heads, range combine + W_v,h + b_v
       char* dqp = (char*)D.dqp.p + (size_t)b0 * H * d * e;
@@ -990,7 +998,8 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
       REQUIRE(cfg->bias_boost == 0.f || h->d.vocab <= kBeamMaxVocab, "beam search boost: vocabulary too large");
     }
     ensure_enc_ws(h, B);
-    ensure_dec_ws(h, B, R, Tc, out_ld);
+    const int xm = nb > 1 ? h->beam_xmode : h->xmode;   // this call's cross-attention formulation
+    ensure_dec_ws(h, B, R, Tc, out_ld, xm);
     const int buf = h->gen_count++ % h->nctx;
     DecCtx& D = h->dc[buf];
     // beam state [R] / [R][max_new] / [R][Tc] / [R][K] / [B][2] in one buffer
@@ -1004,7 +1013,7 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     //      last read that buffer has finished. It overlaps the previous call's decode.
     sync_in(h, stream, h->he);
     HIPCHK(hipStreamWaitEvent(h->he, h->ev_dec[buf], 0));
-    if (h->xmode == 1) {
+    if (xm == 1) {
       encode_impl(h, mel, B, h->xkv2[buf].p);   // the decode reads the encoder output itself
     } else {
       encode_impl(h, mel, B, nullptr);
@@ -1044,6 +1053,7 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
                cfg->min_new_tokens, D.forced.as<int>(), 0};
     sc.clips = B;
     sc.nb = nb;
+    sc.xmode = xm;
     if (nb > 1) { sc.phys = bm.phys; sc.beam = &bm; }
     for (int p = 0; p + 1 < P; ++p) decode_step(h, sc);   // prompt prefill, teacher-forced
     sc.lm_head = true;
@@ -1084,9 +1094,9 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
       // algorithmic bytes: K and V (xmode 0) or the encoder output once for all heads (xmode 1), of
       // every distinct clip once (the beams of a clip share its rows: counted per clip, not per row)
       const double launches_clips = launches_rows / nb;
-      h->xattn_bytes += h->xmode ? launches_clips / h->H() * h->d.d_model * esize(h->d.dtype)
+      h->xattn_bytes += xm ? launches_clips / h->H() * h->d.d_model * esize(h->d.dtype)
                                  : launches_clips * 64 * 2 * esize(h->d.dtype);
-      h->xattn_flops += h->xmode ? launches_rows * h->d.d_model * 4 : launches_rows * 64 * 4;
+      h->xattn_flops += xm ? launches_rows * h->d.d_model * 4 : launches_rows * 64 * 4;
       stamp_reduce(h->stamps.as<unsigned long long>() + (size_t)buf * h->stamp_slots() * 2 * kStampSub, h->stamp_slots(),
                    h->stamp_acc.as<unsigned long long>(), D.hs);
     }
@@ -1124,7 +1134,7 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
     REQUIRE(B <= 64, "batch > 64 per handle");
     REQUIRE(T <= h->d.n_text_ctx, "decoder_input_ids longer than max_target_positions");
     ensure_enc_ws(h, B);
-    ensure_dec_ws(h, B, B, T, 1);
+    ensure_dec_ws(h, B, B, T, 1, h->xmode);
     const int buf = h->gen_count++ % h->nctx;
     DecCtx& D = h->dc[buf];
     if ((size_t)B * (T + 1) * 4 > D.forced.bytes) { quiesce(h); D.forced.ensure((size_t)B * (T + 1) * 4); }
@@ -1151,6 +1161,7 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
     for (int t = 0; t < T; ++t) {
       StepCfg sc{B, T, 1, buf, true, false, logits + (size_t)t * h->d.vocab, (long)T * h->d.vocab, nullptr, 0.f, 0,
                  D.forced.as<int>(), T + 1};
+      sc.xmode = h->xmode;
       decode_step(h, sc);
     }
     HIPCHK(hipEventRecord(h->ev_dec[buf], D.hs));

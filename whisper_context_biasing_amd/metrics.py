@@ -13,11 +13,14 @@ Pinned by tests/test_metrics.py against the values the reference's formulas give
 """
 from __future__ import annotations
 
+import ctypes as C
 import re
 import unicodedata
 from typing import Iterable, List, Sequence, Tuple
 
 import regex
+
+from . import _lib
 
 ADDITIONAL_DIACRITICS = {
     "œ": "oe", "Œ": "OE", "ø": "o", "Ø": "O", "æ": "ae", "Æ": "AE", "ß": "ss", "ẞ": "SS",
@@ -59,27 +62,31 @@ class BasicTextNormalizer:
         return re.sub(r"\s+", " ", s)
 
 
-def edit_distance(ref: Sequence[str], hyp: Sequence[str]) -> int:
-    """Levenshtein distance over words (substitution = deletion = insertion = 1)."""
-    if not ref:
-        return len(hyp)
-    prev = list(range(len(hyp) + 1))
-    for i, r in enumerate(ref, 1):
-        cur = [i] + [0] * len(hyp)
-        for j, h in enumerate(hyp, 1):
-            cur[j] = min(prev[j] + 1, cur[j - 1] + 1, prev[j - 1] + (r != h))
-        prev = cur
-    return prev[-1]
+def _cstrs(strs: Sequence[str]):
+    arr = (C.c_char_p * max(1, len(strs)))()
+    for i, t in enumerate(strs):
+        arr[i] = t.encode("utf-8")
+    return arr
+
+
+def wer_counts(predictions: Sequence[str], references: Sequence[str], n_threads: int = 0):
+    """Per utterance (word edit distance, reference words) from the C++ scorer
+    (`wcb_wer_counts`, csrc/metric.cpp), utterances in parallel on host threads."""
+    preds, refs = list(predictions), list(references)
+    if len(preds) != len(refs):
+        raise ValueError(f"predictions ({len(preds)}) and references ({len(refs)}) differ in length")
+    n = len(refs)
+    err = (C.c_int64 * max(1, n))()
+    words = (C.c_int64 * max(1, n))()
+    lib = _lib.load()
+    _lib.check(lib.wcb_wer_counts(_cstrs(refs), _cstrs(preds), n, err, words, n_threads), None, "wcb_wer_counts")
+    return list(err[:n]), list(words[:n])
 
 
 def wer(predictions: Iterable[str], references: Iterable[str]) -> float:
     """Corpus WER in percent (jiwer: whitespace words, Σ errors / Σ reference words)."""
-    errors = words = 0
-    for p, r in zip(predictions, references):
-        rw, pw = r.split(), p.split()
-        errors += edit_distance(rw, pw)
-        words += len(rw)
-    return 100.0 * errors / max(words, 1)
+    errors, words = wer_counts(list(predictions), list(references))
+    return 100.0 * sum(errors) / max(sum(words), 1)
 
 
 def parse_refs_preds(text: str) -> Tuple[List[str], List[str]]:
@@ -112,18 +119,11 @@ def bias_wer(refs: Sequence[str], preds: Sequence[str], bias_words: Sequence[Seq
             continue
         r = " ".join(norm(ref).split())
         p = " ".join(norm(pred).split())
-        sd = st = 0
-        for bw in (norm(w) for w in words):
-            toks = bw.split()
-            if not toks:
-                continue
-            rc = r.count(bw)
-            if rc == 0:
-                continue
-            st += len(toks) * rc
-            pc = p.count(bw)
-            if pc != rc:
-                sd += abs(rc - pc) * len(toks)
+        phrases = [norm(w) for w in words]
+        sd, st = C.c_int64(), C.c_int64()
+        _lib.check(_lib.load().wcb_bias_counts(r.encode("utf-8"), p.encode("utf-8"), _cstrs(phrases),
+                                               len(phrases), C.byref(sd), C.byref(st)), None, "wcb_bias_counts")
+        sd, st = sd.value, st.value
         if st > 0:
             total_d += sd
             total_t += st
