@@ -239,6 +239,38 @@ def main():
                   "launches_per_step": v["launches"] / (args.steps if k == "dec_xattn" else prof_steps)}
               for k, v in prof.items()}
 
+    # biased-WER half of the metric, as a plumbing check (random weights: no transcript to score
+    # against): the boosted decode of the last batch against a λ = 0 decode of the same clips, scored
+    # by the C++ host scorer with token ids as words (WER, and compute_bias_wer's tallies over the
+    # bias phrases), untimed
+    bias_plumb = None
+    if rank == 0 and args.boost > 0:
+        from whisper_context_biasing_amd.metrics import wer_counts
+        import ctypes as C
+        from whisper_context_biasing_amd import _lib
+        from whisper_context_biasing_amd.metrics import _cstrs
+        mel = model.log_mel(pcm)
+        kw = dict(max_length=args.new_tokens, min_new_tokens=args.new_tokens, use_graph=use_graph,
+                  num_beams=args.num_beams)
+        boosted = model.generate(mel, bias_list=phrases, bias_boost=args.boost, **kw).cpu().tolist()
+        plain = model.generate(mel, **kw).cpu().tolist()
+        model.synchronize()
+        as_text = lambda rows: [" ".join(map(str, r)) for r in rows]
+        err, words = wer_counts(as_text(boosted), as_text(plain))
+        ptxt = [" ".join(map(str, p)) for p in phrases]
+        bd = bt = 0
+        for r, h in zip(as_text(plain), as_text(boosted)):
+            d_, t_ = C.c_int64(), C.c_int64()
+            _lib.check(_lib.load().wcb_bias_counts((" " + r + " ").encode(), (" " + h + " ").encode(),
+                                                   _cstrs([" " + t + " " for t in ptxt]), len(ptxt),
+                                                   C.byref(d_), C.byref(t_)), None, "wcb_bias_counts")
+            bd += d_.value
+            bt += t_.value
+        bias_plumb = {"wer_boosted_vs_unboosted": round(100.0 * sum(err) / max(sum(words), 1), 3),
+                      "bias_wer_boosted_vs_unboosted": round(100.0 * bd / bt, 3) if bt else 0.0,
+                      "bias_phrase_tokens_in_unboosted": bt,
+                      "note": "plumbing only (random weights): token ids as words, λ=0 decode as reference"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("timing the CPU oracle baseline ...")
@@ -262,6 +294,7 @@ def main():
             "roofline_other": others if roofs else None,
             "phases": phases,
             "cpu_baseline": cpu,
+            "biased_wer": bias_plumb,
         }
         if cpu:
             out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
