@@ -259,7 +259,7 @@ def main():
         err, words = wer_counts(as_text(boosted), as_text(plain))
         ptxt = [" ".join(map(str, p)) for p in phrases]
         bd = bt = 0
-        for r, h in zip(as_text(plain), as_text(boosted)):
+        for r, h in zip(as_text(boosted), as_text(plain)):   # phrases the boost placed, lost without it
             d_, t_ = C.c_int64(), C.c_int64()
             _lib.check(_lib.load().wcb_bias_counts((" " + r + " ").encode(), (" " + h + " ").encode(),
                                                    _cstrs([" " + t + " " for t in ptxt]), len(ptxt),
@@ -267,9 +267,10 @@ def main():
             bd += d_.value
             bt += t_.value
         bias_plumb = {"wer_boosted_vs_unboosted": round(100.0 * sum(err) / max(sum(words), 1), 3),
-                      "bias_wer_boosted_vs_unboosted": round(100.0 * bd / bt, 3) if bt else 0.0,
-                      "bias_phrase_tokens_in_unboosted": bt,
-                      "note": "plumbing only (random weights): token ids as words, λ=0 decode as reference"}
+                      "bias_wer_unboosted_vs_boosted": round(100.0 * bd / bt, 3) if bt else 0.0,
+                      "bias_phrase_tokens_in_boosted": bt,
+                      "note": "plumbing only (random weights): token ids as words; WER of the boosted decode "
+                              "against the λ=0 decode, bias-WER of the λ=0 decode against the boosted one"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
