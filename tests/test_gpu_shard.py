@@ -1,0 +1,64 @@
+"""GPU, world_size 2: utterance sharding end to end on the device. Two processes
+(gloo group; both ranks drive cuda:0 here — the one-GPU box) get the weights by one broadcast of the
+packed bf16 blob, decode their shard of the batch through libwcb with the bias boost, and gather the
+ids; the concatenation in rank order equals the single-process decode of the whole batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+N_CLIPS, TOKENS, MODEL = 6, 16, "tiny.en"
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _decode(model, lo, hi, dims):
+    from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list
+    pcm = torch.from_numpy(synth_batch(hi - lo, start=lo)).cuda()
+    mel = model.log_mel(pcm)
+    phrases = synth_bias_list(200, eot=dims.eos_token_id)
+    ids = model.generate(mel, max_length=TOKENS, min_new_tokens=TOKENS, bias_list=phrases, bias_boost=2.0)
+    return ids.cpu()
+
+
+def _worker(rank, world, port, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from whisper_context_biasing_amd.config import get_dims
+    from whisper_context_biasing_amd.model import WhisperCB
+    from whisper_context_biasing_amd.shard import broadcast_weights, gather_shards, shard_bounds
+    torch.cuda.set_device(0)
+    dims = get_dims(MODEL)
+    sd = broadcast_weights(dims, torch.device("cpu"), seed=0)
+    model = WhisperCB.from_state_dict(dims, sd, dtype="bf16")
+    lo, hi = shard_bounds(N_CLIPS, rank, world)
+    ids = _decode(model, lo, hi, dims)
+    rows = torch.cat(gather_shards(ids, torch.device("cpu")))
+    if rank == 0:
+        np.save(os.path.join(outdir, "sharded.npy"), rows.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_shards_equal_single_process(tmp_path):
+    from whisper_context_biasing_amd.config import get_dims
+    from whisper_context_biasing_amd.model import WhisperCB
+    from whisper_context_biasing_amd.shard import broadcast_weights
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    sharded = np.load(tmp_path / "sharded.npy")
+    dims = get_dims(MODEL)
+    model = WhisperCB.from_state_dict(dims, broadcast_weights(dims, torch.device("cpu"), seed=0), dtype="bf16")
+    full = _decode(model, 0, N_CLIPS, dims).numpy()
+    assert sharded.shape == full.shape == (N_CLIPS, TOKENS)
+    np.testing.assert_array_equal(sharded, full)

@@ -709,8 +709,12 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
     const int mf = g.M <= 16 || sk_mf <= 1 ? 1 : (g.M <= 32 || sk_mf == 2) ? 2 : 4;
     bool ok;
     if (g.sel_val) {   // LM head: 64 columns per workgroup (A re-read 4x less), fused argmax partial
-      if (mf == 1) ok = launch_skinny_mf<T, 1, 4>(g, s);
-      else if (mf == 2) ok = launch_skinny_mf<T, 2, 4>(g, s);
+      // WCB_LM_MF: rows per workgroup for the LM head alone (its 79.7 MB weight stream is re-read by
+      // every row block, from another XCD's L2 or HBM). The argmax-partial epilogue needs BNC = 64.
+      static const int lm_mf = [] { const char* v = getenv("WCB_LM_MF"); return v ? atoi(v) : 0; }();
+      const int lmf = lm_mf <= 0 ? mf : (g.M <= 16 || lm_mf <= 1) ? 1 : (g.M <= 32 || lm_mf == 2) ? 2 : 4;
+      if (lmf == 1) ok = launch_skinny_mf<T, 1, 4>(g, s);
+      else if (lmf == 2) ok = launch_skinny_mf<T, 2, 4>(g, s);
       else ok = launch_skinny_mf<T, 4, 4>(g, s);
     } else if (mf == 1) ok = launch_skinny_mf<T, 1, 1>(g, s);
     else if (mf == 2) ok = launch_skinny_mf<T, 2, 1>(g, s);
