@@ -100,10 +100,13 @@ def test_beam_natural_eos_matches_oracle_f32():
     assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
 
 
-def test_beam_row_groups_match_oracle_f32():
-    """16 clips x 5 beams = 80 decoder rows: two row groups of the skinny decode GEMMs."""
+@pytest.mark.parametrize("group_rows", ["512", "64"])
+def test_beam_row_groups_match_oracle_f32(group_rows):
+    """16 clips x 5 beams = 80 decoder rows: one 80-row chain (default), or two row groups on
+    parallel streams (WCB_GROUP_ROWS=64)."""
     dims, om, mel, enc = case("micro", 0, "diverse", 16)
-    m = model("micro", 0, "diverse", "f32")
+    with _env(WCB_GROUP_ROWS=group_rows):
+        m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=0, recipe="diverse"), dtype="f32")
     ids = m.generate(torch.from_numpy(mel), max_length=16, num_beams=5).cpu().numpy()
     ref = generate_beam(om, enc=enc, num_beams=5, max_length=16)
     assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
@@ -162,12 +165,13 @@ def test_beam_c5_shape_f16_kv_mode():
     assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
 
 
-@pytest.mark.parametrize("beam_xmode", ["0", "1"])
-def test_beam_c3_shape_bf16_row_groups(beam_xmode):
+@pytest.mark.parametrize("beam_xmode,group_rows", [("0", "512"), ("1", "512"), ("0", "64"), ("1", "64")])
+def test_beam_c3_shape_bf16_row_groups(beam_xmode, group_rows):
     """C3 shape (medium layer: d = 1024; per-clip cross-K/V or encoder-space cross-attention) with 13
     clips x 5 beams = 65 decoder rows (two row groups): batch-invariant, and identical to the oracle on
     the high-margin recipe."""
-    dims, om, mel, m = _one_layer("medium", 1, "margin", 13, "bf16", beam_xmode)
+    with _env(WCB_GROUP_ROWS=group_rows):   # one 65-row chain, or two chains on parallel streams
+        dims, om, mel, m = _one_layer("medium", 1, "margin", 13, "bf16", beam_xmode)
     x = torch.from_numpy(mel)
     ids = _batch_invariant(m, x, max_length=8, num_beams=5)
     ref = generate_beam(om, mel=mel, num_beams=5, max_length=8)

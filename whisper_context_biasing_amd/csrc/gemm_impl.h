@@ -702,7 +702,7 @@ static bool launch_skinny_mf(const GemmArgs& g, hipStream_t s) {
 
 template <typename T>
 static void gemm_t(const GemmArgs& g, hipStream_t s) {
-  if (g.M <= 64 || g.mode == 2 || g.ln_w) {
+  if (g.M <= 64 || g.mode == 2 || g.ln_w || g.skinny) {
     // rows per workgroup: up to 16·sk_mf; larger M is split over grid.y (more workgroups, less A
     // traffic per CU) — WCB_SK_MF = 1, 2 or 4
     static const int sk_mf = [] { const char* v = getenv("WCB_SK_MF"); return v ? atoi(v) : 1; }();

@@ -37,6 +37,7 @@ struct GemmArgs {
   // grouped A (skinny path, block-diagonal weights): the A row of output column block n0 starts
   // (n0 / a_grp_n) · a_grp_off elements further (q'_h = W_k,hᵀ q_h: K = 64 columns of head h)
   int a_grp_n = 0; long a_grp_off = 0;
+  int skinny = 0;                  // decode projection: the skinny kernel whatever M (row blocks over grid.y)
   // f16 encoder layers: the layer output is clamped to ±(finfo(f16).max − 1000)
   // ([tf] modeling_whisper.py:409-411); 0 = off
   float clamp = 0.f;

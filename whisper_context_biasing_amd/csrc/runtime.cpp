@@ -166,6 +166,10 @@ struct wcb_handle {
   // the encoder-space kernel: its per-row work is smaller and the beams of a clip share the K/V
   // (measured on C3, medium beam 5: 1805 vs 1414 audio-s/s). WCB_BEAM_XMODE=1 keeps encoder space.
   int beam_xmode = 0;
+  // decoder rows per decode chain (WCB_GROUP_ROWS). One chain for every row count by default: the
+  // beam configurations decode faster as one chain of 80-320-row launches than as 64-row chains on
+  // parallel streams (measured: C3 1814 -> 2215, C5 864 -> 983 audio-s/s; profiles/r01c_sweep_grp_*)
+  int group_rows = 512;
   int xenc_split = 8;   // key ranges per row of the encoder-space kernel (rows x ranges workgroups)
   int xenc_variant = 1; // attn_xenc kernel variant (k_xenc.hip)
   int xqk = 0;          // 1: one GEMM LN(x) → q' with W_k,hᵀW_q,h precombined (WCB_XQK; measured slower: 14 MB per layer)
@@ -363,6 +367,7 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     h->xmode = xenc_supported(h->dt, desc->d_model) ? 1 : 0;
     if (const char* xm = getenv("WCB_XMODE")) h->xmode = (atoi(xm) != 0 && h->xmode) ? 1 : 0;
     h->beam_xmode = 0;
+    if (const char* gr = getenv("WCB_GROUP_ROWS")) h->group_rows = std::max(16, std::min(atoi(gr), 512));
     if (const char* bx = getenv("WCB_BEAM_XMODE")) h->beam_xmode = (atoi(bx) != 0 && h->xmode) ? 1 : 0;
     if (const char* xs = getenv("WCB_XENC_SPLIT")) h->xenc_split = std::max(1, std::min(atoi(xs), kXencMaxSplit));
     if (const char* xv = getenv("WCB_XENC_VARIANT")) h->xenc_variant = atoi(xv);
@@ -640,6 +645,13 @@ GemmArgs rowgemm(const void* A, long lda, const void* W, int M, int N, int K, vo
   return g;
 }
 
+// decode projections: always the skinny kernel (rows over grid.y), also for row groups > 64 rows
+GemmArgs drow(const void* A, long lda, const void* W, int M, int N, int K, void* out, long ldc) {
+  GemmArgs g = rowgemm(A, lda, W, M, N, K, out, ldc);
+  g.skinny = 1;
+  return g;
+}
+
 void run_gemm(wcb_handle* h, const char* cls, const GemmArgs& g) {
   h->timed(cls, 2.0 * g.M * g.N * g.K, 0.0, h->he, [&] { gemm(h->dt, g, h->he); });
 }
@@ -791,7 +803,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
   for (int l = 0; l < L; ++l) {
     const LayerW& w = h->dec[l];
     char* cache = (char*)D.kvself.p + (l * cache_l + (size_t)b0 * H * T * 64) * e;
-    GemmArgs q = rowgemm(x, d, w.qkv_w, nb, 3 * d, d, dq, d);   // LayerNorm fused (f32 A rows)
+    GemmArgs q = drow(x, d, w.qkv_w, nb, 3 * d, d, dq, d);   // LayerNorm fused (f32 A rows)
     q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nbk;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
     gemm(h->dt, q, st_);
@@ -803,7 +815,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     a.row0 = b0; a.phys = c.phys; a.phys_ld = T;
     a.o = datt; a.ldo = d; a.o_Sb = 1; a.B = nb; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1;
     attention_decode(h->dt, a, st_);
-    GemmArgs o = rowgemm(datt, d, w.o_w, nb, d, d, x, d);
+    GemmArgs o = drow(datt, d, w.o_w, nb, d, d, x, d);
     o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st; o.st_nb = nbk;
     gemm(h->dt, o, st_);
     if (c.xmode == 1) {
@@ -811,16 +823,16 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       // over the encoder output per layer for all heads, range combine + W_v,h + b_v
       char* dqp = (char*)D.dqp.p + (size_t)b0 * H * d * e;
       if (w.xqk_w) {   // q' = (W_k,hᵀ W_q,h) LN(x) + W_k,hᵀ b_q,h: one GEMM
-        GemmArgs xq = rowgemm(x, d, w.xqk_w, nb, H * d, d, dqp, (long)H * d);
+        GemmArgs xq = drow(x, d, w.xqk_w, nb, H * d, d, dqp, (long)H * d);
         xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk;
         xq.bias = w.xqk_b;
         gemm(h->dt, xq, st_);
       } else {
-        GemmArgs xq = rowgemm(x, d, w.xq_w, nb, d, d, dq, d);
+        GemmArgs xq = drow(x, d, w.xq_w, nb, d, d, dq, d);
         xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk;
         xq.bias = w.xq_b;
         gemm(h->dt, xq, st_);
-        GemmArgs kq = rowgemm(dq, d, w.xkt_w, nb, H * d, 64, dqp, (long)H * d);
+        GemmArgs kq = drow(dq, d, w.xkt_w, nb, H * d, 64, dqp, (long)H * d);
         kq.a_grp_n = d; kq.a_grp_off = 64;
         gemm(h->dt, kq, st_);
       }
@@ -839,12 +851,12 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       xenc_attention(h->dt, xa, st_);
       char* du = (char*)D.du.p + (size_t)b0 * H * d * e;
       xenc_merge(h->dt, xa, du, (long)H * d, st_);
-      GemmArgs vg = rowgemm(du, (long)H * d, w.xv_w, nb, d, d, datt, d);   // o_h = W_v,h u_h + b_v,h
+      GemmArgs vg = drow(du, (long)H * d, w.xv_w, nb, d, d, datt, d);   // o_h = W_v,h u_h + b_v,h
       vg.a_grp_n = 64; vg.a_grp_off = d; vg.bias = w.xv_b;
       gemm(h->dt, vg, st_);
     } else {
       // cross attention over the precomputed encoder K/V
-      GemmArgs xq = rowgemm(x, d, w.xq_w, nb, d, d, dq, d);
+      GemmArgs xq = drow(x, d, w.xq_w, nb, d, d, dq, d);
       xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk;
       xq.bias = w.xq_b;
       gemm(h->dt, xq, st_);
@@ -865,20 +877,20 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       }
       attention_decode(h->dt, xa, st_);
     }
-    GemmArgs xo = rowgemm(datt, d, w.xo_w, nb, d, d, x, d);
+    GemmArgs xo = drow(datt, d, w.xo_w, nb, d, d, x, d);
     xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st; xo.st_nb = nbk;
     gemm(h->dt, xo, st_);
     // MLP
-    GemmArgs f1 = rowgemm(x, d, w.fc1_w, nb, h->d.ffn, d, dffn, h->d.ffn);
+    GemmArgs f1 = drow(x, d, w.fc1_w, nb, h->d.ffn, d, dffn, h->d.ffn);
     f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nbk;
     f1.bias = w.fc1_b; f1.act = 1;
     gemm(h->dt, f1, st_);
-    GemmArgs f2 = rowgemm(dffn, h->d.ffn, w.fc2_w, nb, d, h->d.ffn, x, d);
+    GemmArgs f2 = drow(dffn, h->d.ffn, w.fc2_w, nb, d, h->d.ffn, x, d);
     f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st; f2.st_nb = nbk;
     gemm(h->dt, f2, st_);
   }
   if (c.lm_head) {
-    GemmArgs lm = rowgemm(x, d, h->tok_emb, nb, h->d.vocab, d, c.logits_out + (size_t)b0 * c.logits_ld, c.logits_ld);
+    GemmArgs lm = drow(x, d, h->tok_emb, nb, h->d.vocab, d, c.logits_out + (size_t)b0 * c.logits_ld, c.logits_ld);
     lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b; lm.st_in = st; lm.st_nb = nbk;
     lm.out_f32 = 1;
     if (c.select && !c.beam) {   // argmax partials with the root boost + EOS mask fused into the LM head
@@ -902,7 +914,9 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
   int* pos = ints + I_POS;
   int* next_ids = ints + I_NEXT;
   embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, D.dx.as<float>(), D.dstats.as<float>(), B, d, D.hs);
-  const int ngrp = (B + 63) / 64;   // the skinny decode GEMMs take <= 64 rows
+  // rows per chain: the skinny projections split rows over grid.y, so a chain can take any number
+  // of rows (WCB_GROUP_ROWS; more chains overlap latency, fewer re-read the weights less often)
+  const int ngrp = (B + h->group_rows - 1) / h->group_rows;
   const int ns = std::max(ngrp, std::max(1, std::min(h->n_sub, B)));
   if (ns == 1 || !D.sub[0]) {        // one stream: row groups back to back
     for (int i = 0; i < ns; ++i) {
