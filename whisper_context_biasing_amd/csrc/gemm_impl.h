@@ -704,9 +704,13 @@ template <typename T>
 static void gemm_t(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 64 || g.mode == 2 || g.ln_w || g.skinny) {
     // rows per workgroup: up to 16·sk_mf; larger M is split over grid.y (more workgroups, less A
-    // traffic per CU) — WCB_SK_MF = 1, 2 or 4
-    static const int sk_mf = [] { const char* v = getenv("WCB_SK_MF"); return v ? atoi(v) : 1; }();
-    const int mf = g.M <= 16 || sk_mf <= 1 ? 1 : (g.M <= 32 || sk_mf == 2) ? 2 : 4;
+    // traffic per CU) — WCB_SK_MF = 1, 2 or 4 overrides the automatic choice
+    // Default (auto): 16 rows per workgroup up to 32 rows (C2 greedy: measured best), 32 up to 160
+    // (C5 80 beam rows: 983 -> 1075 audio-s/s), 64 beyond (C3 320 beam rows: 2217 -> 2437): with many
+    // rows the A re-read per column block, not the weight stream, dominates
+    static const int sk_mf = [] { const char* v = getenv("WCB_SK_MF"); return v ? atoi(v) : 0; }();
+    const int mf = sk_mf <= 0 ? (g.M <= 32 ? 1 : g.M <= 160 ? 2 : 4)
+                              : (g.M <= 16 || sk_mf <= 1 ? 1 : (g.M <= 32 || sk_mf == 2) ? 2 : 4);
     bool ok;
     if (g.sel_val) {   // LM head: 64 columns per workgroup (A re-read 4x less), fused argmax partial
       // WCB_LM_MF: rows per workgroup for the LM head alone (its 79.7 MB weight stream is re-read by
