@@ -232,8 +232,10 @@ __global__ __launch_bounds__(512) void attn_xenc_kernel(XencArgs a) {
 // scores; writes the slice into its private LDS tile (128-byte-row panels, common.h swizzle) for the
 // transposed Eᵀ reads; the 4 partial score tiles are summed through LDS (double-buffered, one barrier
 // per chunk) in a fixed order.
-template <int D> struct XregCfg {
-  static constexpr int NW = D >= 128 ? 4 : D / 32;        // waves = column slices
+// WNW: waves per workgroup for D >= 256 (4 default; 8 = variant 3: half the columns per wave, one
+// workgroup per CU by LDS)
+template <int D, int WNW = 4> struct XregCfg {
+  static constexpr int NW = D >= 256 ? WNW : D >= 128 ? 4 : D / 32;   // waves = column slices
   static constexpr int CW = D / NW;                       // columns per wave
   static constexpr int KSW = CW / 32;                     // k-steps per wave
   static constexpr int CTW = CW / 16;                     // 16-column Uᵀ tiles per wave
@@ -245,10 +247,10 @@ template <int D> struct XregCfg {
 };
 
 // NR = chunks in flight per wave (register ring depth): 2 (two workgroups per CU) or 3 (one).
-template <typename T, int D, int NR>
-__global__ __launch_bounds__(XregCfg<D>::NW * 64, NR == 2 ? 2 : 1) void attn_xenc_reg_kernel(XencArgs a) {
+template <typename T, int D, int NR, int WNW = 4>
+__global__ __launch_bounds__((XregCfg<D, WNW>::NW * 64), ((NR == 2 && WNW == 4) ? 2 : 1)) void attn_xenc_reg_kernel(XencArgs a) {
   using Frag = typename DT<T>::frag;
-  using C = XregCfg<D>;
+  using C = XregCfg<D, WNW>;
   constexpr int CK = kXencCK, NW = C::NW, CW = C::CW, KSW = C::KSW, CTW = C::CTW, PANEL = C::PANEL;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -442,6 +444,19 @@ static void launch_xenc(const XencArgs& a, hipStream_t s) {
     (void)hipFuncSetAttribute((const void*)attn_xenc_reg_kernel<T, D, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               XregCfg<D>::LDS);
     attr_set = true;
+  }
+  if constexpr (D % (8 * 32) == 0 && D >= 512) {
+    static bool attr8 = false;
+    if (!attr8) {
+      (void)hipFuncSetAttribute((const void*)attn_xenc_reg_kernel<T, D, 2, 8>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, XregCfg<D, 8>::LDS);
+      attr8 = true;
+    }
+    if (a.variant == 3) {
+      constexpr int kThreads = XregCfg<D, 8>::NW * 64, kLds = XregCfg<D, 8>::LDS;
+      hipLaunchKernelGGL((attn_xenc_reg_kernel<T, D, 2, 8>), dim3(a.nsplit, a.rows), dim3(kThreads), kLds, s, a);
+      return;
+    }
   }
   if (a.variant == 0)
     hipLaunchKernelGGL((attn_xenc_kernel<T, D>), dim3(a.nsplit, a.rows), dim3(kXencNW * 64), XencCfg<D>::LDS, s, a);
