@@ -218,7 +218,8 @@ def main():
             and (args.num_beams == 1 or os.environ.get("WCB_BEAM_XMODE", "0") == "1")
         kname = ("attn_xenc_kernel (decoder cross-attention in encoder space: one pass over the encoder "
                  "output per layer for all heads)") if xenc else \
-            "attn_decode2p_kernel (decoder cross-attention over precomputed per-layer K/V)"
+            "attn_decode2p_kernel / attn_decode_kernel (decoder cross-attention over precomputed per-layer K/V; " \
+            "single-pass kernel when a launch has <= 2048 (row, head) workgroups)"
         roofs["dec_xattn"] = {"bound": "hbm", "kernel": kname,
                               "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                               "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,

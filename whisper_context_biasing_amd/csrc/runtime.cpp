@@ -157,7 +157,10 @@ struct wcb_handle {
   // Cross-attention: one workgroup per (row, head) over all 1500 keys. Measured (tools/xattn_bench.py,
   // head-major K/V cycling 12 layers): split-KV hand-offs cost more than they hide at 16-32 rows.
   int xsplit = 1;
-  int xvariant = 0;  // cross-attention kernel variant (k_attn.hip launch_decode)
+  // cross-attention kernel variant over precomputed K/V (k_attn.hip launch_decode); -1 = auto: the
+  // single-pass kernel (1) when a launch has few (row, head) workgroups, else the two-pass kernel (0)
+  // (measured: C5 80 rows x 20 heads 1076 -> 1110 audio-s/s with 1; C3 320 x 16 2435 -> 2048 with 1)
+  int xvariant = -1;
   // Cross-attention formulation: 1 = encoder space (k_xenc.hip: the step streams the encoder output,
   // no cross-K/V precompute; 16-bit dtypes, d <= 1024), 0 = precomputed per-layer K/V (f32 "exact"
   // mode, large-v3). Fixed at create (WCB_XMODE overrides where supported).
@@ -869,7 +872,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       xa.o = datt; xa.ldo = d; xa.o_Sb = 1; xa.B = nb; xa.H = H; xa.nkeys = S;
       xa.nsplit = h->xsplit; xa.part = D.xpart.as<float>() + (size_t)b0 * H * kXSplit * 66;
       xa.ticket = D.xticket.as<int>() + (size_t)b0 * H;
-      xa.variant = h->xvariant;
+      xa.variant = h->xvariant >= 0 ? h->xvariant : (nb * H <= 2048 ? 1 : 0);
       if (h->prof_stamps) {
         xa.stamp.base = h->stamps.as<unsigned long long>() + (size_t)c.buf * h->stamp_slots() * 2 * kStampSub;
         xa.stamp.pos = pos;
