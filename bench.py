@@ -14,7 +14,8 @@ barriers; time = max over ranks.
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus `roofline` (dominant kernel:
 the encoder MFMA GEMMs, timed with HIP events on the library's stream inside the timed region)
-and `cpu_baseline` (the numpy oracle timed on this host, rank 0 / N=1 only).
+and `cpu_baseline` (the fp32 PyTorch-CPU restatement, both reference decode modes, timed on this
+host, rank 0 / N=1 only).
 """
 from __future__ import annotations
 
@@ -40,29 +41,53 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(size: str, n_tokens: int, n_phr: int, boost: float, seed: int = 0):
-    """numpy oracle (test infrastructure) on a bounded sample: 1 clip, log-mel + encoder + KV-cached
-    greedy decode of n_tokens with the same bias list and boost. Returns audio-s/s."""
-    from oracle import whisper_np as W
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(size: str, n_tokens: int, n_phr: int, boost: float, seed: int = 0, clips: int = 1):
+    """the fp32 PyTorch-CPU restatement of the reference path (oracle/whisper_torch.py,
+    test infrastructure) on the host cores, on a bounded sample of the same workload (log-mel + encoder
+    + n_tokens greedy tokens with the same bias list and boost), in the reference's two decode modes:
+    (i) use_cache=False exactly as scripts/evaluation.py:178 configures generate(), (ii) KV-cached.
+    `value` is the faster mode (ii). One untimed warm-up clip, then `clips` timed clips per mode."""
+    import torch
+    from oracle import whisper_torch as WT
     from whisper_context_biasing_amd.config import get_dims
     from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list
     from whisper_context_biasing_amd.weights import make_weights
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
-    except Exception:  # pragma: no cover
-        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     dims = get_dims(size)
-    om = W.OracleModel.from_dims(dims, make_weights(dims, seed=seed))
-    pcm = synth_batch(1)
+    m = WT.TorchWhisper(dims, make_weights(dims, seed=seed))
+    pcm = torch.from_numpy(synth_batch(clips))
     phrases = synth_bias_list(n_phr, eot=dims.eos_token_id)
-    t0 = time.perf_counter()
-    mel = W.log_mel(pcm, dims.n_mel)
-    om.generate(mel, max_length=n_tokens, min_new_tokens=n_tokens, bias=phrases, bias_boost=boost)
-    dt = time.perf_counter() - t0
-    return {"value": round(30.0 / dt, 3), "unit": "audio-seconds/sec", "cores": int(threads), "kind": "port",
-            "sample": f"1 clip x 30 s, {size} fp32 numpy oracle (oracle/whisper_np.py): log-mel + encoder + "
-                      f"{n_tokens} KV-cached greedy tokens with {n_phr}-phrase boost; {dt:.2f} s wall"}
+    kw = dict(max_length=n_tokens, min_new_tokens=n_tokens, bias=phrases, bias_boost=boost)
+
+    def run(use_cache, n):
+        t0 = time.perf_counter()
+        mel = WT.log_mel(pcm[:n], dims.n_mel)
+        m.generate(mel, use_cache=use_cache, **kw)
+        return time.perf_counter() - t0
+
+    with torch.no_grad():
+        run(True, 1)                                  # warm-up (thread pool, allocator)
+        t_cached = run(True, clips)
+        t_nocache = run(False, clips)
+    return {"value": round(clips * 30.0 / t_cached, 3), "unit": "audio-seconds/sec",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "host_cpu_count": os.cpu_count(), "cpu_model": _cpu_model(),
+            "modes": {"kv_cached": round(clips * 30.0 / t_cached, 3),
+                      "use_cache_false_reference_config": round(clips * 30.0 / t_nocache, 3)},
+            "sample": f"{clips} clip(s) x 30 s, whisper-{size} fp32 PyTorch-CPU restatement of the reference path "
+                      f"(oracle/whisper_torch.py): log-mel + encoder + {n_tokens} greedy tokens with the "
+                      f"{n_phr}-phrase boost; kv-cached {t_cached:.2f} s, use_cache=False "
+                      f"(scripts/evaluation.py:178) {t_nocache:.2f} s wall; torch threads = the box's CPU share "
+                      f"(OMP_NUM_THREADS), host has {os.cpu_count()} logical CPUs"}
 
 
 def _pmc_traffic(kernel: str):

@@ -79,7 +79,11 @@ def mel_fixture():
     print("mel fixture written")
 
 
-def model_fixture(size, seed, recipe, B, n_tokens, tf_len, beams=True):
+def model_fixture(size, seed, recipe, B, n_tokens, tf_len, beams=True, eager=True, beam_len=24):
+    """Reference outputs for one (size, seed, recipe): encoder slices, teacher-forced logits
+    probes, greedy ids / margins (scripts/evaluation.py decode config) and HF beam-5 ids.
+    The larger sizes (medium, large-v3: the C3 / C5 models at full depth) skip the eager-attention
+    cross-check (eager=False) and may skip the teacher-forced forward (tf_len=0) to bound CPU time."""
     from transformers import GenerationConfig
     dims = get_dims(size)
     sd = make_weights(dims, seed=seed, recipe=recipe)
@@ -90,16 +94,19 @@ def model_fixture(size, seed, recipe, B, n_tokens, tf_len, beams=True):
     out = {"mel_sum": mel.sum(dtype=np.float64)}
     rng = np.random.default_rng(seed + 17)
     dec_ids = np.concatenate([np.full((B, 1), dims.decoder_start_token_id),
-                              rng.integers(0, dims.eos_token_id, size=(B, tf_len - 1))], axis=1)
-    out["tf_decoder_input_ids"] = dec_ids
+                              rng.integers(0, dims.eos_token_id, size=(B, max(tf_len, 1) - 1))], axis=1)
+    if tf_len:
+        out["tf_decoder_input_ids"] = dec_ids
     res = {}
-    for attn in ("sdpa", "eager"):
+    for attn in (("sdpa", "eager") if eager else ("sdpa",)):
         m = ref_model(dims, sd, attn)
         with torch.no_grad():
             x = torch.from_numpy(mel)
             enc = m.model.encoder(x).last_hidden_state.numpy()
-            fw = m(input_features=x, decoder_input_ids=torch.from_numpy(dec_ids), return_dict=True)
-            logits = fw.logits.float().numpy()
+            logits = None
+            if tf_len:
+                fw = m(input_features=x, decoder_input_ids=torch.from_numpy(dec_ids), return_dict=True)
+                logits = fw.logits.float().numpy()
             gc = GenerationConfig(max_length=n_tokens, pad_token_id=dims.pad_token_id,
                                   eos_token_id=dims.eos_token_id,
                                   decoder_start_token_id=dims.decoder_start_token_id, use_cache=False)
@@ -115,34 +122,75 @@ def model_fixture(size, seed, recipe, B, n_tokens, tf_len, beams=True):
             plain = m.generate(input_features=x, max_length=n_tokens).numpy()
             res[attn] = (enc, logits, ids, scores, plain)
             if attn == "sdpa" and beams:
-                gcb = GenerationConfig(max_length=min(n_tokens, 24), pad_token_id=dims.pad_token_id,
+                gcb = GenerationConfig(max_length=min(n_tokens, beam_len), pad_token_id=dims.pad_token_id,
                                        eos_token_id=dims.eos_token_id, num_beams=5,
                                        decoder_start_token_id=dims.decoder_start_token_id, use_cache=True)
                 out["beam5_ids"] = m.generate(input_features=x, generation_config=gcb).numpy()
     enc, logits, ids, scores, plain = res["sdpa"]
     out["enc_slices"] = np.concatenate([enc[:, s] for s in ENC_ROWS], axis=1)
     out["enc_stats"] = np.array([enc.sum(dtype=np.float64), np.abs(enc).sum(dtype=np.float64)])
-    out["tf_logits_probe"] = logits[:, :, VOCAB_PROBE]
-    out["tf_logits_top5_idx"] = np.argsort(-logits, axis=-1, kind="stable")[:, :, :5]
-    out["tf_logits_top5_val"] = np.take_along_axis(logits, out["tf_logits_top5_idx"], -1)
-    lse = np.log(np.exp(logits - logits.max(-1, keepdims=True)).sum(-1)) + logits.max(-1)
-    out["tf_logits_lse"] = lse
+    if logits is not None:
+        out["tf_logits_probe"] = logits[:, :, VOCAB_PROBE]
+        out["tf_logits_top5_idx"] = np.argsort(-logits, axis=-1, kind="stable")[:, :, :5]
+        out["tf_logits_top5_val"] = np.take_along_axis(logits, out["tf_logits_top5_idx"], -1)
+        lse = np.log(np.exp(logits - logits.max(-1, keepdims=True)).sum(-1)) + logits.max(-1)
+        out["tf_logits_lse"] = lse
     out["greedy_sequences"] = ids                    # return_dict_in_generate: includes SOT
     out["greedy_ids"] = plain                        # plain generate(): SOT stripped, pad-right
     srt = np.sort(scores, axis=-1)
     out["greedy_margin"] = srt[..., -1] - srt[..., -2]
     out["greedy_top1"] = scores.argmax(-1)
     out["greedy_step_max"] = srt[..., -1]
-    e_enc, e_logits, e_ids, _, _ = res["eager"]
-    out["eager_vs_sdpa_enc_maxdiff"] = np.abs(e_enc - enc).max()
-    out["eager_vs_sdpa_logits_maxdiff"] = np.abs(e_logits - logits).max()
-    out["eager_greedy_ids"] = e_ids
-    meta = dict(size=size, seed=seed, recipe=recipe, B=B, n_tokens=n_tokens)
+    if "eager" in res:
+        e_enc, e_logits, e_ids, _, _ = res["eager"]
+        out["eager_vs_sdpa_enc_maxdiff"] = np.abs(e_enc - enc).max()
+        if logits is not None:
+            out["eager_vs_sdpa_logits_maxdiff"] = np.abs(e_logits - logits).max()
+        out["eager_greedy_ids"] = e_ids
+    meta = dict(size=size, seed=seed, recipe=recipe, B=B, n_tokens=n_tokens, beam_len=min(n_tokens, beam_len))
     out["meta"] = np.array([str(meta)])
     name = f"model_{size}_{recipe}_s{seed}.npz"
     np.savez_compressed(os.path.join(HERE, name), **out)
     print(name, "greedy", plain.shape, "min margin", out["greedy_margin"].min(),
-          "eager/sdpa enc diff", out["eager_vs_sdpa_enc_maxdiff"])
+          "eager/sdpa enc diff", out.get("eager_vs_sdpa_enc_maxdiff"), flush=True)
+
+
+def prompt_fixture(size, seed, recipe, B, n_tokens, prompt, beam_len=12):
+    """Prompt-conditioned decoding: the reference's biasing prompt
+    `<|startofprev|>` + bias / description tokens (data_utils/data_loader.py:182-366) fed to the
+    reference's generate() as `prompt_ids` ([tf] generation_whisper.py:1909-1911: decoder input =
+    prompt + [decoder_start]; output strips both, :1141; max_length counts new tokens, :1932-1940).
+    Greedy and beam-5 ids."""
+    from transformers import GenerationConfig, WhisperFeatureExtractor
+    dims = get_dims(size)
+    sd = make_weights(dims, seed=seed, recipe=recipe)
+    fe = WhisperFeatureExtractor(feature_size=dims.n_mel)
+    mel = np.stack([fe(c, sampling_rate=16000).input_features[0] for c in synth_batch(B)]).astype(np.float32)
+    m = ref_model(dims, sd)
+    x = torch.from_numpy(mel)
+    pr = torch.tensor(prompt, dtype=torch.long)
+    out = {"prompt_ids": np.asarray(prompt, dtype=np.int64)}
+    with torch.no_grad():
+        m.generation_config = GenerationConfig(max_length=n_tokens, pad_token_id=dims.pad_token_id,
+                                               eos_token_id=dims.eos_token_id,
+                                               decoder_start_token_id=dims.decoder_start_token_id, use_cache=False)
+        m.config.use_cache = False
+        m.config.suppress_tokens = []
+        g = m.generate(input_features=x, max_length=n_tokens, prompt_ids=pr, return_dict_in_generate=True,
+                       output_scores=True)
+        scores = torch.stack(g.scores, 1).float().numpy()
+        srt = np.sort(scores, axis=-1)
+        out["greedy_sequences"] = g.sequences.numpy()
+        out["greedy_margin"] = srt[..., -1] - srt[..., -2]
+        out["greedy_ids"] = m.generate(input_features=x, max_length=n_tokens, prompt_ids=pr).numpy()
+        gcb = GenerationConfig(max_length=beam_len, pad_token_id=dims.pad_token_id, eos_token_id=dims.eos_token_id,
+                               num_beams=5, decoder_start_token_id=dims.decoder_start_token_id, use_cache=True)
+        out["beam5_ids"] = m.generate(input_features=x, generation_config=gcb, prompt_ids=pr).numpy()
+    out["meta"] = np.array([str(dict(size=size, seed=seed, recipe=recipe, B=B, n_tokens=n_tokens,
+                                     beam_len=beam_len))])
+    name = f"prompt_{size}_{recipe}_s{seed}.npz"
+    np.savez_compressed(os.path.join(HERE, name), **out)
+    print(name, "greedy", out["greedy_ids"].shape, "beam", out["beam5_ids"].shape, flush=True)
 
 
 def metric_fixture():
@@ -202,9 +250,27 @@ def wce_fixture(seed=0, T=10):
     print("wce", {k: float(v) for k, v in out.items() if k.startswith("loss")})
 
 
+def big_fixtures():
+    """Round 2: the benchmark model sizes at full depth (C2 small, C3 medium, C5 large-v3) and the
+    prompt-conditioned decode."""
+    model_fixture("small", 0, "diverse", B=2, n_tokens=64, tf_len=6, beam_len=24)
+    model_fixture("small", 1, "margin", B=2, n_tokens=64, tf_len=6, eager=False, beam_len=24)
+    model_fixture("medium", 1, "margin", B=1, n_tokens=16, tf_len=0, eager=False, beam_len=16)
+    model_fixture("medium", 0, "diverse", B=1, n_tokens=16, tf_len=0, eager=False, beams=False)
+    model_fixture("large-v3", 1, "margin", B=1, n_tokens=12, tf_len=0, eager=False, beam_len=12)
+    # <|startofprev|> (multilingual 50361 / .en 50360) + synthetic bias-word tokens
+    prompt_fixture("micro", 0, "diverse", B=2, n_tokens=16, prompt=[50361, 100, 200, 300, 4000, 17])
+    prompt_fixture("small", 1, "margin", B=2, n_tokens=16,
+                   prompt=[50361] + [int(v) for v in np.random.default_rng(5).integers(0, 50257, 40)])
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["wce"]:
         wce_fixture()
+        sys.exit(0)
+    if sys.argv[1:] == ["big"]:
+        torch.set_num_threads(8)
+        big_fixtures()
         sys.exit(0)
     metric_fixture()
     torch.set_num_threads(8)

@@ -16,6 +16,7 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <type_traits>
@@ -646,6 +647,314 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
   }
 }
 
+// Decode GEMM (gemm_dec_kernel): the decode-step projections at up to 32 rows per workgroup.
+// Built from the chain-latency floor measured on MI355X (tools/chain_bench.hip): an empty kernel in a
+// replayed chain costs 1.6 µs, one HBM round trip of 16 KB per workgroup +1.0 µs, 96 KB of the
+// previous kernel's output per workgroup +2.2 µs — so a projection must (a) spread its weights over
+// every CU (16 columns per tile), (b) issue every load of the launch in one burst before anything
+// consumes one (hipcc otherwise sinks loads next to their uses and pays a round trip per group),
+// (c) read as few activation bytes and issue as few load instructions per workgroup as possible.
+//  * workgroup = NW waves (64·NW threads); rows [mb, mb + 16·MF); the K range is split over the waves
+//    (KPW 32-deep k-steps each, K = 32·KPW·NW at compile time).
+//  * AM 0: A = T rows; 3: grouped A (block-diagonal weights, A re-read per tile); 1 / 2: the decoder's
+//    pre-block LayerNorm fused: A = LN(x) of the f32 residual rows g.A (1) or of their T-typed copy
+//    g.ln_a16 (2, half the bytes). The row statistics are computed here from the very values the
+//    workgroup loads (each wave sums its K slice of its lanes' rows, one LDS exchange), and the
+//    LayerNorm weight / bias are staged once per workgroup through LDS: no per-lane parameter loads.
+//  * the A fragments (MF×KPW per lane) are built once and stay in registers while the workgroup walks
+//    its column tiles (P: blockIdx.x, blockIdx.x + gridDim.x, ...): the LM head streams its 79.7 MB
+//    of weights through 256 column walkers without re-reading the activations per tile; the next
+//    tile's weight fragments are loaded (nontemporal: read once) while the current tile reduces.
+//  * one LDS exchange per tile (double-buffered: one barrier per tile), then every thread finishes
+//    one (row, column) output: bias, GELU, residual, f32 / T / x16 stores, KV-cache append (mode 2),
+//    per-16-column LN partial sums (st_out, the older skinny consumers) and the LM head's argmax
+//    partial (sel_val: per workgroup and row, the running best over the tiles it walks).
+template <typename T, int MF, int NW, int KPW, int AM, bool P>
+__global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
+  using Frag = typename DT<T>::frag;
+  constexpr int NT = NW * 64, K = NW * KPW * 32, R = MF * 16;
+  constexpr bool LN = AM == 1 || AM == 2;
+  constexpr int EP = (R * 16 + NT - 1) / NT;         // epilogue outputs per thread (per tile)
+  __shared__ __attribute__((aligned(16))) float red[2][NW][R][17];
+  __shared__ __attribute__((aligned(16))) float lnp[LN ? 2 * K : 4];        // LayerNorm weight, bias
+  __shared__ float2 rst[LN ? NW : 1][LN ? R : 1];                          // per-wave (Σx, Σx²)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int mb = blockIdx.y * R;
+  const int ntile = (g.N + 15) >> 4;
+  const int kb = wave * (KPW * 32) + 8 * (lane >> 4);
+  const int pos_v = g.mode == 2 ? *g.pos : 0;
+  const bool mask_eos = g.sel_val && *g.sel_step < g.sel_min_new;
+
+  auto load_w = [&](Frag (&w)[KPW], int ct) {
+    const long n = min(ct * 16 + (lane & 15), g.N - 1);
+    const T* W = reinterpret_cast<const T*>(g.W) + n * g.ldw + kb;
+#pragma unroll
+    for (int ks = 0; ks < KPW; ++ks) w[ks] = __builtin_nontemporal_load(reinterpret_cast<const Frag*>(W + ks * 32));
+  };
+  // ---------------- every load of the launch is issued here
+  Frag wc[KPW], wn[P ? KPW : 1];
+  int ct = blockIdx.x;
+  load_w(wc, ct);
+  Frag a[MF][KPW];
+  f32x4 xf[AM == 1 ? MF : 1][AM == 1 ? KPW : 1][2];
+  if constexpr (AM == 0 || AM == 2) {
+    const T* A0 = reinterpret_cast<const T*>(AM == 0 ? g.A : g.ln_a16);
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const int m = min(mb + i * 16 + (lane & 15), g.M - 1);
+      const T* ap = A0 + a_row(g, m) + kb;
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) a[i][ks] = load_frag<T>(ap + ks * 32);
+    }
+  }
+  if constexpr (AM == 1) {
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const int m = min(mb + i * 16 + (lane & 15), g.M - 1);
+      const float* xr = reinterpret_cast<const float*>(g.A) + a_row(g, m) + kb;
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) {
+        xf[i][ks][0] = *reinterpret_cast<const f32x4*>(xr + ks * 32);
+        xf[i][ks][1] = *reinterpret_cast<const f32x4*>(xr + ks * 32 + 4);
+      }
+    }
+  }
+  constexpr int LQ = LN ? (2 * K / 4 + NT - 1) / NT : 1;   // LayerNorm parameter chunks per thread
+  f32x4 lq[LQ];
+  if constexpr (LN) {
+#pragma unroll
+    for (int j = 0; j < LQ; ++j) {
+      const int c = (j * NT + tid) * 4;                      // [0, K): weight, [K, 2K): bias
+      lq[j] = c < 2 * K ? *reinterpret_cast<const f32x4*>((c < K ? g.ln_w : g.ln_b) + (c < K ? c : c - K))
+                        : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  float pf_bias[EP], pf_res[EP];   // epilogue operands of this thread's outputs (single-tile launches)
+#pragma unroll
+  for (int it = 0; it < EP; ++it) {
+    const int o = it * NT + tid;
+    const int row = mb + (o >> 4), nn = ct * 16 + (o & 15);
+    const bool ok = !P && o < R * 16 && row < g.M && nn < g.N;
+    pf_bias[it] = (ok && g.bias) ? g.bias[nn] : 0.f;
+    pf_res[it] = (ok && g.resid && !(g.mode == 2 && nn >= g.n_split)) ? g.resid[c_row(g, row) + nn] : 0.f;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // ---------------- LayerNorm of the A rows: statistics from the loaded values, parameters via LDS
+  if constexpr (LN) {
+    float xv[MF][KPW][8];
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float v;
+          if constexpr (AM == 1) v = xf[i][ks][e >> 2][e & 3];
+          else if constexpr (sizeof(T) == 4) v = a[i][ks][e];
+          else if constexpr (__is_same(T, bf16_t)) v = bf16_to_f((bf16_t)a[i][ks][e]);
+          else v = float(a[i][ks][e]);
+          xv[i][ks][e] = v;
+          s1 += v;
+          s2 = fmaf(v, v, s2);
+        }
+      }
+      s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
+      if (lane < 16) rst[wave][i * 16 + lane] = float2{s1, s2};
+    }
+#pragma unroll
+    for (int j = 0; j < LQ; ++j) {
+      const int c = (j * NT + tid) * 4;
+      if (c < 2 * K) *reinterpret_cast<f32x4*>(lnp + c) = lq[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) { const float2 t = rst[w][i * 16 + (lane & 15)]; s1 += t.x; s2 += t.y; }
+      const float mean = s1 / K;
+      const float rstd = rsqrtf(fmaxf(s2 / K - mean * mean, 0.f) + 1e-5f);
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) {
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(lnp + kb + ks * 32);
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(lnp + kb + ks * 32 + 4);
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(lnp + K + kb + ks * 32);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(lnp + K + kb + ks * 32 + 4);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gw = e < 4 ? w0[e] : w1[e - 4], gb = e < 4 ? b0[e] : b1[e - 4];
+          const float v = (xv[i][ks][e] - mean) * rstd * gw + gb;
+          if constexpr (sizeof(T) == 4) a[i][ks][e] = v;
+          else a[i][ks][e] = __builtin_bit_cast(typename std::remove_reference<decltype(a[0][0][0])>::type, DT<T>::fromf(v));
+        }
+      }
+    }
+  }
+
+  float sel_best[EP];
+  int sel_bi[EP];
+#pragma unroll
+  for (int it = 0; it < EP; ++it) { sel_best[it] = -INFINITY; sel_bi[it] = 0x7fffffff; }
+  int buf = 0;
+  for (; ct < ntile; ct += gridDim.x) {
+    const int n0 = ct * 16;
+    // P (persistent column walk): the next tile's weights are in flight behind this tile (clamped:
+    // an unconditional load keeps hipcc from draining the queue at the loop head)
+    if constexpr (P) load_w(wn, min(ct + (int)gridDim.x, ntile - 1));
+    if constexpr (AM == 3) {
+      const T* A = reinterpret_cast<const T*>(g.A) + (long)(n0 / g.a_grp_n) * g.a_grp_off;
+#pragma unroll
+      for (int i = 0; i < MF; ++i) {
+        const int m = min(mb + i * 16 + (lane & 15), g.M - 1);
+#pragma unroll
+        for (int ks = 0; ks < KPW; ++ks) a[i][ks] = load_frag<T>(A + a_row(g, m) + kb + ks * 32);
+      }
+    }
+    f32x4 acc[MF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) acc[i] = mma16(a[i][ks], wc[ks], acc[i]);
+    }
+    // partial tile of this wave → LDS: lane holds rows 4(lane>>4)+e of tile i, column lane&15
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[buf][wave][i * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[i][e];
+    __syncthreads();
+    // epilogue: output o = tid + NT·it → (row o/16, column o%16): a row's 16 columns are 16
+    // consecutive lanes, so the per-row reductions (LN partials, argmax partial) are shuffles
+#pragma unroll
+    for (int it = 0; it < EP; ++it) {
+      const int o = it * NT + tid;
+      const int lrow = o >> 4, col = o & 15, row = mb + lrow, nn = n0 + col;
+      const bool valid = o < R * 16 && row < g.M && nn < g.N;
+      float v = 0.f;
+      if (o < R * 16) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) v += red[buf][w][lrow][col];
+      }
+      if (valid) {
+        if (g.bias) v += P ? g.bias[nn] : pf_bias[it];
+        if (g.act == 1) v = gelu_t<T>(v);
+        if (g.mode == 2 && nn >= g.n_split) {   // k / v of the new token → self-attention KV cache
+          const int n2 = nn - g.n_split;
+          const int hh = n2 >> 6, dd = n2 & 63;
+          const int kv = hh / g.hs_H, h = hh % g.hs_H;
+          const long off = ((((long)kv * g.hs_B + row) * g.hs_H + h) * g.kv_T + pos_v) * 64 + dd;
+          reinterpret_cast<T*>(g.kv_out)[off] = DT<T>::fromf(v);
+        } else if (!g.sel_val || g.out) {
+          const long off = c_row(g, row) + nn;
+          if (g.resid) v += P ? g.resid[off] : pf_res[it];
+          if (g.out_f32) reinterpret_cast<float*>(g.out)[off] = v;
+          else reinterpret_cast<T*>(g.out)[off] = DT<T>::fromf(v);
+          if (g.out16) reinterpret_cast<T*>(g.out16)[off] = DT<T>::fromf(v);
+        }
+      }
+      if (g.st_out) {
+        float a1 = valid ? v : 0.f, a2 = valid ? v * v : 0.f;
+#pragma unroll
+        for (int x = 1; x < 16; x <<= 1) { a1 += __shfl_xor(a1, x, 64); a2 += __shfl_xor(a2, x, 64); }
+        if (valid && col == 0) {
+          float* p = g.st_out + ((long)row * g.st_nb + ct) * 2;
+          p[0] = a1;
+          p[1] = a2;
+        }
+      }
+      if (g.sel_val) {
+        float x = -INFINITY;
+        int xi = 0x7fffffff;
+        if (valid) {
+          x = v;
+          if (g.sel_lam != 0.f && ((g.sel_root_bits[nn >> 5] >> (nn & 31)) & 1u)) x += g.sel_lam;
+          if (mask_eos && nn == g.sel_eos) x = -INFINITY;
+          xi = nn;
+        }
+#pragma unroll
+        for (int x2 = 1; x2 < 16; x2 <<= 1) {
+          const float ov = __shfl_xor(x, x2, 64);
+          const int oi = __shfl_xor(xi, x2, 64);
+          if (ov > x || (ov == x && oi < xi)) { x = ov; xi = oi; }
+        }
+        // tiles are walked in increasing column order: a later tile wins only when strictly better
+        if (x > sel_best[it]) { sel_best[it] = x; sel_bi[it] = xi; }
+      }
+    }
+    buf ^= 1;
+    if constexpr (P) {
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) wc[ks] = wn[ks];
+    } else {
+      break;
+    }
+  }
+  if (g.sel_val) {   // one argmax partial per (row, workgroup): sel_val[row][blockIdx.x]
+#pragma unroll
+    for (int it = 0; it < EP; ++it) {
+      const int o = it * NT + tid, row = mb + (o >> 4);
+      if ((o & 15) == 0 && o < R * 16 && row < g.M) {
+        g.sel_val[(long)row * gridDim.x + blockIdx.x] = sel_best[it];
+        g.sel_idx[(long)row * gridDim.x + blockIdx.x] = sel_bi[it];
+      }
+    }
+  }
+}
+
+template <typename T, int MF, int NW, int KPW, int AM>
+static void launch_dec_k(const GemmArgs& g, hipStream_t s) {
+  const int ntile = (g.N + 15) / 16, gy = (g.M + MF * 16 - 1) / (MF * 16);
+  // one tile per workgroup up to ~4 workgroups per CU; beyond (the LM head) a persistent column walk
+  if (!g.sel_val && (AM == 3 || ntile * gy <= 1024)) {
+    hipLaunchKernelGGL((gemm_dec_kernel<T, MF, NW, KPW, AM, false>), dim3(ntile, gy), dim3(NW * 64), 0, s, g);
+  } else {   // the LM head: kDecWalkers column walkers per row block (= argmax partials per row)
+    const int gx = std::min(ntile, kDecWalkers);
+    hipLaunchKernelGGL((gemm_dec_kernel<T, MF, NW, KPW, AM == 3 ? 0 : AM, true>), dim3(gx, gy), dim3(NW * 64), 0, s, g);
+  }
+}
+
+template <typename T, int MF, int NW, int KPW>
+static bool launch_dec_am(const GemmArgs& g, hipStream_t s) {
+  constexpr int K = NW * KPW * 32;
+  if (g.ln_w) {   // the decoder LayerNorms: K = d_model <= 1280
+    if constexpr (K <= 1280) {
+      if (g.ln_a16) launch_dec_k<T, MF, NW, KPW, 2>(g, s);
+      else launch_dec_k<T, MF, NW, KPW, 1>(g, s);
+      return true;
+    }
+    return false;
+  }
+  if (g.a_grp_n) {   // block-diagonal cross-attention products: K = 64 or d_model
+    if constexpr (K <= 1280) {
+      launch_dec_k<T, MF, NW, KPW, 3>(g, s);
+      return true;
+    }
+    return false;
+  }
+  launch_dec_k<T, MF, NW, KPW, 0>(g, s);
+  return true;
+}
+
+// K → (waves, k-steps per wave); f32 ("exact" mode, 2x the fragment registers) takes half the k-steps
+// per wave on twice the waves where the workgroup allows it. Returns false for an unsupported K.
+template <typename T, int MF>
+static bool launch_dec_mf(const GemmArgs& g, hipStream_t s) {
+  constexpr bool F32 = sizeof(T) == 4;
+#define WCB_DEC(k, nw, kpw) if (g.K == k) return launch_dec_am<T, MF, nw, kpw>(g, s);
+  WCB_DEC(64, 2, 1) WCB_DEC(128, 4, 1) WCB_DEC(256, 4, 2)
+  if constexpr (F32) {
+    WCB_DEC(384, 4, 3) WCB_DEC(512, 8, 2) WCB_DEC(768, 8, 3) WCB_DEC(1024, 8, 4) WCB_DEC(1280, 8, 5)
+    WCB_DEC(1536, 16, 3) WCB_DEC(2048, 16, 4) WCB_DEC(3072, 16, 6) WCB_DEC(4096, 16, 8) WCB_DEC(5120, 16, 10)
+  } else {
+    WCB_DEC(384, 4, 3) WCB_DEC(512, 4, 4) WCB_DEC(768, 4, 6) WCB_DEC(1024, 4, 8) WCB_DEC(1280, 8, 5)
+    WCB_DEC(1536, 8, 6) WCB_DEC(2048, 8, 8) WCB_DEC(3072, 8, 12) WCB_DEC(4096, 16, 8) WCB_DEC(5120, 16, 10)
+  }
+#undef WCB_DEC
+  return false;
+}
+
 template <typename T, int BM, int BN, int WM, int WN, int EPI>
 static void launch_tile_e(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
@@ -700,8 +1009,23 @@ static bool launch_skinny_mf(const GemmArgs& g, hipStream_t s) {
   return false;
 }
 
+static inline bool dec_enabled() {
+  static const int on = [] { const char* v = getenv("WCB_DEC"); return v ? atoi(v) : 1; }();
+  return on != 0;
+}
+
 template <typename T>
 static void gemm_t(const GemmArgs& g, hipStream_t s) {
+  if ((g.M <= 64 || g.mode == 2 || g.ln_w || g.skinny) && g.mode != 1 && !g.addrow) {
+    // decode GEMM: WCB_DEC_MF=1 / 2 forces 16- / 32-row workgroups; WCB_DEC=0 keeps the older skinny kernel
+    static const int dec_mf = [] { const char* v = getenv("WCB_DEC_MF"); return v ? atoi(v) : 0; }();
+    if (dec_enabled()) {
+      // 16-row workgroups up to 64 rows (measured C2: 1.074 vs 1.147 ms/token with 32-row workgroups)
+      const bool mf1 = dec_mf == 1 || (dec_mf == 0 && g.M <= 64) || g.K >= 4096;
+      const bool ok = mf1 ? launch_dec_mf<T, 1>(g, s) : launch_dec_mf<T, 2>(g, s);
+      if (ok) return;
+    }
+  }
   if (g.M <= 64 || g.mode == 2 || g.ln_w || g.skinny) {
     // rows per workgroup: up to 16·sk_mf; larger M is split over grid.y (more workgroups, less A
     // traffic per CU) — WCB_SK_MF = 1, 2 or 4 overrides the automatic choice

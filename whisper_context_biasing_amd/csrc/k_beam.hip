@@ -146,7 +146,8 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
     for (int q = 1; q < 4; ++q)
       if (beam_better(wv[q], wi[q], bv, bi)) { bv = wv[q]; bi = wi[q]; bt = wt[q]; }
     if (tid == bt) ++head;
-    if (tid == 0) { a.cand_val[(long)r * a.K + k] = bv; a.cand_tok[(long)r * a.K + k] = bi; }
+    // an all-NaN row leaves bi = INT_MAX: keep the candidate index inside the vocabulary
+    if (tid == 0) { a.cand_val[(long)r * a.K + k] = bv; a.cand_tok[(long)r * a.K + k] = bi >= 0 && bi < a.V ? bi : a.eos; }
     __syncthreads();
   }
 }

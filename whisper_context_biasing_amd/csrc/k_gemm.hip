@@ -1,10 +1,23 @@
 // GEMM dispatch by element type; kernels and tiling live in gemm_impl.h.
+#include <algorithm>
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace wcb {
 void gemm_bf16(const GemmArgs& g, hipStream_t s);
 void gemm_f16(const GemmArgs& g, hipStream_t s);
 void gemm_f32(const GemmArgs& g, hipStream_t s);
+
+bool gemm_dec_supported(DType t, int K) {
+  static const int on = [] { const char* v = getenv("WCB_DEC"); return v ? atoi(v) : 1; }();
+  (void)t;
+  return on && (K == 64 || K == 128 || K == 256 || K == 384 || K == 512 || K == 768 || K == 1024 || K == 1280);
+}
+
+int lm_head_partials(DType t, int K, int vocab) {
+  return gemm_dec_supported(t, K) ? std::min((vocab + 15) / 16, kDecWalkers) : (vocab + 63) / 64;
+}
 
 void gemm(DType t, const GemmArgs& g, hipStream_t s) {
   switch (t) {

@@ -82,16 +82,18 @@ void layernorm(DType t, const float* x, const float* w, const float* b, void* y,
 template <typename T>
 __global__ __launch_bounds__(256) void embed_kernel(const T* __restrict__ emb, const T* __restrict__ pemb, const int* __restrict__ ids,
                                                     const int* __restrict__ pos, float* __restrict__ x, float* __restrict__ st,
-                                                    int M, int d) {
+                                                    int M, int d, T* __restrict__ x16, int V) {
   const int row = blockIdx.x;
   const int p = *pos;
-  const long id = ids[row];
+  const int raw = ids[row];
+  const long id = raw >= 0 && raw < V ? raw : 0;   // never index past the table (ids are produced on device)
   for (int c0 = 0; c0 < d; c0 += 256) {
     const int c = c0 + threadIdx.x;
     float v = 0.f;
     if (c < d) {
       v = DT<T>::tof(emb[id * d + c]) + DT<T>::tof(pemb[(long)p * d + c]);
       x[(long)row * d + c] = v;
+      if (x16) x16[(long)row * d + c] = DT<T>::fromf(v);
     }
     float s1 = v, s2 = v * v;
 #pragma unroll
@@ -104,14 +106,14 @@ __global__ __launch_bounds__(256) void embed_kernel(const T* __restrict__ emb, c
 }
 
 void embed(DType t, const void* emb, const void* pemb, const int* ids, const int* pos, float* x, float* st, int M,
-           int d, hipStream_t s) {
+           int d, hipStream_t s, void* x16, int V) {
   switch (t) {
     case kBF16: hipLaunchKernelGGL(embed_kernel<bf16_t>, dim3(M), dim3(256), 0, s, (const bf16_t*)emb,
-                                   (const bf16_t*)pemb, ids, pos, x, st, M, d); break;
+                                   (const bf16_t*)pemb, ids, pos, x, st, M, d, (bf16_t*)x16, V); break;
     case kF16: hipLaunchKernelGGL(embed_kernel<f16_t>, dim3(M), dim3(256), 0, s, (const f16_t*)emb,
-                                  (const f16_t*)pemb, ids, pos, x, st, M, d); break;
+                                  (const f16_t*)pemb, ids, pos, x, st, M, d, (f16_t*)x16, V); break;
     case kF32: hipLaunchKernelGGL(embed_kernel<float>, dim3(M), dim3(256), 0, s, (const float*)emb,
-                                  (const float*)pemb, ids, pos, x, st, M, d); break;
+                                  (const float*)pemb, ids, pos, x, st, M, d, (float*)x16, V); break;
   }
 }
 

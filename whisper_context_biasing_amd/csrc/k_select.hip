@@ -84,7 +84,9 @@ __global__ __launch_bounds__(64) void select_finalize_kernel(SelectArgs a) {
     if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
   }
   const bool fin = a.finished[m] != 0;
-  const int tok = fin ? a.pad : bi;
+  // a row with no comparable value (all NaN) keeps bi = INT_MAX: emit EOS rather than an index past
+  // the vocabulary (the next step's embedding lookup must stay in bounds)
+  const int tok = fin ? a.pad : (bi >= 0 && bi < a.V ? bi : a.eos);
   // AC transition: tok in trans(s) → its target, else the root child, else root
   int dst = -1;
   for (int t = t0 + lane; t < t1; t += 64)

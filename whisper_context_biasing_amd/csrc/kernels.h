@@ -38,6 +38,11 @@ struct GemmArgs {
   // (n0 / a_grp_n) · a_grp_off elements further (q'_h = W_k,hᵀ q_h: K = 64 columns of head h)
   int a_grp_n = 0; long a_grp_off = 0;
   int skinny = 0;                  // decode projection: the skinny kernel whatever M (row blocks over grid.y)
+  // decode GEMM (gemm_dec_kernel): a T-typed copy of the f32 rows the epilogue writes (the
+  // residual stream x → x16, read back as the LN-fused A operand of the next projection), and the
+  // LN-fused A read from such a copy instead of the f32 rows (lda elements per row)
+  void* out16 = nullptr;
+  const void* ln_a16 = nullptr;
   // f16 encoder layers: the layer output is clamped to ±(finfo(f16).max − 1000)
   // ([tf] modeling_whisper.py:409-411); 0 = off
   float clamp = 0.f;
@@ -51,7 +56,12 @@ void layernorm(DType t, const float* x, const float* w, const float* b, void* y,
 
 // x[r][:] = emb[ids[r]][:] + pos_emb[*pos + r_pos][:] (f32 out), r_pos = r % rows_per_seq.
 void embed(DType t, const void* emb, const void* pos_emb, const int* ids, const int* pos, float* x,
-           float* stats, int M, int d, hipStream_t s);
+           float* stats, int M, int d, hipStream_t s, void* x16 = nullptr, int V = 1 << 30);
+// LM-head argmax partials per row: gemm_dec_kernel walks the vocabulary with kDecWalkers workgroups
+// per row block and writes one partial per walker; the older skinny kernel one per 64 columns.
+constexpr int kDecWalkers = 256;
+bool gemm_dec_supported(DType t, int K);
+int lm_head_partials(DType t, int K, int vocab);
 
 // Attention over heads of 64. q row for (b, i): q + (b·q_Sb + i)·ldq + h·64.
 // key j of (b, h): k + b·k_sb + h·k_sh + j·k_sk (same strides for v).

@@ -130,10 +130,11 @@ struct DecCtx {
   hipStream_t sub[kMaxSub] = {};                // row-group chains (fork/join inside the step graph)
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSub] = {};
   int dec_B = 0, dec_T = 0;
-  DevBuf kvself, dx, dh, dq, dqp, du, datt, dffn, dstats, xpart, xml, xticket, logits, part_val, part_idx, ints, outbuf,
-      forced, beam;
+  DevBuf kvself, dx, dx16, dh, dq, dqp, du, datt, dffn, dstats, xpart, xml, xticket, logits, part_val, part_idx, ints,
+      outbuf, forced, beam;
   int nchunk = 64;
   hipGraphExec_t gexec = nullptr;               // captured decode step
+  hipGraphExec_t gexec_k = nullptr;             // steps_per_graph consecutive decode steps in one graph
   std::string gkey;
 };
 
@@ -176,6 +177,13 @@ struct wcb_handle {
   int xenc_split = 8;   // key ranges per row of the encoder-space kernel (rows x ranges workgroups)
   int xenc_variant = 1; // attn_xenc kernel variant (k_xenc.hip)
   int xqk = 0;          // 1: one GEMM LN(x) → q' with W_k,hᵀW_q,h precombined (WCB_XQK; measured slower: 14 MB per layer)
+  // decoder LayerNorm input: 1 = the T-typed copy of the residual stream (half the bytes per
+  // projection workgroup; statistics still from the f32 rows), 0 = the f32 rows (WCB_LN16)
+  int ln16 = 0;
+  int steps_per_graph = 8;   // decode steps captured per replayed graph (WCB_STEPS_PER_GRAPH)
+  // decode projections on gemm_dec_kernel (K supported): the LayerNorm consumers compute their row
+  // statistics from the rows they load, so the producers publish no per-16-column partial sums
+  bool dec_gemm = false;
   std::map<std::string, std::vector<float>> host_w;
   std::vector<DevBuf> owned;
   bool ready = false;
@@ -375,6 +383,10 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     if (const char* xs = getenv("WCB_XENC_SPLIT")) h->xenc_split = std::max(1, std::min(atoi(xs), kXencMaxSplit));
     if (const char* xv = getenv("WCB_XENC_VARIANT")) h->xenc_variant = atoi(xv);
     if (const char* xq = getenv("WCB_XQK")) h->xqk = atoi(xq);
+    if (const char* l16 = getenv("WCB_LN16")) h->ln16 = atoi(l16);
+    if (const char* sg = getenv("WCB_STEPS_PER_GRAPH")) h->steps_per_graph = std::max(1, std::min(atoi(sg), 64));
+    if (h->dt == kF32) h->ln16 = 0;   // f32 "exact" mode: the copy would be the f32 rows themselves
+    h->dec_gemm = gemm_dec_supported(h->dt, desc->d_model);
     // DFT table [416 cols][416 k]: col 2b = win·cos(2πbk/400), col 2b+1 = −win·sin(2πbk/400)
     std::vector<float> dft((size_t)kNCol * kNCol, 0.f);
     for (int c = 0; c < 402; ++c) {
@@ -429,7 +441,8 @@ void wcb_destroy(wcb_handle* h) {
   (void)hipDeviceSynchronize();
   for (DecCtx& D : h->dc) {
     if (D.gexec) (void)hipGraphExecDestroy(D.gexec);
-    for (DevBuf* b : {&D.kvself, &D.dx, &D.dh, &D.dq, &D.dqp, &D.du, &D.datt, &D.dffn, &D.dstats, &D.xpart, &D.xml, &D.xticket,
+    if (D.gexec_k) (void)hipGraphExecDestroy(D.gexec_k);
+    for (DevBuf* b : {&D.kvself, &D.dx, &D.dx16, &D.dh, &D.dq, &D.dqp, &D.du, &D.datt, &D.dffn, &D.dstats, &D.xpart, &D.xml, &D.xticket,
                       &D.logits, &D.part_val, &D.part_idx, &D.ints, &D.outbuf, &D.forced, &D.beam})
       b->release();
     if (D.ev_fork) (void)hipEventDestroy(D.ev_fork);
@@ -718,7 +731,8 @@ enum { I_STEP = 0, I_POS = 1, I_DONE = 2, I_TICKET = 3, I_UNFIN = 4, I_NEXT = 16
 void drop_graphs(wcb_handle* h) {
   for (DecCtx& D : h->dc) {
     if (D.gexec) (void)hipGraphExecDestroy(D.gexec);
-    D.gexec = nullptr;
+    if (D.gexec_k) (void)hipGraphExecDestroy(D.gexec_k);
+    D.gexec = D.gexec_k = nullptr;
     D.gkey.clear();
   }
 }
@@ -744,6 +758,7 @@ void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode
     D.dec_B = std::max(D.dec_B, B);
     D.dec_T = std::max(D.dec_T, T);
     D.dx.ensure((size_t)B * d * 4);
+    D.dx16.ensure((size_t)B * d * e);
     D.dh.ensure((size_t)B * d * e);
     D.dq.ensure((size_t)B * d * e);
     D.datt.ensure((size_t)B * d * e);
@@ -755,7 +770,7 @@ void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode
     D.du.ensure((size_t)B * h->H() * d * e);
     D.xticket.ensure((size_t)B * h->H() * 4);     // zeroed on allocation; combiners reset their slot
     D.logits.ensure((size_t)B * h->d.vocab * 4);
-    D.nchunk = (h->d.vocab + 63) / 64;      // one argmax partial per LM-head workgroup (64 columns)
+    D.nchunk = lm_head_partials(h->dt, (int)d, h->d.vocab);   // argmax partials per row of the LM head
     D.part_val.ensure((size_t)B * D.nchunk * 4);
     D.part_idx.ensure((size_t)B * D.nchunk * 4);
     D.ints.ensure(need[5]);
@@ -795,8 +810,11 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
   int* ints = D.ints.as<int>();
   int* pos = ints + I_POS;
   float* x = D.dx.as<float>() + (size_t)b0 * d;
+  char* x16 = (char*)D.dx16.p + (size_t)b0 * d * e;       // T copy of x: the LN-fused A operand
+  const void* lna = h->ln16 ? x16 : nullptr;
   const int nbk = d / 16;
   float* st = D.dstats.as<float>() + (size_t)b0 * nbk * 2;
+  float* st_pub = h->dec_gemm ? nullptr : st;   // LN partial sums only for the older skinny consumers
   char* dq = (char*)D.dq.p + (size_t)b0 * d * e;
   char* datt = (char*)D.datt.p + (size_t)b0 * d * e;
   char* dffn = (char*)D.dffn.p + (size_t)b0 * h->d.ffn * e;
@@ -807,7 +825,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     const LayerW& w = h->dec[l];
     char* cache = (char*)D.kvself.p + (l * cache_l + (size_t)b0 * H * T * 64) * e;
     GemmArgs q = drow(x, d, w.qkv_w, nb, 3 * d, d, dq, d);   // LayerNorm fused (f32 A rows)
-    q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nbk;
+    q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nbk; q.ln_a16 = lna;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
     gemm(h->dt, q, st_);
     AttnArgs a;
@@ -819,7 +837,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     a.o = datt; a.ldo = d; a.o_Sb = 1; a.B = nb; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1;
     attention_decode(h->dt, a, st_);
     GemmArgs o = drow(datt, d, w.o_w, nb, d, d, x, d);
-    o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st; o.st_nb = nbk;
+    o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st_pub; o.st_nb = nbk; o.out16 = x16;
     gemm(h->dt, o, st_);
     if (c.xmode == 1) {
       // cross attention in encoder space: q'_h = W_k,hᵀ q_h (block-diagonal GEMM, K = 64), one pass
@@ -827,12 +845,12 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       char* dqp = (char*)D.dqp.p + (size_t)b0 * H * d * e;
       if (w.xqk_w) {   // q' = (W_k,hᵀ W_q,h) LN(x) + W_k,hᵀ b_q,h: one GEMM
         GemmArgs xq = drow(x, d, w.xqk_w, nb, H * d, d, dqp, (long)H * d);
-        xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk;
+        xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
         xq.bias = w.xqk_b;
         gemm(h->dt, xq, st_);
       } else {
         GemmArgs xq = drow(x, d, w.xq_w, nb, d, d, dq, d);
-        xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk;
+        xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
         xq.bias = w.xq_b;
         gemm(h->dt, xq, st_);
         GemmArgs kq = drow(dq, d, w.xkt_w, nb, H * d, 64, dqp, (long)H * d);
@@ -860,7 +878,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     } else {
       // cross attention over the precomputed encoder K/V
       GemmArgs xq = drow(x, d, w.xq_w, nb, d, d, dq, d);
-      xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk;
+      xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
       xq.bias = w.xq_b;
       gemm(h->dt, xq, st_);
       AttnArgs xa;
@@ -881,20 +899,20 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       attention_decode(h->dt, xa, st_);
     }
     GemmArgs xo = drow(datt, d, w.xo_w, nb, d, d, x, d);
-    xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st; xo.st_nb = nbk;
+    xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st_pub; xo.st_nb = nbk; xo.out16 = x16;
     gemm(h->dt, xo, st_);
     // MLP
     GemmArgs f1 = drow(x, d, w.fc1_w, nb, h->d.ffn, d, dffn, h->d.ffn);
-    f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nbk;
+    f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nbk; f1.ln_a16 = lna;
     f1.bias = w.fc1_b; f1.act = 1;
     gemm(h->dt, f1, st_);
     GemmArgs f2 = drow(dffn, h->d.ffn, w.fc2_w, nb, d, h->d.ffn, x, d);
-    f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st; f2.st_nb = nbk;
+    f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st_pub; f2.st_nb = nbk; f2.out16 = x16;
     gemm(h->dt, f2, st_);
   }
   if (c.lm_head) {
     GemmArgs lm = drow(x, d, h->tok_emb, nb, h->d.vocab, d, c.logits_out + (size_t)b0 * c.logits_ld, c.logits_ld);
-    lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b; lm.st_in = st; lm.st_nb = nbk;
+    lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b; lm.st_in = st; lm.st_nb = nbk; lm.ln_a16 = lna;
     lm.out_f32 = 1;
     if (c.select && !c.beam) {   // argmax partials with the root boost + EOS mask fused into the LM head
       lm.sel_val = D.part_val.as<float>() + (size_t)b0 * D.nchunk;
@@ -916,7 +934,8 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
   int* ints = D.ints.as<int>();
   int* pos = ints + I_POS;
   int* next_ids = ints + I_NEXT;
-  embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, D.dx.as<float>(), D.dstats.as<float>(), B, d, D.hs);
+  embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, D.dx.as<float>(), h->dec_gemm ? nullptr : D.dstats.as<float>(), B, d,
+        D.hs, D.dx16.p, h->d.vocab);
   // rows per chain: the skinny projections split rows over grid.y, so a chain can take any number
   // of rows (WCB_GROUP_ROWS; more chains overlap latency, fewer re-read the weights less often)
   const int ngrp = (B + h->group_rows - 1) / h->group_rows;
@@ -1079,24 +1098,36 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     snprintf(key, sizeof key, "%d/%d/%d/%d/%p/%a/%d/%d/%d/%d", B, nb, Tc, out_ld, (const void*)bs, cfg->bias_boost,
              cfg->min_new_tokens, h->n_sub, (int)h->prof_stamps, P);
     const int max_new = cfg->max_new_tokens;
-    const int chunk = 8;
+    // The decode step replays as a hipGraph; steps_per_graph steps are captured into one graph so the
+    // per-replay gap is paid once per chunk (every position-dependent value is read on the device, so
+    // a multi-step graph is the single-step graph unrolled). Natural-EOS mode polls the device
+    // "all finished" flag once per chunk.
+    const int chunk = h->steps_per_graph;
     int done = 0, steps = 0;
     if (cfg->use_graph && (!D.gexec || D.gkey != key)) {
       if (D.gexec) { (void)hipGraphExecDestroy(D.gexec); D.gexec = nullptr; }
-      hipGraph_t graph;
-      HIPCHK(hipStreamBeginCapture(D.hs, hipStreamCaptureModeThreadLocal));
-      decode_step(h, sc);
-      HIPCHK(hipStreamEndCapture(D.hs, &graph));
-      HIPCHK(hipGraphInstantiate(&D.gexec, graph, nullptr, nullptr, 0));
-      HIPCHK(hipGraphDestroy(graph));
+      if (D.gexec_k) { (void)hipGraphExecDestroy(D.gexec_k); D.gexec_k = nullptr; }
+      for (int k : {1, chunk}) {
+        if (k == 1 ? false : chunk == 1) break;
+        hipGraph_t graph;
+        HIPCHK(hipStreamBeginCapture(D.hs, hipStreamCaptureModeThreadLocal));
+        for (int i = 0; i < k; ++i) decode_step(h, sc);
+        HIPCHK(hipStreamEndCapture(D.hs, &graph));
+        HIPCHK(hipGraphInstantiate(k == 1 ? &D.gexec : &D.gexec_k, graph, nullptr, nullptr, 0));
+        HIPCHK(hipGraphDestroy(graph));
+      }
       D.gkey = key;
     }
     h->timed("decode_loop", 0, 0, D.hs, [&] {
       while (steps < max_new) {
         const int n = std::min(chunk, max_new - steps);
-        for (int i = 0; i < n; ++i) {
-          if (cfg->use_graph) HIPCHK(hipGraphLaunch(D.gexec, D.hs));
-          else decode_step(h, sc);
+        if (cfg->use_graph && n == chunk && D.gexec_k) {
+          HIPCHK(hipGraphLaunch(D.gexec_k, D.hs));
+        } else {
+          for (int i = 0; i < n; ++i) {
+            if (cfg->use_graph) HIPCHK(hipGraphLaunch(D.gexec, D.hs));
+            else decode_step(h, sc);
+          }
         }
         steps += n;
         if (fixed_len) continue;
