@@ -28,7 +28,6 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")   # before torch/HIP initialise (see the package __init__)
 sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)

@@ -95,7 +95,10 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
                 void* enc_out, void* stream);
 
 /* bias list: n_phrases token sequences, phrase i = tokens[offsets[i] .. offsets[i+1]) (host
- * arrays). Built into an Aho-Corasick automaton on the device (boost semantics: k_select.hip). */
+ * arrays). Built into an Aho-Corasick automaton on the device (boost semantics: k_select.hip).
+ * Lifetime: an automaton belongs to the handle that created it; wcb_bias_destroy waits for that
+ * handle's queued work and drops the decode graphs that captured it (serialise it with the handle's
+ * other calls, like every call on a handle). It may outlive the handle (destroy it afterwards). */
 int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets, int n_phrases,
                     wcb_bias** out);
 void wcb_bias_destroy(wcb_bias* b);

@@ -84,7 +84,8 @@ def generate_beam(om, mel=None, num_beams: int = 5, max_length: int = 225, enc=N
     Lt = min(P + int(max_length), n_ctx)
     ac = AhoCorasick(bias or [])
     lam = F32(bias_boost)
-    xkv = om.cross_kv(np.repeat(enc, nb, axis=0))        # beams of one clip share its encoder state
+    # beams of one clip share its encoder state: cross-K/V once per clip, repeated per beam row
+    xkv = [(np.repeat(k, nb, axis=0), np.repeat(v, nb, axis=0)) for k, v in om.cross_kv(enc)]
 
     run_seq = np.full((B, nb, Lt), om.pad, dtype=np.int64)
     run_seq[:, :, :P] = np.asarray(pre, dtype=np.int64)

@@ -257,7 +257,7 @@ class OracleModel:
     def generate(self, mel=None, max_length: int = 225, enc=None, min_new_tokens: int = 0,
                  bias: Optional[Sequence[Sequence[int]]] = None, bias_boost: float = 0.0,
                  prefix: Optional[Sequence[int]] = None, return_logits: bool = False,
-                 use_cache: bool = True, trim: bool = True):
+                 use_cache: bool = True, trim: bool = True, return_margins: bool = False):
         """Greedy decode with the reference's eval semantics:
         init = [decoder_start] ([tf] generation_whisper.py:1489,1591-1606); ≤ max_length new
         tokens (max_length+1 total incl. SOT, [tf] generation_whisper.py:1932-1940); fp32
@@ -267,7 +267,9 @@ class OracleModel:
         and pads are dropped per row as Whisper does ([tf] generation_whisper.py:1063-1086).
         `min_new_tokens` masks EOS (benchmark mode); `bias`/`bias_boost` apply
         the A8 boost (oracle/bias_ref.py). `use_cache=False` recomputes the whole prefix every
-        step exactly like `scripts/evaluation.py:178`.
+        step exactly like `scripts/evaluation.py:178`. `return_margins` adds the per-step gap between
+        the best and the second-best selection score (after boost and mask) of every row [B, steps]
+        (inf for finished rows): the margin gate of the reduced-precision parity tests.
         """
         if enc is None:
             enc = self.encode(mel)
@@ -284,18 +286,20 @@ class OracleModel:
         finished = np.zeros(B, dtype=bool)
         out = []
         all_logits = []
+        margins = []
         n_new = 0
         while True:
             if return_logits:
                 all_logits.append(logits_last.copy())
             mask_eos = self.eos if n_new < min_new_tokens else -1
             toks = np.empty(B, dtype=np.int64)
+            mg = np.full(B, np.inf, dtype=np.float64)
             for b in range(B):
                 if finished[b]:
                     toks[b] = self.pad
                     continue
                 if lam == 0.0 and mask_eos < 0:
-                    toks[b] = int(np.argmax(logits_last[b]))
+                    row = logits_last[b]
                 else:
                     row = logits_last[b].copy()
                     if lam != 0.0:
@@ -303,8 +307,12 @@ class OracleModel:
                             row[v] = F32(row[v] + F32(lam))
                     if mask_eos >= 0:
                         row[mask_eos] = -np.inf
-                    toks[b] = int(np.argmax(row))
+                toks[b] = int(np.argmax(row))
+                if return_margins:
+                    top2 = np.partition(row, -2)[-2:]
+                    mg[b] = float(top2[1]) - float(top2[0])
                 states[b] = ac.delta(states[b], int(toks[b]))
+            margins.append(mg)
             finished |= toks == self.eos
             out.append(toks)
             n_new += 1
@@ -319,4 +327,6 @@ class OracleModel:
         ids = np.stack(out, axis=1)
         if trim:   # Whisper's post-processing of the generate() output (oracle/beam_np.py)
             ids = whisper_trim(ids, self.eos, self.pad)
+        if return_margins:
+            return ids, np.stack(margins, axis=1)
         return (ids, np.stack(all_logits, axis=1)) if return_logits else ids

@@ -1,0 +1,187 @@
+"""GPU: the benchmark configurations of BASELINE.json end to end through the C ABI, at full depth.
+
+* Reference goldens (tests/golden/make_golden.py big — the reference model class itself run on CPU):
+  whisper-small (C2 / C4 model), full-depth medium (C3), full-depth large-v3 (C5). f32 mode must be
+  token-exact for greedy and beam-5; the 16-bit modes are exact on the high-margin recipe and
+  margin-gated on the diverse recipe (steps whose reference top-1/top-2 gap is below tau may differ).
+* The configurations with the 1000 / 5000-phrase boost (no reference implementation: oracle-pinned):
+  C2 = small, 32 clips, bf16, lambda 2, 64 tokens — rows checked against the numpy oracle on the same
+  clips (margin-gated; f32 mode exact) and against the same clips decoded as a smaller batch;
+  C3 = medium, beam 5, bf16, 1000 phrases; C5 = large-v3, beam 5, fp16, 5000 phrases (reduced batch).
+"""
+import gc
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import whisper_np as W  # noqa: E402
+from oracle.beam_np import generate_beam  # noqa: E402
+from whisper_context_biasing_amd.config import get_dims  # noqa: E402
+from whisper_context_biasing_amd.model import WhisperCB  # noqa: E402
+from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list  # noqa: E402
+from whisper_context_biasing_amd.weights import make_weights  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TAU = 0.05   # margin gate (bf16 / fp16 logits vs the fp32 reference)
+
+_W, _M = {}, {}
+
+
+def weights(size, seed, recipe):
+    key = (size, seed, recipe)
+    if key not in _W:
+        if any(k[0] != size for k in _W):   # one model size resident at a time (large-v3: 6.2 GB f32)
+            _W.clear()
+            _M.clear()
+            gc.collect()
+        _W[key] = make_weights(get_dims(size), seed=seed, recipe=recipe)
+    return _W[key]
+
+
+def model(size, seed, recipe, dtype):
+    key = (size, seed, recipe, dtype)
+    if key not in _M:
+        sd = weights(size, seed, recipe)
+        _M[key] = WhisperCB.from_state_dict(get_dims(size), sd, dtype=dtype)
+    return _M[key]
+
+
+def golden(size, recipe, seed):
+    g = np.load(os.path.join(GOLD, f"model_{size}_{recipe}_s{seed}.npz"))
+    return g, eval(str(g["meta"][0]), {})
+
+
+def mel_of(dims, B, start=0):
+    return torch.from_numpy(W.log_mel(synth_batch(B, start=start), dims.n_mel))
+
+
+def gated_equal(ids, ref, margin, tau=TAU):
+    """Token-by-token equality up to (excluding) the first step of a row whose reference margin < tau."""
+    checked = 0
+    for b in range(ref.shape[0]):
+        for t in range(ref.shape[1]):
+            if margin[b, t] < tau:
+                break
+            assert t < ids.shape[1] and ids[b, t] == ref[b, t], (b, t, ids[b], ref[b])
+            checked += 1
+    return checked
+
+
+# ------------------------------------------------------------------ checks (tests below, grouped by size)
+def check_f32_greedy_and_beam(size, recipe, seed):
+    g, meta = golden(size, recipe, seed)
+    dims = get_dims(size)
+    m = model(size, seed, recipe, "f32")
+    x = mel_of(dims, meta["B"])
+    ids = m.generate(x, max_length=meta["n_tokens"]).cpu().numpy()
+    assert ids.shape == g["greedy_ids"].shape and np.array_equal(ids, g["greedy_ids"]), (ids, g["greedy_ids"])
+    if "beam5_ids" in g.files:
+        b = m.generate(x, max_length=meta["beam_len"], num_beams=5).cpu().numpy()
+        assert b.shape == g["beam5_ids"].shape and np.array_equal(b, g["beam5_ids"]), (b, g["beam5_ids"])
+
+
+def check_16bit_greedy(size, recipe, seed, dtype):
+    """The benchmark dtypes (C2 / C3 bf16, C5 fp16) against the fp32 reference: exact on the high-margin
+    recipe, margin-gated on the diverse recipe."""
+    g, meta = golden(size, recipe, seed)
+    dims = get_dims(size)
+    m = model(size, seed, recipe, dtype)
+    ids = m.generate(mel_of(dims, meta["B"]), max_length=meta["n_tokens"]).cpu().numpy()
+    if recipe == "margin":
+        assert np.array_equal(ids, g["greedy_ids"]), (ids, g["greedy_ids"])
+    else:
+        assert gated_equal(ids, g["greedy_ids"], g["greedy_margin"]) >= 1
+
+
+def check_16bit_beam5(size, dtype):
+    g, meta = golden(size, "margin", 1)
+    dims = get_dims(size)
+    m = model(size, 1, "margin", dtype)
+    b = m.generate(mel_of(dims, meta["B"]), max_length=meta["beam_len"], num_beams=5).cpu().numpy()
+    assert b.shape == g["beam5_ids"].shape and np.array_equal(b, g["beam5_ids"]), (b, g["beam5_ids"])
+
+
+def check_beam5_boost(size, dtype, n_phr, B):
+    dims = get_dims(size)
+    m = model(size, 1, "margin", dtype)
+    phrases = synth_bias_list(n_phr, eot=dims.eos_token_id)
+    x = mel_of(dims, B)
+    ids = m.generate(x, max_length=8, num_beams=5, bias_list=phrases, bias_boost=2.0).cpu().numpy()
+    om = W.OracleModel.from_dims(dims, weights(size, 1, "margin"))
+    ref = generate_beam(om, mel=x.numpy(), num_beams=5, max_length=8, bias=phrases, bias_boost=2.0)
+    assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
+
+
+# ------------------------------------------------------------------ whisper-small (C2 / C4)
+@pytest.mark.parametrize("recipe,seed", [("diverse", 0), ("margin", 1)])
+def test_small_f32_greedy_and_beam5_match_reference(recipe, seed):
+    check_f32_greedy_and_beam("small", recipe, seed)
+
+
+@pytest.mark.parametrize("recipe,seed", [("margin", 1), ("diverse", 0)])
+def test_small_bf16_greedy_matches_reference(recipe, seed):
+    check_16bit_greedy("small", recipe, seed, "bf16")
+
+
+def test_small_bf16_beam5_matches_reference():
+    check_16bit_beam5("small", "bf16")
+
+
+@pytest.mark.parametrize("recipe,seed,dtype", [("margin", 1, "bf16"), ("margin", 1, "f32"), ("diverse", 0, "bf16")])
+def test_c2_small_b32_1000_phrase_boost(recipe, seed, dtype):
+    """C2: whisper-small, 32 clips, 64 tokens (EOS masked), 1000 phrases, lambda 2. Rows 0-3 against the
+    oracle on clips 0-3 (bf16 margin-gated on the boosted scores, f32 exact), and the batch of 32 agrees
+    with the same 4 clips decoded alone (batch composition does not change a row)."""
+    dims = get_dims("small")
+    m = model("small", seed, recipe, dtype)
+    phrases = synth_bias_list(1000, eot=dims.eos_token_id)
+    x = mel_of(dims, 32)
+    kw = dict(max_length=64, min_new_tokens=64, bias_list=phrases, bias_boost=2.0)
+    ids = m.generate(x, **kw).cpu().numpy()
+    assert ids.shape == (32, 64)
+    four = m.generate(x[:4], **kw).cpu().numpy()
+    assert np.array_equal(four, ids[:4])
+    om = W.OracleModel.from_dims(dims, weights("small", seed, recipe))
+    ref, margin = om.generate(x[:4].numpy(), max_length=64, min_new_tokens=64, bias=phrases, bias_boost=2.0,
+                              return_margins=True, trim=False)
+    if dtype == "f32":
+        assert np.array_equal(ids[:4], ref), (ids[:4], ref)
+    else:
+        assert gated_equal(ids[:4], ref, margin) >= 4
+
+
+# ------------------------------------------------------------------ whisper-medium, 24 layers (C3)
+@pytest.mark.parametrize("recipe,seed", [("margin", 1), ("diverse", 0)])
+def test_medium_f32_greedy_and_beam5_match_reference(recipe, seed):
+    check_f32_greedy_and_beam("medium", recipe, seed)
+
+
+def test_medium_bf16_greedy_and_beam5_match_reference():
+    check_16bit_greedy("medium", "margin", 1, "bf16")
+    check_16bit_beam5("medium", "bf16")
+
+
+def test_c3_medium_bf16_beam5_1000_phrase_boost():
+    """C3 at reduced batch: full-depth medium, beam 5, bf16, 1000 phrases (lambda 2) on the high-margin
+    recipe: identical to the oracle's beam search with the same boost."""
+    check_beam5_boost("medium", "bf16", 1000, 2)
+
+
+# ------------------------------------------------------------------ whisper-large-v3, 32 layers (C5)
+def test_large_v3_f32_greedy_and_beam5_match_reference():
+    check_f32_greedy_and_beam("large-v3", "margin", 1)
+
+
+def test_large_v3_f16_greedy_and_beam5_match_reference():
+    check_16bit_greedy("large-v3", "margin", 1, "f16")
+    check_16bit_beam5("large-v3", "f16")
+
+
+def test_c5_large_v3_f16_beam5_5000_phrase_boost():
+    """C5 at reduced batch: full-depth large-v3 (128 mel bins), beam 5, fp16 with the encoder clamp,
+    5000 phrases (lambda 2), high-margin recipe: identical to the oracle."""
+    check_beam5_boost("large-v3", "f16", 5000, 1)

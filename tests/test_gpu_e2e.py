@@ -156,3 +156,49 @@ def test_greedy_bf16_kv_formulation_high_margin_exact():
             os.environ["WCB_XMODE"] = old
     ids = m.generate(torch.from_numpy(mel), max_length=ref.shape[1]).cpu().numpy()
     assert np.array_equal(ids, ref)
+
+
+def _collate_spans(samples, pad=50256):
+    """bias_spans exactly as the reference collator pads them (data_utils/data_collator.py:107-125):
+    every span right-padded with 50256 to the longest span, every sample to the most spans."""
+    L = max(len(sp) for s in samples for sp in s)
+    N = max(len(s) for s in samples)
+    return torch.tensor([[list(sp) + [pad] * (L - len(sp)) for sp in s] + [[pad] * L] * (N - len(s))
+                         for s in samples], dtype=torch.long)
+
+
+def test_generate_with_collator_bias_spans():
+    """The drop-in path: generate(input_features, labels, bias_spans=<collator tensor>, bias_boost>0) boosts
+    the union of the batch's spans (padding stripped); the collator's all-zeros [B, 1, 1] form boosts
+    nothing; bias_boost = 0 ignores the spans like the reference."""
+    dims, sd, om, mel, enc = case("micro", 0, "diverse", 2)
+    m = model("micro", 0, "diverse", "f32")
+    plain = om.generate(mel, enc=enc, max_length=16, min_new_tokens=16)
+    samples = [[list(map(int, plain[0, 2:5])), [11, 12]], [list(map(int, plain[1, 1:3])) + [7, 8]]]
+    spans = _collate_spans(samples)
+    union = [s for smp in samples for s in smp]
+    x = torch.from_numpy(mel)
+    kw = dict(max_length=16, min_new_tokens=16)
+    got = m.generate(x, bias_spans=spans, bias_boost=2.0, **kw).cpu().numpy()
+    via_list = m.generate(x, bias_list=union, bias_boost=2.0, **kw).cpu().numpy()
+    ref = om.generate(mel, enc=enc, bias=union, bias_boost=2.0, **kw)
+    assert np.array_equal(got, via_list) and np.array_equal(got, ref), (got, ref)
+    zeros = m.generate(x, bias_spans=torch.zeros(2, 1, 1, dtype=torch.long), bias_boost=2.0, **kw).cpu().numpy()
+    unboosted = m.generate(x, bias_spans=spans, bias_boost=0.0, **kw).cpu().numpy()
+    assert np.array_equal(zeros, plain) and np.array_equal(unboosted, plain)
+
+
+def test_generate_splits_batches_above_64_clips():
+    """A reference eval batch larger than one library call (64 clips) is decoded in order in several
+    calls and re-padded: the same rows as decoding the parts separately."""
+    dims = get_dims("micro")
+    m = model("micro", 0, "diverse", "f32")
+    mel = torch.from_numpy(W.log_mel(synth_batch(70), dims.n_mel))
+    ids = m.generate(mel, max_length=12).cpu().numpy()
+    a = m.generate(mel[:64], max_length=12).cpu().numpy()
+    b = m.generate(mel[64:], max_length=12).cpu().numpy()
+    w = max(a.shape[1], b.shape[1])
+    pad = lambda t: np.pad(t, ((0, 0), (0, w - t.shape[1])), constant_values=dims.pad_token_id)
+    assert ids.shape == (70, w) and np.array_equal(ids, np.concatenate([pad(a), pad(b)]))
+    beams = m.generate(mel[:70], max_length=6, num_beams=8).cpu().numpy()   # 512 / 8 = 64 clips per call
+    assert beams.shape[0] == 70

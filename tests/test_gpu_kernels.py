@@ -238,3 +238,25 @@ def test_gemm_ring_encoder_shapes(dt, M, N, K, act, resid):
     tol = 1e-4 if resid else (8e-3 if dt == "bf16" else 1e-3)
     err = ((out.double() - ref).abs() - tol * ref.abs()).max().item()
     assert err < 2e-4, err
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("Sk,split", [(1500, 1), (1500, 4), (37, 1), (1, 3)])
+def test_decode_attention_variants(dt, variant, Sk, split):
+    """Every cross-attention kernel variant in the runtime's head-major K/V layout, with and without
+    split-KV (variant 0 = the two-pass kernel beam search over precomputed K/V runs), vs fp64."""
+    lib = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(variant * 100 + Sk + split)
+    B, H = 5, 3
+    q = (torch.randn(B, H * 64, generator=g) * 0.3).to(DT[dt][0]).cuda()
+    k = torch.randn(B, H, Sk, 64, generator=g).to(DT[dt][0]).cuda()
+    v = torch.randn(B, H, Sk, 64, generator=g).to(DT[dt][0]).cuda()
+    o = torch.empty_like(q)
+    _lib.check(lib.wcb_op_attention_decode(DT[dt][1], q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), B, H, Sk,
+                                           split, variant, _s()), None, "attention_decode")
+    torch.cuda.synchronize()
+    p = torch.softmax(q.double().view(B, H, 1, 64) @ k.double().transpose(-1, -2), -1)
+    ref = (p @ v.double()).view(B, H * 64)
+    tol = 1e-5 if dt == "f32" else 1e-2
+    assert (o.double() - ref).abs().max().item() < tol

@@ -3,14 +3,10 @@
 Hand-written HIP kernels for gfx950 in `csrc/`, built into `libwcb.so` (C ABI: include/wcb.h).
 `WhisperCB` (model.py) is the drop-in for the reference model's generate()/forward() surface.
 """
-import os
-
-# The library runs the encoder stream and two decode streams concurrently (plus the caller's stream);
-# HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware queues (default 4), and streams sharing a
-# queue serialise against each other. Measured on MI355X: 4 or 8 queues cost 35-55 % of throughput.
-# The variable is read when the HIP runtime initialises, so it is set here, before any GPU call,
-# unless the user chose a value.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# The library runs one encoder stream and two decode streams beside the caller's stream. Round 2
+# measured the C2 benchmark at GPU_MAX_HW_QUEUES = 4 (the HIP default), 5, 6, 8 and 16: 14,818-14,966
+# audio-s/s, i.e. no dependence on the hardware-queue count, so nothing is set here (round 1 set 16
+# before HIP initialised, which silently did nothing when torch initialised HIP first).
 
 from .config import MODELS, WhisperDims, get_dims  # noqa: E402,F401
 

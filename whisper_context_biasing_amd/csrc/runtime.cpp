@@ -118,6 +118,8 @@ struct ProfEntry {
 struct wcb_bias {
   int n_states = 1;
   int vocab = 0;
+  uint64_t id = 0;                  // decode-graph cache key (never reused, unlike the address)
+  wcb_handle* owner = nullptr;      // the handle whose decode graphs may hold these device buffers
   DevBuf root_bits, root_child, trans_off, trans_tok, trans_dst;
 };
 
@@ -158,10 +160,11 @@ struct wcb_handle {
   // Cross-attention: one workgroup per (row, head) over all 1500 keys. Measured (tools/xattn_bench.py,
   // head-major K/V cycling 12 layers): split-KV hand-offs cost more than they hide at 16-32 rows.
   int xsplit = 1;
-  // cross-attention kernel variant over precomputed K/V (k_attn.hip launch_decode); -1 = auto: the
-  // single-pass kernel (1) when a launch has few (row, head) workgroups, else the two-pass kernel (0)
-  // (measured: C5 80 rows x 20 heads 1076 -> 1110 audio-s/s with 1; C3 320 x 16 2435 -> 2048 with 1)
-  int xvariant = -1;
+  // cross-attention kernel variant over precomputed K/V (k_attn.hip launch_decode), fixed at create
+  // from the model — never from the batch, whose composition must not change a clip's tokens (the
+  // two kernels sum in different orders): the single-pass kernel (1) for 20 heads (large-v3, C5:
+  // 1076 -> 1110 audio-s/s), the two-pass kernel (0) otherwise (medium, C3: 2435 vs 2048 with 1)
+  int xvariant = 0;
   // Cross-attention formulation: 1 = encoder space (k_xenc.hip: the step streams the encoder output,
   // no cross-K/V precompute; 16-bit dtypes, d <= 1024), 0 = precomputed per-layer K/V (f32 "exact"
   // mode, large-v3). Fixed at create (WCB_XMODE overrides where supported).
@@ -206,6 +209,8 @@ struct wcb_handle {
   DevBuf xkv2[kMaxCtx];
   // default (empty) bias automaton
   std::unique_ptr<wcb_bias> empty_bias;
+  std::vector<wcb_bias*> biases;     // live automatons created on this handle (lifetime, wcb.h)
+  uint64_t next_bias_id = 1;
   // profiling
   bool prof = false, prof_stamps = false;
   std::vector<ProfEntry> prof_e;
@@ -374,6 +379,7 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     HIPCHK(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
     if (const char* xs = getenv("WCB_XSPLIT")) h->xsplit = std::max(1, std::min(atoi(xs), kXSplit));
+    h->xvariant = desc->n_heads >= 20 ? 1 : 0;
     if (const char* xv = getenv("WCB_XVARIANT")) h->xvariant = atoi(xv);
     h->xmode = xenc_supported(h->dt, desc->d_model) ? 1 : 0;
     if (const char* xm = getenv("WCB_XMODE")) h->xmode = (atoi(xm) != 0 && h->xmode) ? 1 : 0;
@@ -439,6 +445,7 @@ void wcb_destroy(wcb_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
+  for (wcb_bias* b : h->biases) b->owner = nullptr;   // still valid to destroy; no graph holds them now
   for (DecCtx& D : h->dc) {
     if (D.gexec) (void)hipGraphExecDestroy(D.gexec);
     if (D.gexec_k) (void)hipGraphExecDestroy(D.gexec_k);
@@ -890,7 +897,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       xa.o = datt; xa.ldo = d; xa.o_Sb = 1; xa.B = nb; xa.H = H; xa.nkeys = S;
       xa.nsplit = h->xsplit; xa.part = D.xpart.as<float>() + (size_t)b0 * H * kXSplit * 66;
       xa.ticket = D.xticket.as<int>() + (size_t)b0 * H;
-      xa.variant = h->xvariant >= 0 ? h->xvariant : (nb * H <= 2048 ? 1 : 0);
+      xa.variant = h->xvariant;   // fixed per handle: the same clip decodes alike in any batch
       if (h->prof_stamps) {
         xa.stamp.base = h->stamps.as<unsigned long long>() + (size_t)c.buf * h->stamp_slots() * 2 * kStampSub;
         xa.stamp.pos = pos;
@@ -1095,8 +1102,8 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     sc.lm_head = true;
     sc.select = true;
     char key[256];
-    snprintf(key, sizeof key, "%d/%d/%d/%d/%p/%a/%d/%d/%d/%d", B, nb, Tc, out_ld, (const void*)bs, cfg->bias_boost,
-             cfg->min_new_tokens, h->n_sub, (int)h->prof_stamps, P);
+    snprintf(key, sizeof key, "%d/%d/%d/%d/%llu/%a/%d/%d/%d/%d", B, nb, Tc, out_ld, (unsigned long long)bs->id,
+             cfg->bias_boost, cfg->min_new_tokens, h->n_sub, (int)h->prof_stamps, P);
     const int max_new = cfg->max_new_tokens;
     // The decode step replays as a hipGraph; steps_per_graph steps are captured into one graph so the
     // per-replay gap is paid once per chunk (every position-dependent value is read on the device, so
@@ -1278,6 +1285,8 @@ int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets
     auto b = std::make_unique<wcb_bias>();
     b->n_states = ns;
     b->vocab = V;
+    b->id = h->next_bias_id++;
+    b->owner = h;
     HIPCHK(hipSetDevice(h->device));
     b->root_bits.ensure(bits.size() * 4);
     HIPCHK(hipMemcpy(b->root_bits.p, bits.data(), bits.size() * 4, hipMemcpyHostToDevice));
@@ -1291,12 +1300,31 @@ int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets
       HIPCHK(hipMemcpy(b->trans_tok.p, tok.data(), tok.size() * 4, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(b->trans_dst.p, dst.data(), dst.size() * 4, hipMemcpyHostToDevice));
     }
+    h->biases.push_back(b.get());
     *out = b.release();
   });
 }
 
+// Lifetime (wcb.h): the decode graphs of the owning handle capture the automaton's device buffers.
+// Destroying it waits for the handle's queued work and drops those graphs (they are re-captured by
+// the next wcb_generate), so a graph can never replay reads of freed memory.
 void wcb_bias_destroy(wcb_bias* b) {
   if (!b) return;
+  if (wcb_handle* h = b->owner) {
+    (void)hipSetDevice(h->device);
+    try {
+      quiesce(h);
+    } catch (...) {
+    }
+    for (DecCtx& D : h->dc)
+      if (D.gkey.find("/" + std::to_string(b->id) + "/") != std::string::npos) {
+        if (D.gexec) (void)hipGraphExecDestroy(D.gexec);
+        if (D.gexec_k) (void)hipGraphExecDestroy(D.gexec_k);
+        D.gexec = D.gexec_k = nullptr;
+        D.gkey.clear();
+      }
+    h->biases.erase(std::remove(h->biases.begin(), h->biases.end(), b), h->biases.end());
+  }
   for (DevBuf* x : {&b->root_bits, &b->root_child, &b->trans_off, &b->trans_tok, &b->trans_dst}) x->release();
   delete b;
 }

@@ -20,6 +20,7 @@ memory and streams. There is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+from collections import OrderedDict
 from dataclasses import dataclass
 from types import SimpleNamespace
 from typing import Dict, List, Optional, Sequence
@@ -107,7 +108,10 @@ class WhisperCB:
                                                  eos_token_id=dims.eos_token_id,
                                                  decoder_start_token_id=dims.decoder_start_token_id,
                                                  use_cache=True, num_beams=1, forced_decoder_ids=None)
-        self._bias_cache: Dict[tuple, BiasList] = {}
+        # device automatons of recently used bias lists (LRU: per-batch bias_spans lists would otherwise
+        # accumulate one V-sized automaton per distinct batch)
+        self._bias_cache: "OrderedDict[tuple, BiasList]" = OrderedDict()
+        self.bias_cache_size = 8
         self._loaded = False
 
     # ------------------------------------------------------------------ construction / weights
@@ -198,12 +202,21 @@ class WhisperCB:
         if b is None:
             b = BiasList(self, phrases)
             self._bias_cache[key] = b
+            while len(self._bias_cache) > self.bias_cache_size:
+                self._bias_cache.popitem(last=False)   # wcb_bias_destroy drops graphs that captured it
+        else:
+            self._bias_cache.move_to_end(key)
         return b
+
+    # the reference collator pads bias_spans with the literal 50256 whatever the model
+    # (data_utils/data_collator.py:119-121)
+    collator_span_pad = 50256
 
     def _spans_to_phrases(self, bias_spans) -> List[List[int]]:
         """Union of the collator's padded per-sample spans ([B, N, L], pad 50256 —
-        data_utils/data_collator.py:107-125) with the padding stripped."""
-        pad = 50256
+        data_utils/data_collator.py:107-125; the all-zeros [B, 1, 1] "no spans" form gives none) with
+        the padding stripped."""
+        pad = self.collator_span_pad
         arr = torch.as_tensor(bias_spans).cpu().numpy()
         out, seen = [], set()
         for sample in arr:
@@ -236,12 +249,31 @@ class WhisperCB:
         """
         if not self._loaded:
             raise _lib.WcbError("weights not loaded")
+        x_all = self._features(input_features)
+        nb_req = int(num_beams if num_beams is not None else getattr(generation_config or self.generation_config,
+                                                                      "num_beams", 1) or 1)
+        per_call = self.max_clips_per_call(nb_req)
+        if x_all.shape[0] > per_call:
+            # the library takes at most 64 clips (512 decoder rows) per call: split, decode in order,
+            # re-pad to the longest row (Whisper's padding of the joined output)
+            kw = dict(labels=labels, bias_spans=bias_spans, max_length=max_length, num_beams=num_beams,
+                      bias_list=bias_list, bias_boost=bias_boost, min_new_tokens=min_new_tokens,
+                      prompt_ids=prompt_ids, return_dict_in_generate=return_dict_in_generate,
+                      generation_config=generation_config, use_graph=use_graph, block=True)
+            if bias_list is None and bias_boost > 0 and bias_spans is not None:
+                kw["bias_list"], kw["bias_spans"] = self._spans_to_phrases(bias_spans), None
+            parts = [self.generate(x_all[i:i + per_call], **kw) for i in range(0, x_all.shape[0], per_call)]
+            seqs = [p.sequences if return_dict_in_generate else p for p in parts]
+            Wd = max(t.shape[1] for t in seqs)
+            fill = self.dims.pad_token_id
+            out = torch.cat([torch.nn.functional.pad(t, (0, Wd - t.shape[1]), value=fill) for t in seqs])
+            return GenerateOutput(sequences=out) if return_dict_in_generate else out
         gc = generation_config or self.generation_config
         max_length = int(max_length if max_length is not None else getattr(gc, "max_length", 448))
         num_beams = int(num_beams if num_beams is not None else getattr(gc, "num_beams", 1) or 1)
         if not 1 <= num_beams <= 8:
             raise ValueError("num_beams must be in [1, 8]")
-        x = self._features(input_features)
+        x = x_all
         B = x.shape[0]
         prefix = [self.dims.decoder_start_token_id]
         if prompt_ids is not None:
@@ -271,6 +303,11 @@ class WhisperCB:
             sot = torch.tensor(prefix, dtype=torch.int64, device=self.device)[None].expand(B, -1)
             return GenerateOutput(sequences=torch.cat([sot, ids], dim=1))
         return self._whisper_trim(ids)
+
+    @staticmethod
+    def max_clips_per_call(num_beams: int = 1) -> int:
+        """Clips one wcb_generate call takes (64, and at most 512 decoder rows = clips x beams)."""
+        return max(1, min(64, 512 // max(1, int(num_beams))))
 
     def _whisper_trim(self, ids: torch.Tensor) -> torch.Tensor:
         """Whisper's short-form post-processing ([tf] generation_whisper.py:1063-1086, then
@@ -314,6 +351,15 @@ class WhisperCB:
                 decoder_input_ids = dec
         ids = torch.as_tensor(decoder_input_ids).to(self.device, torch.int32).contiguous()
         x = self._features(input_features)
+        if x.shape[0] > 64:   # 64 clips per library call: split, concatenate
+            outs = [self.forward(x[i:i + 64], decoder_input_ids=ids[i:i + 64]) for i in range(0, x.shape[0], 64)]
+            logits = torch.cat([o.logits for o in outs])
+            enc = torch.cat([o.encoder_last_hidden_state for o in outs])
+            loss = None
+            if labels is not None:
+                from .loss import weighted_ce
+                loss = weighted_ce(logits, labels.to(self.device), bias_spans, self.bias_weight)
+            return Seq2SeqLMOutput(loss=loss, logits=logits, encoder_last_hidden_state=enc)
         B, T = ids.shape
         logits = torch.empty(B, T, self.dims.vocab, dtype=torch.float32, device=self.device)
         enc = torch.empty(B, self.dims.n_audio_ctx, self.dims.d_model, dtype=self.torch_dtype, device=self.device)

@@ -69,17 +69,25 @@ def max_over_ranks(value: float, device: torch.device) -> float:
     return float(t.item())
 
 
-def gather_shards(local: torch.Tensor, device: torch.device) -> List[torch.Tensor]:
-    """Collect every rank's result rows (evaluation-time convenience; not on the timed path)."""
+def gather_shards(local: torch.Tensor, device: torch.device, pad_value: int = 0) -> List[torch.Tensor]:
+    """Collect every rank's result rows (evaluation-time convenience; not on the timed path).
+
+    Ranks may return different numbers of rows and — with natural-EOS decoding, where generate()
+    trims each shard to its own longest row — different widths: both are all-gathered first, every
+    shard is padded (rows with zeros, columns with `pad_value`, the tokenizer's pad id) to the global
+    maximum for the collective, and each rank's rows come back at the common width."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return [local]
     world = dist.get_world_size()
-    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=device)
-    ns = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(ns, n)
-    mx = int(max(int(x.item()) for x in ns))
-    pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=device)
-    pad[:local.shape[0]] = local.to(device)
-    bufs = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(bufs, pad)
-    return [b[:int(k.item())] for b, k in zip(bufs, ns)]
+    local = local.reshape(local.shape[0], -1) if local.dim() == 1 else local
+    shp = torch.tensor([local.shape[0], local.shape[1] if local.dim() > 1 else 1], dtype=torch.int64, device=device)
+    shps = [torch.zeros_like(shp) for _ in range(world)]
+    dist.all_gather(shps, shp)
+    mr = int(max(int(x[0].item()) for x in shps))
+    mc = int(max(int(x[1].item()) for x in shps))
+    buf = torch.full((mr, mc) + tuple(local.shape[2:]), pad_value, dtype=local.dtype, device=device)
+    buf[local.shape[0]:] = 0
+    buf[:local.shape[0], :local.shape[1]] = local.to(device)
+    bufs = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(bufs, buf)
+    return [b[:int(k[0].item())] for b, k in zip(bufs, shps)]
