@@ -34,6 +34,8 @@ PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, ch
 PEAK_F16_TFLOPS = 2500.0
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
+ENC_GEMMS = ("enc_conv1", "enc_conv2", "enc_qkv", "enc_out", "enc_fc1", "enc_fc2")
+DEC_PROJ = ("dec_qkv", "dec_out", "dec_xq", "dec_kq", "dec_vg", "dec_xo", "dec_fc1", "dec_fc2", "lm_head")
 
 
 def log(*a):
@@ -89,17 +91,19 @@ def cpu_baseline(size: str, n_tokens: int, n_phr: int, boost: float, seed: int =
                       f"(OMP_NUM_THREADS), host has {os.cpu_count()} logical CPUs"}
 
 
-def _pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass (profiles/*pmc*.json,
-    written by tools/pmc_traffic.py: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE), or None."""
+def _pmc_traffic(kernel: str, grid: int):
+    """HBM bytes per launch of (kernel symbol, grid) from the committed rocprofv3 PMC passes
+    (profiles/*pmc*.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2 (gfx950 correction) +
+    WRITE_SIZE), or None."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if kernel in d.get("kernels", {}):
-            return d["kernels"][kernel]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+        e = d.get("kernels", {}).get(f"{kernel}|{grid}")
+        if e:
+            return e["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
     return None
 
 
@@ -126,6 +130,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=2, help="steps of the serialised roofline pass")
     ap.add_argument("--no-overlap", action="store_true",
                     help="serialise batches (default: batch i+1's front end + encoder overlap batch i's decode)")
     args = ap.parse_args()
@@ -182,10 +187,6 @@ def main():
         log(f"warmup {i} done, ids {tuple(ids.shape)}")
     assert ids.shape[0] == B and (args.num_beams > 1 or ids.shape == (B, args.new_tokens))
     keep.clear()
-    if not args.no_profile:
-        # inside the timed region only the device stamps of the decode cross-attention are on (they
-        # live in the kernel; HIP timing events on the library streams perturb the stream overlap)
-        model.profile_enable(True, events=False, stamps=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -199,70 +200,84 @@ def main():
     elapsed = max_over_ranks(time.perf_counter() - t0, dev)
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B * 30.0 / (elapsed / args.steps)
-    prof, prof_steps = {}, args.steps
+    keep.clear()
+
+    # ---- per-kernel-class roofline: a separate, untimed pass of the same step in which every launch
+    #      (front end, encoder, each decode-step kernel) carries the kernel's own begin/end timestamps
+    #      (hipExtLaunchKernel events; the decode runs eagerly since a replayed graph node cannot carry
+    #      them) — the source rocprofv3's kernel trace reads, so profiles/ reproduces these durations.
+    prof, prof_steps = {}, 0
     if not args.no_profile:
-        prof = model.profile_read()
-        # phase breakdown + encoder GEMM timing: a separate, untimed pass with HIP events on every
-        # front-end / encoder launch
-        prof_steps = max(2, min(args.steps, 5))
+        prof_steps = max(1, min(args.steps, args.profile_steps))
         model.profile_enable(True, events=True, stamps=False)
         for i in range(prof_steps):
-            step()
+            mel = model.log_mel(pcm)
+            model.generate(mel, max_length=args.new_tokens, min_new_tokens=args.new_tokens, bias_list=phrases,
+                           bias_boost=args.boost, use_graph=False, block=True, num_beams=args.num_beams)
         model.synchronize()
         torch.cuda.synchronize()
-        pass_prof = model.profile_read()
+        prof = model.profile_read()
         model.profile_enable(False)
-        keep.clear()
-        pass_prof.pop("dec_xattn", None)
-        for k, v in pass_prof.items():
-            prof.setdefault(k, v)
-    roofs = {}
-    if prof.get("enc_gemm"):
-        # encoder tile GEMMs: HIP events on the encoder stream around every launch
-        p = prof["enc_gemm"]
-        avg_ms = p["ms"] / p["launches"]
-        achieved = p["flops"] / p["launches"] / (avg_ms * 1e-3) / 1e12
-        peak = {"bf16": PEAK_BF16_TFLOPS, "f16": PEAK_F16_TFLOPS}.get(args.dtype, PEAK_F32_TFLOPS)
-        kn = ("gemm_ring_kernel (encoder QKV/out/fc1/fc2/conv2, LDS-DMA ring; conv1 gemm_tile_kernel)"
-              if args.dtype in ("bf16", "f16") else "gemm_tile_kernel (encoder conv/QKV/out/fc1/fc2)")
-        roofs["enc_gemm"] = {"bound": "mfma", "kernel": kn,
-                             "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                             "frac": round(achieved / peak, 4), "traffic": None,
-                             "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": p["flops"] / p["launches"],
-                             "total_ms_per_step": round(p["ms"] / prof_steps, 3),
-                             "timing": "hip_events (separate profiled pass of the same step)"}
-    if prof.get("dec_xattn"):
-        # decode cross-attention: replayed inside the decode hipGraph, so each launch is timed by
-        # s_memrealtime stamps (first workgroup start → last workgroup end) written by the kernel
-        p = prof["dec_xattn"]
-        avg_ms = p["ms"] / p["launches"]
-        bpl = p["bytes"] / p["launches"]
-        achieved = bpl / (avg_ms * 1e-3) / 1e9
-        xenc = args.dtype in ("bf16", "f16") and dims.d_model <= 1024 and os.environ.get("WCB_XMODE", "1") != "0" \
-            and (args.num_beams == 1 or os.environ.get("WCB_BEAM_XMODE", "0") == "1")
-        kname = ("attn_xenc_kernel (decoder cross-attention in encoder space: one pass over the encoder "
-                 "output per layer for all heads)") if xenc else \
-            "attn_decode2p_kernel / attn_decode_kernel (decoder cross-attention over precomputed per-layer K/V; " \
-            "single-pass kernel when a launch has <= 2048 (row, head) workgroups)"
-        roofs["dec_xattn"] = {"bound": "hbm", "kernel": kname,
-                              "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                              "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-                              "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": bpl,
-                              "total_ms_per_step": round(p["ms"] / args.steps, 3),
-                              "timing": "device s_memrealtime stamps (graph node), inside the timed region"}
-    roof = None
-    if roofs:
-        dom = max(roofs, key=lambda k: roofs[k]["total_ms_per_step"])   # dominant = most kernel time
-        roof = dict(roofs[dom])
-        # the committed PMC pass (tools/measure.sh) measures the default C2 workload only
+        prof.pop("decode_loop", None)
+        prof.pop("xkv_gemm_total", None)
+    roof, others = None, {}
+    if prof:
+        peak_mfma = {"bf16": PEAK_BF16_TFLOPS, "f16": PEAK_F16_TFLOPS}.get(args.dtype, PEAK_F32_TFLOPS)
+        classes = {}
+        for k, v in prof.items():
+            if not v["launches"] or v["ms"] <= 0:
+                continue
+            avg_ms = v["ms"] / v["launches"]
+            mfma = k.startswith("enc_") or k == "xkv_gemm"   # encoder / cross-K/V GEMMs and flash attention
+            if mfma:
+                ach = v["flops"] / v["launches"] / (avg_ms * 1e-3) / 1e12
+                peak, unit = peak_mfma, "TFLOP/s"
+            else:
+                ach = v["bytes"] / v["launches"] / (avg_ms * 1e-3) / 1e9
+                peak, unit = PEAK_HBM_GBS, "GB/s"
+            classes[k] = {"bound": "mfma" if mfma else "hbm",
+                          "kernel": v.get("kernel", "").split("(")[0], "grid": v.get("grid", 0),
+                          "achieved": round(ach, 1), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
+                          "traffic": None, "avg_launch_ms": round(avg_ms, 5),
+                          "launches_per_step": v["launches"] / prof_steps,
+                          "bytes_per_launch": v["bytes"] / v["launches"], "flops_per_launch": v["flops"] / v["launches"],
+                          "total_ms_per_step": round(v["ms"] / prof_steps, 3)}
+        # dominant = the (kernel symbol, grid) with the most time per step — rocprofv3's grouping, so
+        # classes sharing one kernel instance and grid (e.g. dec_out / dec_xo) are summed as it sums them
+        groups = {}
+        for k, c in classes.items():
+            gk = f'{c["kernel"]}|{c["grid"]}'
+            g = groups.setdefault(gk, {"classes": [], "ms": 0.0, "launches": 0.0, "bytes": 0.0, "flops": 0.0})
+            g["classes"].append(k)
+            g["ms"] += c["total_ms_per_step"]
+            g["launches"] += c["launches_per_step"]
+            g["bytes"] += c["bytes_per_launch"] * c["launches_per_step"]
+            g["flops"] += c["flops_per_launch"] * c["launches_per_step"]
+        gk = max(groups, key=lambda k: groups[k]["ms"])
+        g = groups[gk]
+        dom = max(g["classes"], key=lambda k: classes[k]["total_ms_per_step"])
+        c = classes[dom]
+        avg_ms = g["ms"] / g["launches"]
+        per = (g["flops"] if c["bound"] == "mfma" else g["bytes"]) / g["launches"]
+        ach = per / (avg_ms * 1e-3) / (1e12 if c["bound"] == "mfma" else 1e9)
+        roof = dict(c, **{"class": "+".join(g["classes"]), "achieved": round(ach, 1),
+                          "frac": round(ach / c["peak"], 4), "avg_launch_ms": round(avg_ms, 5),
+                          "launches_per_step": g["launches"], "bytes_per_launch": g["bytes"] / g["launches"],
+                          "flops_per_launch": g["flops"] / g["launches"], "total_ms_per_step": round(g["ms"], 3),
+                          "timing": "kernel begin/end timestamps of every launch (hipExtLaunchKernel events) in a "
+                                    f"serialised profiling pass of {prof_steps} step(s); rocprofv3 trace of the "
+                                    "same command: profiles/ (tools/check_roofline.py compares the two)"})
         c2 = (args.model, args.batch, args.num_beams, args.dtype, args.new_tokens) == ("small", 32, 1, "bf16", 64)
-        tr = _pmc_traffic(dom) if c2 else None
+        tr = _pmc_traffic(roof["kernel"], roof["grid"]) if c2 else None
         if tr:
             roof["traffic"], roof["traffic_source"] = tr
-        others = {k: v for k, v in roofs.items() if k != dom}
-    phases = {k: {"ms_per_step": round(v["ms"] / (args.steps if k == "dec_xattn" else prof_steps), 3),
-                  "launches_per_step": v["launches"] / (args.steps if k == "dec_xattn" else prof_steps)}
+        others = {k: v for k, v in classes.items() if k not in g["classes"]}
+    phases = {k: {"ms_per_step": round(v["ms"] / prof_steps, 3), "launches_per_step": v["launches"] / prof_steps}
               for k, v in prof.items()}
+    if phases:   # family totals: every encoder GEMM, every decode projection (LM head included)
+        fam = lambda pred: round(sum(v["ms_per_step"] for k, v in phases.items() if pred(k)), 3)
+        phases["family:enc_gemm"] = {"ms_per_step": fam(lambda k: k in ENC_GEMMS)}
+        phases["family:dec_proj"] = {"ms_per_step": fam(lambda k: k in DEC_PROJ)}
 
     # biased-WER half of the metric, as a plumbing check (random weights: no transcript to score
     # against): the boosted decode of the last batch against a λ = 0 decode of the same clips, scored
@@ -317,7 +332,7 @@ def main():
                        "hipgraph_decode": use_graph, "batches_in_flight": (int(os.environ.get("WCB_DECODE_CTX", "2")) + 1) if overlap else 1},
             "rtf": round(1.0 / (value / world), 6),
             "roofline": roof,
-            "roofline_other": others if roofs else None,
+            "roofline_other": others or None,
             "phases": phases,
             "cpu_baseline": cpu,
             "biased_wer": bias_plumb,

@@ -113,6 +113,11 @@ int wcb_profile_enable(wcb_handle* h, int enable);
 int wcb_profile_read(wcb_handle* h, int n, char (*names)[32], int64_t* launches, double* ms,
                      double* flops, double* bytes);
 
+/* entry i of wcb_profile_read: the (demangled) kernel symbol of the class's first launch and its grid
+ * in threads, as rocprofv3's kernel trace names them (Kernel_Name, Grid_Size_X); "" when the class
+ * launched nothing or was stamped on the device */
+int wcb_profile_kernel(wcb_handle* h, int i, char* name, int cap, int64_t* grid);
+
 /* debug: copy an internal workspace buffer (xt, hbuf, x, h, qkv, att, ffn, encout, xkv, logits)
  * into dst (device) after synchronising; enc_layers limits later encodes to that many layers
  * (-1 = all). bytes == 0 only sets the limit. */

@@ -11,7 +11,7 @@ cat "$O/bench_default.json"
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-profile > "$O/bench_noprof.json" 2> "$O/bench_noprof.err" || exit 1
 cat "$O/bench_noprof.json"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/trace" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$O/trace_bench.json" 2> "$O/trace_bench.err" || exit 1
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$O/trace" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline > "$O/trace_bench.json" 2> "$O/trace_bench.err" || exit 1
 # PMC passes on a light run of the same launches (4 tokens, serialised batches): one counter group each
 PMC_ARGS="--steps 1 --warmup 1 --new-tokens 4 --no-overlap --no-cpu-baseline --no-profile"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch" -o run --output-format csv -- python3 "$R/bench.py" $PMC_ARGS > "$O/pmc_fetch.out" 2> "$O/pmc_fetch.err" || { tail -5 "$O/pmc_fetch.err"; exit 1; }
@@ -19,4 +19,9 @@ timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write" -o run --output
 cd "$R"
 python tools/prof_summary.py "$(ls "$O"/trace/*kernel_trace.csv "$O"/trace/*/*kernel_trace.csv 2>/dev/null | head -1)" 40 > "$O/kernel_summary.txt"
 cat "$O/kernel_summary.txt" | head -25
-python tools/pmc_traffic.py "$O/pmc_fetch" "$O/pmc_write" "$O/pmc_traffic.json"
+python tools/pmc_traffic.py "$O/pmc_fetch" "$O/pmc_write" "$O/pmc_traffic.json" > /dev/null
+TRACE="$(ls "$O"/trace/*kernel_trace.csv "$O"/trace/*/*kernel_trace.csv 2>/dev/null | head -1)"
+python tools/check_roofline.py "$O/bench_default.json" "$TRACE" > "$O/check_default.json"; cat "$O/check_default.json"
+python tools/check_roofline.py "$O/trace_bench.json" "$TRACE" > "$O/check_traced.json"; cat "$O/check_traced.json"
+STATS="$(ls "$O"/trace/*kernel_stats.csv "$O"/trace/*/*kernel_stats.csv 2>/dev/null | head -1)"
+cp "$STATS" "$O/kernel_stats.csv"

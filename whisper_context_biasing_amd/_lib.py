@@ -48,6 +48,7 @@ SIGNATURES = {
     "wcb_debug_copy": (C.c_int, [_P, C.c_char_p, _P, C.c_int64, C.c_int]),
     "wcb_profile_enable": (C.c_int, [_P, C.c_int]),
     "wcb_profile_read": (C.c_int, [_P, C.c_int, _P, _P, _P, _P, _P]),
+    "wcb_profile_kernel": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_int64)]),
     "wcb_op_gemm": (C.c_int, [C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P, _P,
                               C.c_int, _P]),
     "wcb_op_gemm_ln": (C.c_int, [C.c_int, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P,

@@ -411,7 +411,7 @@ static void launch_ring_e(const GemmArgs& g, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
+  WCB_LAUNCH((gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
 }
 
 template <typename T, int BM, int BN, int WM, int WN, int NS>
@@ -908,10 +908,10 @@ static void launch_dec_k(const GemmArgs& g, hipStream_t s) {
   const int ntile = (g.N + 15) / 16, gy = (g.M + MF * 16 - 1) / (MF * 16);
   // one tile per workgroup up to ~4 workgroups per CU; beyond (the LM head) a persistent column walk
   if (!g.sel_val && (AM == 3 || ntile * gy <= 1024)) {
-    hipLaunchKernelGGL((gemm_dec_kernel<T, MF, NW, KPW, AM, false>), dim3(ntile, gy), dim3(NW * 64), 0, s, g);
+    WCB_LAUNCH((gemm_dec_kernel<T, MF, NW, KPW, AM, false>), dim3(ntile, gy), dim3(NW * 64), 0, s, g);
   } else {   // the LM head: kDecWalkers column walkers per row block (= argmax partials per row)
     const int gx = std::min(ntile, kDecWalkers);
-    hipLaunchKernelGGL((gemm_dec_kernel<T, MF, NW, KPW, AM == 3 ? 0 : AM, true>), dim3(gx, gy), dim3(NW * 64), 0, s, g);
+    WCB_LAUNCH((gemm_dec_kernel<T, MF, NW, KPW, AM == 3 ? 0 : AM, true>), dim3(gx, gy), dim3(NW * 64), 0, s, g);
   }
 }
 
@@ -967,7 +967,7 @@ static void launch_tile_e(const GemmArgs& g, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_tile_kernel<T, BM, BN, WM, WN, EPI>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
+  WCB_LAUNCH((gemm_tile_kernel<T, BM, BN, WM, WN, EPI>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
 }
 
 template <typename T, int BM, int BN, int WM, int WN>
@@ -988,8 +988,8 @@ static void launch_tile(const GemmArgs& g, hipStream_t s) {
 template <typename T, int MF, int NF, int NW, int KS>
 static void launch_skinny_k(const GemmArgs& g, hipStream_t s) {
   const dim3 grid((g.N + NF * 16 - 1) / (NF * 16), (g.M + MF * 16 - 1) / (MF * 16));
-  if (g.ln_w) hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NF, NW, KS, true>), grid, dim3(NW * 64), 0, s, g);
-  else hipLaunchKernelGGL((gemm_skinny_kernel<T, MF, NF, NW, KS, false>), grid, dim3(NW * 64), 0, s, g);
+  if (g.ln_w) WCB_LAUNCH((gemm_skinny_kernel<T, MF, NF, NW, KS, true>), grid, dim3(NW * 64), 0, s, g);
+  else WCB_LAUNCH((gemm_skinny_kernel<T, MF, NF, NW, KS, false>), grid, dim3(NW * 64), 0, s, g);
 }
 
 // K = NW waves x KS steps x 32: pick the wave count first, then the (compile-time) steps per wave.

@@ -313,16 +313,16 @@ __global__ __launch_bounds__(NW * 64) void attn_decode2p_kernel(AttnArgs a) {
 template <typename T>
 static void launch_decode(const AttnArgs& b, dim3 grid, int variant, hipStream_t s) {
   if (b.phys) {   // beam-search self-attention: keys through the row map
-    hipLaunchKernelGGL((attn_decode_kernel<T, 4, 8, true>), grid, dim3(256), 0, s, b);
+    WCB_LAUNCH((attn_decode_kernel<T, 4, 8, true>), grid, dim3(256), 0, s, b);
     return;
   }
   switch (variant) {
-    case 0: hipLaunchKernelGGL((attn_decode2p_kernel<T, 8>), grid, dim3(512), 0, s, b); break;
-    case 1: hipLaunchKernelGGL((attn_decode_kernel<T, 4, 8>), grid, dim3(256), 0, s, b); break;
-    case 2: hipLaunchKernelGGL((attn_decode_kernel<T, 4, 4>), grid, dim3(256), 0, s, b); break;
-    case 3: hipLaunchKernelGGL((attn_decode_kernel<T, 8, 4>), grid, dim3(512), 0, s, b); break;
-    case 4: hipLaunchKernelGGL((attn_decode_kernel<T, 8, 8>), grid, dim3(512), 0, s, b); break;
-    default: hipLaunchKernelGGL((attn_decode_kernel<T, 16, 4>), grid, dim3(1024), 0, s, b); break;
+    case 0: WCB_LAUNCH((attn_decode2p_kernel<T, 8>), grid, dim3(512), 0, s, b); break;
+    case 1: WCB_LAUNCH((attn_decode_kernel<T, 4, 8>), grid, dim3(256), 0, s, b); break;
+    case 2: WCB_LAUNCH((attn_decode_kernel<T, 4, 4>), grid, dim3(256), 0, s, b); break;
+    case 3: WCB_LAUNCH((attn_decode_kernel<T, 8, 4>), grid, dim3(512), 0, s, b); break;
+    case 4: WCB_LAUNCH((attn_decode_kernel<T, 8, 8>), grid, dim3(512), 0, s, b); break;
+    default: WCB_LAUNCH((attn_decode_kernel<T, 16, 4>), grid, dim3(1024), 0, s, b); break;
   }
 }
 
@@ -481,8 +481,8 @@ bool attention_flash(DType t, const AttnArgs& a, hipStream_t s) {
   constexpr int QW = 2;
   const dim3 grid((a.Sq + 4 * QW * 16 - 1) / (4 * QW * 16), a.B * a.H);
   switch (t) {
-    case kBF16: hipLaunchKernelGGL((attn_flash_kernel<bf16_t, QW>), grid, dim3(256), 0, s, a); return true;
-    case kF16: hipLaunchKernelGGL((attn_flash_kernel<f16_t, QW>), grid, dim3(256), 0, s, a); return true;
+    case kBF16: WCB_LAUNCH((attn_flash_kernel<bf16_t, QW>), grid, dim3(256), 0, s, a); return true;
+    case kF16: WCB_LAUNCH((attn_flash_kernel<f16_t, QW>), grid, dim3(256), 0, s, a); return true;
     default: return false;
   }
 }

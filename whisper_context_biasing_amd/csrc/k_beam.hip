@@ -325,14 +325,14 @@ __global__ __launch_bounds__(256) void beam_output_kernel(BeamArgs a) {
 }
 
 void beam_init(const BeamArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(beam_init_kernel, dim3(a.B * a.nb), dim3(256), 0, s, a);
+  WCB_LAUNCH(beam_init_kernel, dim3(a.B * a.nb), dim3(256), 0, s, a);
 }
 void beam_select(const BeamArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(beam_topk_kernel, dim3(a.B * a.nb), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(beam_step_kernel, dim3(a.B), dim3(256), 0, s, a);
+  WCB_LAUNCH(beam_topk_kernel, dim3(a.B * a.nb), dim3(256), 0, s, a);
+  WCB_LAUNCH(beam_step_kernel, dim3(a.B), dim3(256), 0, s, a);
 }
 void beam_output(const BeamArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(beam_output_kernel, dim3(a.B), dim3(256), 0, s, a);
+  WCB_LAUNCH(beam_output_kernel, dim3(a.B), dim3(256), 0, s, a);
 }
 
 }  // namespace wcb

@@ -108,13 +108,13 @@ void logmel_power_mel(const float* pcm, long pcm_stride, int n_samples, int B, c
                       const int* mel_hi, const float* mel_w, int n_mel, float* mel_out, unsigned* clip_max,
                       hipStream_t s) {
   (void)hipMemsetAsync(clip_max, 0, sizeof(unsigned) * B, s);
-  hipLaunchKernelGGL(logmel_power_mel_kernel, dim3((kFrames + kFPB - 1) / kFPB, B), dim3(256), 0, s, pcm, pcm_stride,
+  WCB_LAUNCH(logmel_power_mel_kernel, dim3((kFrames + kFPB - 1) / kFPB, B), dim3(256), 0, s, pcm, pcm_stride,
                      n_samples, dft, mel_lo, mel_hi, mel_w, n_mel, mel_out, clip_max);
 }
 
 void logmel_normalize(float* mel, const unsigned* clip_max, int B, int n_mel, hipStream_t s) {
   const long total = (long)B * n_mel * kFrames;
-  hipLaunchKernelGGL(logmel_normalize_kernel, dim3(2048), dim3(256), 0, s, mel, clip_max, n_mel * kFrames, total);
+  WCB_LAUNCH(logmel_normalize_kernel, dim3(2048), dim3(256), 0, s, mel, clip_max, n_mel * kFrames, total);
 }
 
 // mel f32 [B][n_mel][3000] → T [B][3002][n_mel] (rows 0 and 3001 zero: conv1 padding=1),
@@ -142,9 +142,9 @@ __global__ void mel_to_conv_input_kernel(const float* __restrict__ mel, int n_me
 void mel_to_conv_input(DType t, const float* mel, int B, int n_mel, void* xt, long clip_stride, hipStream_t s) {
   const dim3 grid((kFrames + 63) / 64, (n_mel + 63) / 64, B);
   switch (t) {
-    case kBF16: hipLaunchKernelGGL(mel_to_conv_input_kernel<bf16_t>, grid, dim3(256), 0, s, mel, n_mel, (bf16_t*)xt, clip_stride); break;
-    case kF16: hipLaunchKernelGGL(mel_to_conv_input_kernel<f16_t>, grid, dim3(256), 0, s, mel, n_mel, (f16_t*)xt, clip_stride); break;
-    case kF32: hipLaunchKernelGGL(mel_to_conv_input_kernel<float>, grid, dim3(256), 0, s, mel, n_mel, (float*)xt, clip_stride); break;
+    case kBF16: WCB_LAUNCH(mel_to_conv_input_kernel<bf16_t>, grid, dim3(256), 0, s, mel, n_mel, (bf16_t*)xt, clip_stride); break;
+    case kF16: WCB_LAUNCH(mel_to_conv_input_kernel<f16_t>, grid, dim3(256), 0, s, mel, n_mel, (f16_t*)xt, clip_stride); break;
+    case kF32: WCB_LAUNCH(mel_to_conv_input_kernel<float>, grid, dim3(256), 0, s, mel, n_mel, (float*)xt, clip_stride); break;
   }
 }
 

@@ -126,8 +126,8 @@ __global__ __launch_bounds__(1024) void wce_reduce_kernel(WceArgs a) {
 }
 
 void weighted_ce(const WceArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(wce_row_kernel, dim3(a.B * a.T), dim3(kWceThreads), 0, s, a);
-  hipLaunchKernelGGL(wce_reduce_kernel, dim3(1), dim3(1024), 0, s, a);
+  WCB_LAUNCH(wce_row_kernel, dim3(a.B * a.T), dim3(kWceThreads), 0, s, a);
+  WCB_LAUNCH(wce_reduce_kernel, dim3(1), dim3(1024), 0, s, a);
 }
 
 }  // namespace wcb

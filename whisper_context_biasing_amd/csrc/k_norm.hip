@@ -60,12 +60,12 @@ static void layernorm_t(const float* x, const float* w, const float* b, void* y,
   T* yy = reinterpret_cast<T*>(y);
   // every Whisper width is a multiple of 64: d/64 elements per lane, grouped VEC at a time
   if (d % 256 == 0 && d <= 2048) {
-    if (d <= 1024) hipLaunchKernelGGL((layernorm_kernel<T, 4, 4>), grid, blk, 0, s, x, w, b, yy, M, d);
-    else hipLaunchKernelGGL((layernorm_kernel<T, 4, 8>), grid, blk, 0, s, x, w, b, yy, M, d);
+    if (d <= 1024) WCB_LAUNCH((layernorm_kernel<T, 4, 4>), grid, blk, 0, s, x, w, b, yy, M, d);
+    else WCB_LAUNCH((layernorm_kernel<T, 4, 8>), grid, blk, 0, s, x, w, b, yy, M, d);
   } else if (d % 128 == 0 && d <= 1024) {
-    hipLaunchKernelGGL((layernorm_kernel<T, 2, 8>), grid, blk, 0, s, x, w, b, yy, M, d);
+    WCB_LAUNCH((layernorm_kernel<T, 2, 8>), grid, blk, 0, s, x, w, b, yy, M, d);
   } else {
-    hipLaunchKernelGGL((layernorm_kernel<T, 1, 32>), grid, blk, 0, s, x, w, b, yy, M, d);
+    WCB_LAUNCH((layernorm_kernel<T, 1, 32>), grid, blk, 0, s, x, w, b, yy, M, d);
   }
 }
 
@@ -108,11 +108,11 @@ __global__ __launch_bounds__(256) void embed_kernel(const T* __restrict__ emb, c
 void embed(DType t, const void* emb, const void* pemb, const int* ids, const int* pos, float* x, float* st, int M,
            int d, hipStream_t s, void* x16, int V) {
   switch (t) {
-    case kBF16: hipLaunchKernelGGL(embed_kernel<bf16_t>, dim3(M), dim3(256), 0, s, (const bf16_t*)emb,
+    case kBF16: WCB_LAUNCH(embed_kernel<bf16_t>, dim3(M), dim3(256), 0, s, (const bf16_t*)emb,
                                    (const bf16_t*)pemb, ids, pos, x, st, M, d, (bf16_t*)x16, V); break;
-    case kF16: hipLaunchKernelGGL(embed_kernel<f16_t>, dim3(M), dim3(256), 0, s, (const f16_t*)emb,
+    case kF16: WCB_LAUNCH(embed_kernel<f16_t>, dim3(M), dim3(256), 0, s, (const f16_t*)emb,
                                   (const f16_t*)pemb, ids, pos, x, st, M, d, (f16_t*)x16, V); break;
-    case kF32: hipLaunchKernelGGL(embed_kernel<float>, dim3(M), dim3(256), 0, s, (const float*)emb,
+    case kF32: WCB_LAUNCH(embed_kernel<float>, dim3(M), dim3(256), 0, s, (const float*)emb,
                                   (const float*)pemb, ids, pos, x, st, M, d, (float*)x16, V); break;
   }
 }
@@ -122,7 +122,7 @@ __global__ void fill_i32_kernel(int* p, int v, long n) {
 }
 void fill_i32(int* p, int v, long n, hipStream_t s) {
   const int grid = (int)min((n + 255) / 256, 1024L);
-  hipLaunchKernelGGL(fill_i32_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, p, v, n);
+  WCB_LAUNCH(fill_i32_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, p, v, n);
 }
 
 __global__ __launch_bounds__(64) void stamp_reduce_kernel(unsigned long long* slots, long n, unsigned long long* acc) {
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(64) void stamp_reduce_kernel(unsigned long long* sl
   if (threadIdx.x == 0 && used) { atomicAdd(acc, ticks); atomicAdd(acc + 1, used); }
 }
 void stamp_reduce(unsigned long long* slots, long n, unsigned long long* acc, hipStream_t s) {
-  hipLaunchKernelGGL(stamp_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, slots, n, acc);
+  WCB_LAUNCH(stamp_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, slots, n, acc);
 }
 
 }  // namespace wcb

@@ -124,7 +124,7 @@ __global__ void advance_forced_kernel(int* next_ids, const int* forced, int M, i
   if (threadIdx.x == 0) *pos = p + 1;
 }
 void advance_forced(int* next_ids, const int* forced, int M, int ld, int* pos, hipStream_t s) {
-  hipLaunchKernelGGL(advance_forced_kernel, dim3(1), dim3(256), 0, s, next_ids, forced, M, ld, pos);
+  WCB_LAUNCH(advance_forced_kernel, dim3(1), dim3(256), 0, s, next_ids, forced, M, ld, pos);
 }
 
 // next_ids[b] = src[b·ld + col]
@@ -132,7 +132,7 @@ __global__ void gather_col_kernel(int* dst, const int* src, int M, int ld, int c
   for (int b = threadIdx.x; b < M; b += blockDim.x) dst[b] = src[(long)b * ld + col];
 }
 void gather_col(int* dst, const int* src, int M, int ld, int col, hipStream_t s) {
-  hipLaunchKernelGGL(gather_col_kernel, dim3(1), dim3(256), 0, s, dst, src, M, ld, col);
+  WCB_LAUNCH(gather_col_kernel, dim3(1), dim3(256), 0, s, dst, src, M, ld, col);
 }
 
 struct IntChunk { int n; int v[256]; };
@@ -144,17 +144,17 @@ void write_i32(int* dst, const int* host_src, int n, hipStream_t s) {
     IntChunk c;
     c.n = n - o < 256 ? n - o : 256;
     for (int i = 0; i < c.n; ++i) c.v[i] = host_src[o + i];
-    hipLaunchKernelGGL(write_i32_kernel, dim3(1), dim3(256), 0, s, dst + o, c);
+    WCB_LAUNCH(write_i32_kernel, dim3(1), dim3(256), 0, s, dst + o, c);
   }
 }
 
 void select_finalize(const SelectArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(select_finalize_kernel, dim3(a.M), dim3(64), 0, s, a);
+  WCB_LAUNCH(select_finalize_kernel, dim3(a.M), dim3(64), 0, s, a);
 }
 
 void select_greedy(const SelectArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(select_partial_kernel, dim3(a.nchunk, a.M), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(select_finalize_kernel, dim3(a.M), dim3(64), 0, s, a);
+  WCB_LAUNCH(select_partial_kernel, dim3(a.nchunk, a.M), dim3(256), 0, s, a);
+  WCB_LAUNCH(select_finalize_kernel, dim3(a.M), dim3(64), 0, s, a);
 }
 
 }  // namespace wcb

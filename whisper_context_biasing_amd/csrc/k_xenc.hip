@@ -454,17 +454,17 @@ static void launch_xenc(const XencArgs& a, hipStream_t s) {
     }
     if (a.variant == 3) {
       constexpr int kThreads = XregCfg<D, 8>::NW * 64, kLds = XregCfg<D, 8>::LDS;
-      hipLaunchKernelGGL((attn_xenc_reg_kernel<T, D, 2, 8>), dim3(a.nsplit, a.rows), dim3(kThreads), kLds, s, a);
+      WCB_LAUNCH((attn_xenc_reg_kernel<T, D, 2, 8>), dim3(a.nsplit, a.rows), dim3(kThreads), kLds, s, a);
       return;
     }
   }
   if (a.variant == 0)
-    hipLaunchKernelGGL((attn_xenc_kernel<T, D>), dim3(a.nsplit, a.rows), dim3(kXencNW * 64), XencCfg<D>::LDS, s, a);
+    WCB_LAUNCH((attn_xenc_kernel<T, D>), dim3(a.nsplit, a.rows), dim3(kXencNW * 64), XencCfg<D>::LDS, s, a);
   else if (a.variant == 2)
-    hipLaunchKernelGGL((attn_xenc_reg_kernel<T, D, 3>), dim3(a.nsplit, a.rows), dim3(XregCfg<D>::NW * 64),
+    WCB_LAUNCH((attn_xenc_reg_kernel<T, D, 3>), dim3(a.nsplit, a.rows), dim3(XregCfg<D>::NW * 64),
                        XregCfg<D>::LDS, s, a);
   else
-    hipLaunchKernelGGL((attn_xenc_reg_kernel<T, D, 2>), dim3(a.nsplit, a.rows), dim3(XregCfg<D>::NW * 64),
+    WCB_LAUNCH((attn_xenc_reg_kernel<T, D, 2>), dim3(a.nsplit, a.rows), dim3(XregCfg<D>::NW * 64),
                        XregCfg<D>::LDS, s, a);
 }
 
@@ -490,7 +490,7 @@ void xenc_attention(DType t, const XencArgs& a, hipStream_t s) {
 template <typename T>
 static void launch_merge_t(const XencArgs& a, void* u, long ldu, hipStream_t s) {
   const dim3 grid(a.H, a.rows);
-#define WCB_XC(DD) case DD: hipLaunchKernelGGL((xenc_merge_kernel<T, DD>), grid, dim3(256), 0, s, a, (T*)u, ldu); break;
+#define WCB_XC(DD) case DD: WCB_LAUNCH((xenc_merge_kernel<T, DD>), grid, dim3(256), 0, s, a, (T*)u, ldu); break;
   switch (a.D) { WCB_XC(64) WCB_XC(128) WCB_XC(256) WCB_XC(384) WCB_XC(512) WCB_XC(768) WCB_XC(1024) default: break; }
 #undef WCB_XC
 }

@@ -1,9 +1,37 @@
 // Host-side launch interface of the libwcb device kernels (internal; the public C-ABI is include/wcb.h).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 namespace wcb {
+
+// Profiling pass only: while `start`/`stop` are set (runtime.cpp, wcb_handle::timed), every launch in
+// the scope goes through hipExtLaunchKernel with the event pair attached to the dispatch itself, so the
+// pair carries the kernel's own begin/end timestamps (the same source rocprofv3's kernel trace reads),
+// not an enqueue-to-completion interval. `start` marks the first launch of the scope, `stop` the last.
+struct LaunchTimer {
+  hipEvent_t start = nullptr, stop = nullptr;
+  int n = 0;
+  const void* fn = nullptr;   // first kernel of the scope and its grid in threads (rocprofv3's Grid_Size)
+  long grid = 0;
+};
+inline thread_local LaunchTimer g_launch_timer;
+
+#define WCB_LAUNCH(K, G, B, SH, S, ...)                                                              \
+  do {                                                                                               \
+    ::wcb::LaunchTimer& lt_ = ::wcb::g_launch_timer;                                                 \
+    if (lt_.stop) {                                                                                  \
+      if (!lt_.n) {                                                                                  \
+        lt_.fn = reinterpret_cast<const void*>(K);                                                   \
+        lt_.grid = (long)dim3(G).x * dim3(B).x;                                                      \
+      }                                                                                              \
+      hipExtLaunchKernelGGL(K, G, B, SH, S, lt_.n ? nullptr : lt_.start, lt_.stop, 0, __VA_ARGS__);  \
+      ++lt_.n;                                                                                       \
+    } else {                                                                                         \
+      hipLaunchKernelGGL(K, G, B, SH, S, __VA_ARGS__);                                               \
+    }                                                                                                \
+  } while (0)
 
 enum DType : int { kBF16 = 0, kF16 = 1, kF32 = 2 };
 

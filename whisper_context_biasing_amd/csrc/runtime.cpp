@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cxxabi.h>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -111,6 +112,8 @@ struct ProfEntry {
   std::string name;
   int64_t launches = 0;
   double ms = 0, flops = 0, bytes = 0;
+  const void* fn = nullptr;   // kernel of the class's first launch and its grid in threads
+  long grid = 0;
 };
 
 }  // namespace
@@ -269,12 +272,39 @@ struct wcb_handle {
     if (!prof) { f(); return; }
     const int id = prof_id(name);
     hipEvent_t a = get_ev(), b = get_ev();
+    g_launch_timer = LaunchTimer{a, b, 0};   // kernel begin/end timestamps (kernels.h, WCB_LAUNCH)
+    try {
+      f();
+    } catch (...) {
+      g_launch_timer = LaunchTimer{};
+      throw;
+    }
+    const int n = g_launch_timer.n;
+    if (n && !prof_e[id].fn) {
+      prof_e[id].fn = g_launch_timer.fn;
+      prof_e[id].grid = g_launch_timer.grid;
+    }
+    g_launch_timer = LaunchTimer{};
+    if (n == 0) {   // nothing launched (copies / memsets only): a zero-width interval
+      HIPCHK(hipEventRecord(a, st));
+      HIPCHK(hipEventRecord(b, st));
+    }
+    prof_e[id].launches += 1;
+    prof_e[id].flops += flops;
+    prof_e[id].bytes += bytes;
+    prof_pending.push_back({id, {a, b}});
+  }
+  // an enclosing interval (e.g. the whole decode loop) from plain stream events: enqueue-to-completion,
+  // used for totals only, never for a per-launch duration
+  template <typename F>
+  void timed_wall(const char* name, hipStream_t st, F&& f) {
+    if (!prof) { f(); return; }
+    const int id = prof_id(name);
+    hipEvent_t a = get_ev(), b = get_ev();
     HIPCHK(hipEventRecord(a, st));
     f();
     HIPCHK(hipEventRecord(b, st));
     prof_e[id].launches += 1;
-    prof_e[id].flops += flops;
-    prof_e[id].bytes += bytes;
     prof_pending.push_back({id, {a, b}});
   }
   void prof_collect() {
@@ -675,6 +705,19 @@ GemmArgs drow(const void* A, long lda, const void* W, int M, int N, int K, void*
   return g;
 }
 
+// algorithmic bytes of a decode-step GEMM: the weights once, the A rows, the written C rows
+double gemm_bytes(const wcb_handle* h, const GemmArgs& g) {
+  const double e = esize(h->d.dtype);
+  const double a_bytes = g.ln_w && !g.ln_a16 ? 4.0 : e;
+  const double c_bytes = g.out_f32 ? 4.0 : e;
+  return (double)g.N * g.K * e + (double)g.M * g.K * a_bytes + (double)g.M * g.N * c_bytes;
+}
+// one decode-step GEMM launch; timed per class only in the eager profiling pass (events cannot
+// bracket a node of a replayed graph)
+void dgemm(wcb_handle* h, const char* cls, const GemmArgs& g, hipStream_t st) {
+  h->timed(cls, 2.0 * g.M * g.N * g.K, gemm_bytes(h, g), st, [&] { gemm(h->dt, g, st); });
+}
+
 void run_gemm(wcb_handle* h, const char* cls, const GemmArgs& g) {
   h->timed(cls, 2.0 * g.M * g.N * g.K, 0.0, h->he, [&] { gemm(h->dt, g, h->he); });
 }
@@ -693,14 +736,14 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
     g.a_Mb = kFrames; g.a_strideB = xt_stride;
     g.c_Mb = kFrames; g.c_strideB = hb_stride;
     g.bias = h->conv1_b; g.act = 1;
-    run_gemm(h, "enc_gemm", g);
+    run_gemm(h, "enc_conv1", g);
   }
   {  // conv2 (stride 2) + GELU + positions → x (f32 residual stream)
     GemmArgs g = rowgemm(h->hbuf.p, 2L * d, h->conv2_w, (int)M, d, 3 * d, h->x.p, d);
     g.a_Mb = S; g.a_strideB = hb_stride;
     g.c_Mb = S; g.c_strideB = (long)S * d;   // c_Mb also indexes the position table
     g.bias = h->conv2_b; g.act = 1; g.addrow = h->enc_pos; g.out_f32 = 1;
-    run_gemm(h, "enc_gemm", g);
+    run_gemm(h, "enc_conv2", g);
   }
   const int nl = h->dbg_enc_layers >= 0 ? std::min(h->dbg_enc_layers, h->d.n_layers) : h->d.n_layers;
   for (int l = 0; l < nl; ++l) {
@@ -708,7 +751,7 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
     h->timed("layernorm", 0, M * d * (4.0 + e), h->he, [&] { layernorm(h->dt, h->x.as<float>(), w.ln1_w, w.ln1_b, h->h.p, (int)M, d, h->he); });
     GemmArgs q = rowgemm(h->h.p, d, w.qkv_w, (int)M, 3 * d, d, h->qkv.p, 3 * d);
     q.bias = w.qkv_b;
-    run_gemm(h, "enc_gemm", q);
+    run_gemm(h, "enc_qkv", q);
     AttnArgs a;
     a.q = h->qkv.p; a.ldq = 3 * d; a.q_Sb = S; a.Sq = S;
     a.k = (char*)h->qkv.p + d * e; a.v = (char*)h->qkv.p + 2 * d * e;
@@ -719,15 +762,15 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
     });
     GemmArgs o = rowgemm(h->att.p, d, w.o_w, (int)M, d, d, h->x.p, d);
     o.bias = w.o_b; o.resid = h->x.as<float>(); o.out_f32 = 1;
-    run_gemm(h, "enc_gemm", o);
+    run_gemm(h, "enc_out", o);
     h->timed("layernorm", 0, M * d * (4.0 + e), h->he, [&] { layernorm(h->dt, h->x.as<float>(), w.ln2_w, w.ln2_b, h->h.p, (int)M, d, h->he); });
     GemmArgs f1 = rowgemm(h->h.p, d, w.fc1_w, (int)M, h->d.ffn, d, h->ffn.p, h->d.ffn);
     f1.bias = w.fc1_b; f1.act = 1;
-    run_gemm(h, "enc_gemm", f1);
+    run_gemm(h, "enc_fc1", f1);
     GemmArgs f2 = rowgemm(h->ffn.p, h->d.ffn, w.fc2_w, (int)M, d, h->d.ffn, h->x.p, d);
     f2.bias = w.fc2_b; f2.resid = h->x.as<float>(); f2.out_f32 = 1;
     if (h->dt == kF16) f2.clamp = 65504.f - 1000.f;   // fp16 layer-output clamp (large-v3 fp16 config)
-    run_gemm(h, "enc_gemm", f2);
+    run_gemm(h, "enc_fc2", f2);
   }
   void* dst = enc_out ? enc_out : h->encout.p;
   h->timed("layernorm", 0, M * d * (4.0 + e), h->he, [&] { layernorm(h->dt, h->x.as<float>(), h->enc_ln_w, h->enc_ln_b, dst, (int)M, d, h->he); });
@@ -802,6 +845,7 @@ struct StepCfg {
   const int* forced; int forced_ld;    // advance_forced source when !select
   int clips = 0, nb = 1;               // encoder outputs (0: B) and decoder rows per encoder output
   int xmode = 1;                       // cross-attention formulation of this call (wcb_handle::xmode)
+  int host_pos = -1;                   // decoder position of this step when known on the host (eager)
   const int* phys = nullptr;           // beam search: cache row of every key position [B][T]
   const BeamArgs* beam = nullptr;      // beam search selection (replaces the greedy select)
 };
@@ -834,7 +878,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     GemmArgs q = drow(x, d, w.qkv_w, nb, 3 * d, d, dq, d);   // LayerNorm fused (f32 A rows)
     q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nbk; q.ln_a16 = lna;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
-    gemm(h->dt, q, st_);
+    dgemm(h, "dec_qkv", q, st_);
     AttnArgs a;
     a.q = dq; a.ldq = d; a.q_Sb = 1; a.Sq = 1;
     const char* cache0 = (char*)D.kvself.p + l * cache_l * e;   // K/V rows addressed absolutely
@@ -842,10 +886,14 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     a.k_sb = (long)H * T * 64; a.k_sh = (long)T * 64; a.k_sk = 64;
     a.row0 = b0; a.phys = c.phys; a.phys_ld = T;
     a.o = datt; a.ldo = d; a.o_Sb = 1; a.B = nb; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1;
-    attention_decode(h->dt, a, st_);
+    {
+      const double t_keys = c.host_pos >= 0 ? c.host_pos + 1 : 0;   // keys this step (eager pass)
+      h->timed("dec_self_attn", 4.0 * nb * H * t_keys * 64, nb * H * t_keys * 128.0 * e, st_,
+               [&] { attention_decode(h->dt, a, st_); });
+    }
     GemmArgs o = drow(datt, d, w.o_w, nb, d, d, x, d);
     o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st_pub; o.st_nb = nbk; o.out16 = x16;
-    gemm(h->dt, o, st_);
+    dgemm(h, "dec_out", o, st_);
     if (c.xmode == 1) {
       // cross attention in encoder space: q'_h = W_k,hᵀ q_h (block-diagonal GEMM, K = 64), one pass
       // over the encoder output per layer for all heads, range combine + W_v,h + b_v
@@ -854,15 +902,15 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
         GemmArgs xq = drow(x, d, w.xqk_w, nb, H * d, d, dqp, (long)H * d);
         xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
         xq.bias = w.xqk_b;
-        gemm(h->dt, xq, st_);
+        dgemm(h, "dec_xq", xq, st_);
       } else {
         GemmArgs xq = drow(x, d, w.xq_w, nb, d, d, dq, d);
         xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
         xq.bias = w.xq_b;
-        gemm(h->dt, xq, st_);
+        dgemm(h, "dec_xq", xq, st_);
         GemmArgs kq = drow(dq, d, w.xkt_w, nb, H * d, 64, dqp, (long)H * d);
         kq.a_grp_n = d; kq.a_grp_off = 64;
-        gemm(h->dt, kq, st_);
+        dgemm(h, "dec_kq", kq, st_);
       }
       XencArgs xa;
       xa.enc = h->xkv2[c.buf].p; xa.enc_sb = (long)S * d;
@@ -876,18 +924,21 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
         xa.stamp.pos = pos;
         xa.stamp.stride = L * wcb_handle::kMaxSub; xa.stamp.idx = l * wcb_handle::kMaxSub + chain;
       }
-      xenc_attention(h->dt, xa, st_);
+      // algorithmic bytes: every distinct clip's encoder output once (beams of a clip share it)
+      h->timed("dec_xattn", 4.0 * nb * H * (double)S * d, (double)nb / c.nb * S * d * e, st_,
+               [&] { xenc_attention(h->dt, xa, st_); });
       char* du = (char*)D.du.p + (size_t)b0 * H * d * e;
-      xenc_merge(h->dt, xa, du, (long)H * d, st_);
+      h->timed("dec_xmerge", 0, (double)nb * H * d * (h->xenc_split * 4.0 + e), st_,
+               [&] { xenc_merge(h->dt, xa, du, (long)H * d, st_); });
       GemmArgs vg = drow(du, (long)H * d, w.xv_w, nb, d, d, datt, d);   // o_h = W_v,h u_h + b_v,h
       vg.a_grp_n = 64; vg.a_grp_off = d; vg.bias = w.xv_b;
-      gemm(h->dt, vg, st_);
+      dgemm(h, "dec_vg", vg, st_);
     } else {
       // cross attention over the precomputed encoder K/V
       GemmArgs xq = drow(x, d, w.xq_w, nb, d, d, dq, d);
       xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
       xq.bias = w.xq_b;
-      gemm(h->dt, xq, st_);
+      dgemm(h, "dec_xq", xq, st_);
       AttnArgs xa;
       const char* xkv = (const char*)h->xkv2[c.buf].p + l * xkv_l * e;
       xa.q = dq; xa.ldq = d; xa.q_Sb = 1; xa.Sq = 1;
@@ -903,19 +954,20 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
         xa.stamp.pos = pos;
         xa.stamp.stride = L * wcb_handle::kMaxSub; xa.stamp.idx = l * wcb_handle::kMaxSub + chain;
       }
-      attention_decode(h->dt, xa, st_);
+      h->timed("dec_xattn", 4.0 * nb * H * (double)S * 64, (double)nb / c.nb * H * S * 128.0 * e, st_,
+               [&] { attention_decode(h->dt, xa, st_); });
     }
     GemmArgs xo = drow(datt, d, w.xo_w, nb, d, d, x, d);
     xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st_pub; xo.st_nb = nbk; xo.out16 = x16;
-    gemm(h->dt, xo, st_);
+    dgemm(h, "dec_xo", xo, st_);
     // MLP
     GemmArgs f1 = drow(x, d, w.fc1_w, nb, h->d.ffn, d, dffn, h->d.ffn);
     f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nbk; f1.ln_a16 = lna;
     f1.bias = w.fc1_b; f1.act = 1;
-    gemm(h->dt, f1, st_);
+    dgemm(h, "dec_fc1", f1, st_);
     GemmArgs f2 = drow(dffn, h->d.ffn, w.fc2_w, nb, d, h->d.ffn, x, d);
     f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st_pub; f2.st_nb = nbk; f2.out16 = x16;
-    gemm(h->dt, f2, st_);
+    dgemm(h, "dec_fc2", f2, st_);
   }
   if (c.lm_head) {
     GemmArgs lm = drow(x, d, h->tok_emb, nb, h->d.vocab, d, c.logits_out + (size_t)b0 * c.logits_ld, c.logits_ld);
@@ -927,7 +979,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       lm.sel_root_bits = c.bias->root_bits.as<uint32_t>(); lm.sel_lam = c.lam;
       lm.sel_eos = h->d.eos_token_id; lm.sel_step = ints + I_STEP; lm.sel_min_new = c.min_new;
     }
-    gemm(h->dt, lm, st_);
+    dgemm(h, "lm_head", lm, st_);
   }
 }
 
@@ -941,8 +993,10 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
   int* ints = D.ints.as<int>();
   int* pos = ints + I_POS;
   int* next_ids = ints + I_NEXT;
-  embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, D.dx.as<float>(), h->dec_gemm ? nullptr : D.dstats.as<float>(), B, d,
+  h->timed("dec_embed", 0, (double)B * d * (2.0 * esize(h->d.dtype) + 4), D.hs, [&] {
+    embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, D.dx.as<float>(), h->dec_gemm ? nullptr : D.dstats.as<float>(), B, d,
         D.hs, D.dx16.p, h->d.vocab);
+  });
   // rows per chain: the skinny projections split rows over grid.y, so a chain can take any number
   // of rows (WCB_GROUP_ROWS; more chains overlap latency, fewer re-read the weights less often)
   const int ngrp = (B + h->group_rows - 1) / h->group_rows;
@@ -963,7 +1017,7 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     for (int i = 0; i < ns; ++i) HIPCHK(hipStreamWaitEvent(D.hs, D.ev_join[i], 0));
   }
   if (c.select && c.beam) {
-    beam_select(*c.beam, D.hs);
+    h->timed("dec_select", 0, (double)B * h->d.vocab * 4, D.hs, [&] { beam_select(*c.beam, D.hs); });
   } else if (c.select) {
     SelectArgs s;
     s.logits = c.logits_out; s.ld = c.logits_ld; s.M = B; s.V = h->d.vocab;
@@ -978,7 +1032,7 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     s.part_val = D.part_val.as<float>(); s.part_idx = D.part_idx.as<int>(); s.nchunk = D.nchunk;
     s.all_done = ints + I_DONE;
     s.ticket = ints + I_TICKET; s.unfinished = ints + I_UNFIN;
-    select_finalize(s, D.hs);
+    h->timed("dec_select", 0, (double)B * D.nchunk * 8, D.hs, [&] { select_finalize(s, D.hs); });
   } else {
     advance_forced(next_ids, c.forced, B, c.forced_ld, pos, D.hs);
   }
@@ -1060,7 +1114,7 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
       encode_impl(h, mel, B, h->xkv2[buf].p);   // the decode reads the encoder output itself
     } else {
       encode_impl(h, mel, B, nullptr);
-      h->timed("xkv_gemm_total", 0, 0, h->he, [&] { cross_kv(h, B, buf, h->encout.p); });
+      h->timed_wall("xkv_gemm_total", h->he, [&] { cross_kv(h, B, buf, h->encout.p); });
     }
     HIPCHK(hipEventRecord(h->ev_xkv[buf], h->he));
     // ---- decode stream
@@ -1105,13 +1159,15 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     snprintf(key, sizeof key, "%d/%d/%d/%d/%llu/%a/%d/%d/%d/%d", B, nb, Tc, out_ld, (unsigned long long)bs->id,
              cfg->bias_boost, cfg->min_new_tokens, h->n_sub, (int)h->prof_stamps, P);
     const int max_new = cfg->max_new_tokens;
+    // per-launch HIP events (profiling bit 0) cannot bracket nodes of a replayed graph: eager launches
+    const bool use_graph = cfg->use_graph && !h->prof;
     // The decode step replays as a hipGraph; steps_per_graph steps are captured into one graph so the
     // per-replay gap is paid once per chunk (every position-dependent value is read on the device, so
     // a multi-step graph is the single-step graph unrolled). Natural-EOS mode polls the device
     // "all finished" flag once per chunk.
     const int chunk = h->steps_per_graph;
     int done = 0, steps = 0;
-    if (cfg->use_graph && (!D.gexec || D.gkey != key)) {
+    if (use_graph && (!D.gexec || D.gkey != key)) {
       if (D.gexec) { (void)hipGraphExecDestroy(D.gexec); D.gexec = nullptr; }
       if (D.gexec_k) { (void)hipGraphExecDestroy(D.gexec_k); D.gexec_k = nullptr; }
       for (int k : {1, chunk}) {
@@ -1125,15 +1181,19 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
       }
       D.gkey = key;
     }
-    h->timed("decode_loop", 0, 0, D.hs, [&] {
+    h->timed_wall("decode_loop", D.hs, [&] {
       while (steps < max_new) {
         const int n = std::min(chunk, max_new - steps);
-        if (cfg->use_graph && n == chunk && D.gexec_k) {
+        if (use_graph && n == chunk && D.gexec_k) {
           HIPCHK(hipGraphLaunch(D.gexec_k, D.hs));
         } else {
           for (int i = 0; i < n; ++i) {
-            if (cfg->use_graph) HIPCHK(hipGraphLaunch(D.gexec, D.hs));
-            else decode_step(h, sc);
+            if (use_graph) {
+              HIPCHK(hipGraphLaunch(D.gexec, D.hs));
+            } else {
+              sc.host_pos = P - 1 + steps + i;
+              decode_step(h, sc);
+            }
           }
         }
         steps += n;
@@ -1395,6 +1455,26 @@ int wcb_profile_read(wcb_handle* h, int n, char (*names)[32], int64_t* launches,
     count = (int)h->prof_e.size();
   });
   return rc == WCB_OK ? count : rc;
+}
+
+int wcb_profile_kernel(wcb_handle* h, int i, char* name, int cap, int64_t* grid) {
+  return guarded(h, [&] {
+    REQUIRE(h && name && cap > 0, "bad argument");
+    REQUIRE(i >= 0 && i < (int)h->prof_e.size(), "profile entry out of range");
+    const ProfEntry& e = h->prof_e[i];
+    std::string nm;
+    if (e.fn) {
+      const char* raw = hipKernelNameRefByPtr(e.fn, nullptr);
+      if (raw) {
+        int st = 0;
+        char* dm = abi::__cxa_demangle(raw, nullptr, nullptr, &st);
+        nm = (st == 0 && dm) ? dm : raw;
+        free(dm);
+      }
+    }
+    snprintf(name, (size_t)cap, "%s", nm.c_str());
+    if (grid) *grid = e.grid;
+  });
 }
 
 // ------------------------------------------------------------------------------ kernel-level ops

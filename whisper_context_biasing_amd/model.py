@@ -381,7 +381,7 @@ class WhisperCB:
         _lib.check(self._lib.wcb_profile_enable(self._h, mode), self._h, "wcb_profile_enable")
 
     def profile_read(self) -> Dict[str, dict]:
-        n = 32
+        n = 64
         names = (C.c_char * 32 * n)()
         launches = (C.c_int64 * n)()
         ms = (C.c_double * n)()
@@ -392,5 +392,10 @@ class WhisperCB:
         out = {}
         for i in range(min(cnt, n)):
             nm = bytes(names[i]).split(b"\0", 1)[0].decode()
-            out[nm] = dict(launches=launches[i], ms=ms[i], flops=flops[i], bytes=byts[i])
+            kname = C.create_string_buffer(512)
+            grid = C.c_int64(0)
+            _lib.check(self._lib.wcb_profile_kernel(self._h, i, kname, 512, C.byref(grid)), self._h,
+                       "wcb_profile_kernel")
+            out[nm] = dict(launches=launches[i], ms=ms[i], flops=flops[i], bytes=byts[i],
+                           kernel=kname.value.decode(errors="replace"), grid=grid.value)
         return out
