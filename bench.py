@@ -61,13 +61,14 @@ def cpu_baseline(size: str, n_tokens: int, n_phr: int, boost: float, seed: int =
     import torch
     from oracle import whisper_torch as WT
     from whisper_context_biasing_amd.config import get_dims
-    from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list
+    from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list, synth_word_start
     from whisper_context_biasing_amd.weights import make_weights
     dims = get_dims(size)
     m = WT.TorchWhisper(dims, make_weights(dims, seed=seed))
     pcm = torch.from_numpy(synth_batch(clips))
     phrases = synth_bias_list(n_phr, eot=dims.eos_token_id)
-    kw = dict(max_length=n_tokens, min_new_tokens=n_tokens, bias=phrases, bias_boost=boost)
+    kw = dict(max_length=n_tokens, min_new_tokens=n_tokens, bias=phrases, bias_boost=boost,
+              word_start=synth_word_start(dims.eos_token_id, dims.vocab))
 
     def run(use_cache, n):
         t0 = time.perf_counter()
@@ -139,7 +140,7 @@ def main():
     import torch.distributed as dist
     from whisper_context_biasing_amd.config import get_dims
     from whisper_context_biasing_amd.model import WhisperCB
-    from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list
+    from whisper_context_biasing_amd.synth import runner_up_phrases, synth_batch, synth_bias_list, synth_word_start
     from whisper_context_biasing_amd.shard import broadcast_weights, max_over_ranks, shard_bounds
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -165,7 +166,18 @@ def main():
     B = args.batch
     lo, hi = shard_bounds(world * B, rank, world)                      # this rank's utterances
     pcm = torch.from_numpy(synth_batch(hi - lo, start=lo)).to(dev)     # resident in HBM before timing
-    phrases = synth_bias_list(args.bias_phrases, eot=dims.eos_token_id)
+    # bias list (untimed setup): matches start only at word-start tokens (synthetic half of the
+    # vocabulary, the role of BPE's leading-space tokens); one phrase per clip built from its own
+    # lam = 0 decode's runner-up continuation (so the boost has something to place and the biased-WER
+    # half of the metric is not vacuous), the rest of the list from the reference's bias-word pool
+    ws = synth_word_start(dims.eos_token_id, dims.vocab)
+    model.set_word_start(ws)
+    targets, placed = [], []
+    if args.boost > 0 and args.num_beams == 1:
+        _, placed, targets = runner_up_phrases(model, model.log_mel(pcm), args.new_tokens, args.boost, ws)
+    seen = {tuple(p) for p in placed}
+    pool = [p for p in synth_bias_list(args.bias_phrases, eot=dims.eos_token_id) if tuple(p) not in seen]
+    phrases = placed + pool[:max(0, args.bias_phrases - len(placed))]
     bias = model.bias_list(phrases)
     use_graph = not args.no_graph
 
@@ -279,10 +291,10 @@ def main():
         phases["family:enc_gemm"] = {"ms_per_step": fam(lambda k: k in ENC_GEMMS)}
         phases["family:dec_proj"] = {"ms_per_step": fam(lambda k: k in DEC_PROJ)}
 
-    # biased-WER half of the metric, as a plumbing check (random weights: no transcript to score
-    # against): the boosted decode of the last batch against a λ = 0 decode of the same clips, scored
-    # by the C++ host scorer with token ids as words (WER, and compute_bias_wer's tallies over the
-    # bias phrases), untimed
+    # biased-WER half of the metric (random weights: no transcript to score against): the boosted
+    # decode of the benchmark batch against its lam = 0 decode, scored by the C++ host scorer with
+    # token ids as words — WER, compute_bias_wer's tallies over the bias list, and the recall of the
+    # placed phrases (each clip's runner-up continuation, absent from its lam = 0 decode); untimed
     bias_plumb = None
     if rank == 0 and args.boost > 0:
         from whisper_context_biasing_amd.metrics import wer_counts
@@ -306,11 +318,23 @@ def main():
                                                    C.byref(d_), C.byref(t_)), None, "wcb_bias_counts")
             bd += d_.value
             bt += t_.value
+        has = lambda row, p: any(row[i:i + len(p)] == p for i in range(len(row) - len(p) + 1))
+        hit_b = sum(has(boosted[b], placed[i]) for i, (b, _) in enumerate(targets))
+        hit_p = sum(has(plain[b], placed[i]) for i, (b, _) in enumerate(targets))
+        at_b = sum(boosted[b][t:t + 2] == placed[i] for i, (b, t) in enumerate(targets))
+        at_p = sum(plain[b][t:t + 2] == placed[i] for i, (b, t) in enumerate(targets))
         bias_plumb = {"wer_boosted_vs_unboosted": round(100.0 * sum(err) / max(sum(words), 1), 3),
                       "bias_wer_unboosted_vs_boosted": round(100.0 * bd / bt, 3) if bt else 0.0,
                       "bias_phrase_tokens_in_boosted": bt,
-                      "note": "plumbing only (random weights): token ids as words; WER of the boosted decode "
-                              "against the λ=0 decode, bias-WER of the λ=0 decode against the boosted one"}
+                      "placed_phrases": len(placed),
+                      "placed_phrase_recall_boosted": round(hit_b / len(placed), 4) if placed else None,
+                      "placed_phrase_recall_unboosted": round(hit_p / len(placed), 4) if placed else None,
+                      "placed_at_target_step_boosted": round(at_b / len(placed), 4) if placed else None,
+                      "placed_at_target_step_unboosted": round(at_p / len(placed), 4) if placed else None,
+                      "note": "random weights: token ids as words; WER of the boosted decode against the "
+                              "lam=0 decode, bias-WER of the lam=0 decode against the boosted one over the "
+                              "whole bias list, recall of each clip's placed phrase (its lam=0 runner-up "
+                              "continuation) in that clip's decode"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -95,12 +95,17 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
                 void* enc_out, void* stream);
 
 /* bias list: n_phrases token sequences, phrase i = tokens[offsets[i] .. offsets[i+1]) (host
- * arrays). Built into an Aho-Corasick automaton on the device (boost semantics: k_select.hip).
+ * arrays), built into an Aho-Corasick automaton on the device. word_start (host, [vocab] bytes, or
+ * NULL = every token) marks the tokens a match may START at — for a BPE vocabulary the tokens that
+ * begin a word (leading space); tokenise phrases as they appear inside a transcript. Boost
+ * semantics (oracle/bias_ref.py, k_select.hip): each token scores +lam·n(s, v) where n counts the
+ * tokens the transition adds to the current match minus the dropped, unfinished ones (retraction);
+ * completed phrases keep their bonus.
  * Lifetime: an automaton belongs to the handle that created it; wcb_bias_destroy waits for that
  * handle's queued work and drops the decode graphs that captured it (serialise it with the handle's
  * other calls, like every call on a handle). It may outlive the handle (destroy it afterwards). */
 int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets, int n_phrases,
-                    wcb_bias** out);
+                    const uint8_t* word_start, wcb_bias** out);
 void wcb_bias_destroy(wcb_bias* b);
 int wcb_bias_num_states(const wcb_bias* b);
 
@@ -114,7 +119,7 @@ int wcb_profile_read(wcb_handle* h, int n, char (*names)[32], int64_t* launches,
                      double* flops, double* bytes);
 
 /* entry i of wcb_profile_read: the (demangled) kernel symbol of the class's first launch and its grid
- * in threads, as rocprofv3's kernel trace names them (Kernel_Name, Grid_Size_X); "" when the class
+ * in threads (x·y·z), as rocprofv3 names them (Kernel_Name; Grid_Size = Grid_Size_X·Y·Z); "" when the class
  * launched nothing or was stamped on the device */
 int wcb_profile_kernel(wcb_handle* h, int i, char* name, int cap, int64_t* grid);
 

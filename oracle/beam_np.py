@@ -69,7 +69,8 @@ def whisper_trim(ids: np.ndarray, eos: int, pad: int) -> np.ndarray:
 def generate_beam(om, mel=None, num_beams: int = 5, max_length: int = 225, enc=None,
                   min_new_tokens: int = 0, bias: Optional[Sequence[Sequence[int]]] = None,
                   bias_boost: float = 0.0, prefix: Optional[Sequence[int]] = None,
-                  length_penalty: float = 1.0, trim: bool = True, return_scores: bool = False):
+                  length_penalty: float = 1.0, trim: bool = True, return_scores: bool = False,
+                  word_start=None):
     """Beam search over `om` (oracle/whisper_np.OracleModel). Returns the best finished sequence of
     every utterance (new tokens only), Whisper-trimmed unless `trim=False` (then [B, W] with
     W = longest best sequence incl. its EOS, pad-filled — the C-ABI output)."""
@@ -82,7 +83,7 @@ def generate_beam(om, mel=None, num_beams: int = 5, max_length: int = 225, enc=N
     P = len(pre)
     n_ctx = om.w("model.decoder.embed_positions.weight").shape[0]
     Lt = min(P + int(max_length), n_ctx)
-    ac = AhoCorasick(bias or [])
+    ac = AhoCorasick(bias or [], word_start)
     lam = F32(bias_boost)
     # beams of one clip share its encoder state: cross-K/V once per clip, repeated per beam row
     xkv = [(np.repeat(k, nb, axis=0), np.repeat(v, nb, axis=0)) for k, v in om.cross_kv(enc)]
@@ -108,8 +109,7 @@ def generate_beam(om, mel=None, num_beams: int = 5, max_length: int = 225, enc=N
         logp = log_softmax_f32(logits)
         if lam != 0:
             for r in range(R):
-                for v in ac.boosted_tokens(int(states[r // nb, r % nb])):
-                    logp[r, v] = F32(logp[r, v] + lam)
+                logp[r] = ac.boost_row(logp[r], int(states[r // nb, r % nb]), lam)
         if cur - P < min_new_tokens:
             logp[:, om.eos] = -np.inf
         acc = (logp.reshape(B, nb, V) + run_sc[:, :, None]).astype(F32).reshape(B, nb * V)

@@ -257,7 +257,8 @@ class OracleModel:
     def generate(self, mel=None, max_length: int = 225, enc=None, min_new_tokens: int = 0,
                  bias: Optional[Sequence[Sequence[int]]] = None, bias_boost: float = 0.0,
                  prefix: Optional[Sequence[int]] = None, return_logits: bool = False,
-                 use_cache: bool = True, trim: bool = True, return_margins: bool = False):
+                 use_cache: bool = True, trim: bool = True, return_margins: bool = False,
+                 word_start=None):
         """Greedy decode with the reference's eval semantics:
         init = [decoder_start] ([tf] generation_whisper.py:1489,1591-1606); ≤ max_length new
         tokens (max_length+1 total incl. SOT, [tf] generation_whisper.py:1932-1940); fp32
@@ -265,8 +266,8 @@ class OracleModel:
         emit pad; stop when all rows finished ([tf] :2928-2936); output excludes SOT and is right-
         padded with pad ([tf] generation_whisper.py:936-943,1141-1144); with `trim` the trailing EOS
         and pads are dropped per row as Whisper does ([tf] generation_whisper.py:1063-1086).
-        `min_new_tokens` masks EOS (benchmark mode); `bias`/`bias_boost` apply
-        the A8 boost (oracle/bias_ref.py). `use_cache=False` recomputes the whole prefix every
+        `min_new_tokens` masks EOS (benchmark mode); `bias`/`bias_boost`/`word_start`
+        apply the A8 boost (oracle/bias_ref.py). `use_cache=False` recomputes the whole prefix every
         step exactly like `scripts/evaluation.py:178`. `return_margins` adds the per-step gap between
         the best and the second-best selection score (after boost and mask) of every row [B, steps]
         (inf for finished rows): the margin gate of the reduced-precision parity tests.
@@ -275,7 +276,7 @@ class OracleModel:
             enc = self.encode(mel)
         B = enc.shape[0]
         xkv = self.cross_kv(enc)
-        ac = AhoCorasick(bias or [])
+        ac = AhoCorasick(bias or [], word_start)
         lam = float(bias_boost)
         pre = list(prefix) if prefix else [self.start]
         seq = np.tile(np.asarray(pre, dtype=np.int64)[None], (B, 1))
@@ -301,10 +302,7 @@ class OracleModel:
                 if lam == 0.0 and mask_eos < 0:
                     row = logits_last[b]
                 else:
-                    row = logits_last[b].copy()
-                    if lam != 0.0:
-                        for v in ac.boosted_tokens(states[b]):
-                            row[v] = F32(row[v] + F32(lam))
+                    row = ac.boost_row(logits_last[b], states[b], lam) if lam != 0.0 else logits_last[b].copy()
                     if mask_eos >= 0:
                         row[mask_eos] = -np.inf
                 toks[b] = int(np.argmax(row))

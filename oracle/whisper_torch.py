@@ -131,7 +131,8 @@ class TorchWhisper:
     # ------------------------------------------------------------------------------ generate
     @torch.no_grad()
     def generate(self, mel: torch.Tensor, max_length: int = 225, min_new_tokens: int = 0, use_cache: bool = True,
-                 bias: Optional[Sequence[Sequence[int]]] = None, bias_boost: float = 0.0) -> np.ndarray:
+                 bias: Optional[Sequence[Sequence[int]]] = None, bias_boost: float = 0.0,
+                 word_start=None) -> np.ndarray:
         """Greedy decode with the reference's eval semantics (oracle/whisper_np.py generate): start from
         [decoder_start], argmax of fp32 logits (lowest index on ties), finished rows emit pad, stop when
         every row finished or max_length new tokens. `use_cache=False` = scripts/evaluation.py:178: every
@@ -139,7 +140,7 @@ class TorchWhisper:
         dims = self.dims
         enc = self.encode(mel)
         B = enc.shape[0]
-        ac = AhoCorasick(bias or [])
+        ac = AhoCorasick(bias or [], word_start)
         lam = float(bias_boost)
         seq = torch.full((B, 1), dims.decoder_start_token_id, dtype=torch.long)
         cache = {} if use_cache else None
@@ -151,10 +152,9 @@ class TorchWhisper:
         out = []
         while True:
             row = logits.clone()
-            if lam != 0.0:
+            if lam != 0.0:   # bonus lam * n(state, v), oracle/bias_ref.py
                 for b in range(B):
-                    for v in ac.boosted_tokens(states[b]):
-                        row[b, v] += lam
+                    row[b] += torch.from_numpy(np.float32(lam) * ac.unit_vector(states[b], row.shape[1]).astype(np.float32))
             if len(out) < min_new_tokens:
                 row[:, dims.eos_token_id] = float("-inf")
             tok = row.argmax(dim=-1)

@@ -20,7 +20,7 @@ from oracle import whisper_np as W  # noqa: E402
 from oracle.beam_np import generate_beam  # noqa: E402
 from whisper_context_biasing_amd.config import get_dims  # noqa: E402
 from whisper_context_biasing_amd.model import WhisperCB  # noqa: E402
-from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list  # noqa: E402
+from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list, synth_word_start  # noqa: E402
 from whisper_context_biasing_amd.weights import make_weights  # noqa: E402
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -76,18 +76,24 @@ def test_beam5_f32_matches_reference_golden(size):
         assert ids.shape == ref.shape and np.array_equal(ids, ref), (use_graph, ids, ref)
 
 
-@pytest.mark.parametrize("nb,lam,min_new,n_phr", [(2, 0.0, 0, 0), (3, 2.0, 0, 200), (5, 2.0, 12, 1000),
-                                                  (8, 8.0, 0, 50)])
-def test_beam_boost_matches_oracle_f32(nb, lam, min_new, n_phr):
+@pytest.mark.parametrize("nb,lam,min_new,n_phr,gate", [(2, 0.0, 0, 0, False), (3, 2.0, 0, 200, False),
+                                                       (5, 2.0, 12, 1000, False), (8, 8.0, 0, 50, False),
+                                                       (5, 2.0, 12, 1000, True), (4, 4.0, 0, 200, True)])
+def test_beam_boost_matches_oracle_f32(nb, lam, min_new, n_phr, gate):
+    """Beam scores carry the per-step bonus including the retraction of abandoned matches (and, with
+    `gate`, word-start gated starts): token-exact against the oracle's beam search."""
     dims, om, mel, enc = case("micro", 0, "diverse", 2)
     m = model("micro", 0, "diverse", "f32")
+    ws = synth_word_start(dims.eos_token_id, dims.vocab) if gate else None
+    m.set_word_start(ws)
     plain = om.generate(mel, enc=enc, max_length=24, min_new_tokens=24)
     phrases = synth_bias_list(n_phr, eot=dims.eos_token_id) if n_phr else []
     phrases = phrases + [list(map(int, plain[0, 2:5])), list(map(int, plain[1, 1:3])) + [7, 8]]
     ids = m.generate(torch.from_numpy(mel), max_length=24, num_beams=nb, bias_list=phrases, bias_boost=lam,
                      min_new_tokens=min_new).cpu().numpy()
+    m.set_word_start(None)
     ref = generate_beam(om, enc=enc, num_beams=nb, max_length=24, bias=phrases, bias_boost=lam,
-                        min_new_tokens=min_new)
+                        min_new_tokens=min_new, word_start=ws)
     assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
 
 

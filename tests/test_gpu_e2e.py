@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 from oracle import whisper_np as W  # noqa: E402
 from whisper_context_biasing_amd.config import get_dims  # noqa: E402
 from whisper_context_biasing_amd.model import WhisperCB  # noqa: E402
-from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list  # noqa: E402
+from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list, synth_word_start  # noqa: E402
 from whisper_context_biasing_amd.weights import make_weights  # noqa: E402
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -102,17 +102,23 @@ def test_natural_eos_and_padding():
     assert np.array_equal(ids, ref)
 
 
-@pytest.mark.parametrize("n_phr,lam", [(50, 0.0), (50, 2.0), (1000, 2.0), (200, 8.0)])
-def test_bias_boost_matches_oracle_f32(n_phr, lam):
+@pytest.mark.parametrize("n_phr,lam,gate", [(50, 0.0, False), (50, 2.0, False), (1000, 2.0, False), (200, 8.0, False),
+                                            (1000, 2.0, True), (200, 8.0, True)])
+def test_bias_boost_matches_oracle_f32(n_phr, lam, gate):
+    """The boost of oracle/bias_ref.py (retraction of unfinished matches; with `gate`, matches start only
+    at the synthetic word-start tokens), token-exact in f32 mode."""
     dims, sd, om, mel, enc = case("micro", 0, "diverse", 2)
     m = model("micro", 0, "diverse", "f32")
+    ws = synth_word_start(dims.eos_token_id, dims.vocab) if gate else None
+    m.set_word_start(ws)
     phrases = synth_bias_list(n_phr, eot=dims.eos_token_id)
     # make phrases reachable: include prefixes of the plain greedy output as phrases
     plain = om.generate(mel, enc=enc, max_length=24)
     phrases = phrases + [list(map(int, plain[0, 2:5])), list(map(int, plain[1, 1:3])) + [7, 8]]
     ids = m.generate(torch.from_numpy(mel), max_length=24, bias_list=phrases, bias_boost=lam,
                      min_new_tokens=24).cpu().numpy()
-    ref = om.generate(mel, enc=enc, max_length=24, bias=phrases, bias_boost=lam, min_new_tokens=24)
+    m.set_word_start(None)
+    ref = om.generate(mel, enc=enc, max_length=24, bias=phrases, bias_boost=lam, min_new_tokens=24, word_start=ws)
     assert np.array_equal(ids, ref), (ids, ref)
     if lam == 0.0:
         plain24 = m.generate(torch.from_numpy(mel), max_length=24, min_new_tokens=24).cpu().numpy()

@@ -15,7 +15,8 @@ def main():
     roof = json.loads(line)["roofline"]
     g = collections.defaultdict(list)
     for r in csv.DictReader(open(sys.argv[2])):
-        g[f'{r["Kernel_Name"].split("(")[0]}|{r["Grid_Size_X"]}'].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        g[f'{r["Kernel_Name"].split("(")[0]}|{grid}'].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     top = max(g, key=lambda k: sum(g[k]))
     key = f'{roof["kernel"]}|{roof["grid"]}'
     dur = g.get(key)

@@ -27,7 +27,7 @@ def load(pass_dir: str, counter: str):
                 continue
             key = (f, r.get("Dispatch_Id") or r.get("Correlation_Id"))
             per[key] += float(r["Counter_Value"])
-            meta[key] = f'{r["Kernel_Name"].split("(")[0]}|{int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)}'
+            meta[key] = f'{r["Kernel_Name"].split("(")[0]}|{int(r.get("Grid_Size") or 0)}'
     out = collections.defaultdict(list)
     for k, v in per.items():
         out[meta[k]].append(v)

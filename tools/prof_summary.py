@@ -7,7 +7,8 @@ path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_trace.c
 rows = list(csv.DictReader(open(path)))
 g = collections.defaultdict(list)
 for r in rows:
-    k = (r["Kernel_Name"].split("(")[0][:60], r["Grid_Size_X"], r["Workgroup_Size_X"])
+    grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])   # total threads
+    k = (r["Kernel_Name"].split("(")[0][:60], grid, r["Workgroup_Size_X"])
     g[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 tot = sum(sum(v) for v in g.values())
 for k, v in sorted(g.items(), key=lambda kv: -sum(kv[1]))[:int(sys.argv[2]) if len(sys.argv) > 2 else 30]:

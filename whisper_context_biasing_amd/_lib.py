@@ -42,7 +42,7 @@ SIGNATURES = {
                                C.POINTER(C.c_int32), _P]),
     "wcb_synchronize": (C.c_int, [_P]),
     "wcb_forward": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, _P, _P, _P]),
-    "wcb_bias_create": (C.c_int, [_P, _P, _P, C.c_int, C.POINTER(_P)]),
+    "wcb_bias_create": (C.c_int, [_P, _P, _P, C.c_int, _P, C.POINTER(_P)]),
     "wcb_bias_destroy": (None, [_P]),
     "wcb_bias_num_states": (C.c_int, [_P]),
     "wcb_debug_copy": (C.c_int, [_P, C.c_char_p, _P, C.c_int64, C.c_int]),

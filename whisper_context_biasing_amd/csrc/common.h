@@ -46,6 +46,10 @@ template <> struct DT<float> {
   WCB_DEV static float fromf(float f) { return f; }
 };
 
+// A8 bias boost (oracle/bias_ref.py): x + lam·units as one f32 product and one f32 add, never a
+// fused multiply-add, so every kernel rounds exactly like the oracle
+WCB_DEV float bias_bonus(float x, float lam, int units) { return __fadd_rn(x, __fmul_rn(lam, (float)units)); }
+
 WCB_DEV f32x4 mma16(const s16x8& a, const s16x8& b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }

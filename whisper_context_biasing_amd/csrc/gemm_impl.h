@@ -629,7 +629,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
       int xi = 0x7fffffff;
       if (valid) {
         x = v;
-        if (g.sel_lam != 0.f && ((g.sel_root_bits[nn >> 5] >> (nn & 31)) & 1u)) x += g.sel_lam;
+        if (g.sel_lam != 0.f)
+          x = bias_bonus(x, g.sel_lam, g.sel_rowbase[row] + (int)((g.sel_root_bits[nn >> 5] >> (nn & 31)) & 1u));
         if (mask_eos && nn == g.sel_eos) x = -INFINITY;
         xi = nn;
       }
@@ -730,6 +731,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
     }
   }
   float pf_bias[EP], pf_res[EP];   // epilogue operands of this thread's outputs (single-tile launches)
+  int pf_rb[EP];                   // bias-boost base units of this thread's rows (LM head)
 #pragma unroll
   for (int it = 0; it < EP; ++it) {
     const int o = it * NT + tid;
@@ -737,6 +739,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
     const bool ok = !P && o < R * 16 && row < g.M && nn < g.N;
     pf_bias[it] = (ok && g.bias) ? g.bias[nn] : 0.f;
     pf_res[it] = (ok && g.resid && !(g.mode == 2 && nn >= g.n_split)) ? g.resid[c_row(g, row) + nn] : 0.f;
+    pf_rb[it] = (g.sel_val && g.sel_lam != 0.f && o < R * 16 && row < g.M) ? g.sel_rowbase[row] : 0;
   }
   __builtin_amdgcn_sched_barrier(0);
   // ---------------- LayerNorm of the A rows: statistics from the loaded values, parameters via LDS
@@ -869,7 +872,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
         int xi = 0x7fffffff;
         if (valid) {
           x = v;
-          if (g.sel_lam != 0.f && ((g.sel_root_bits[nn >> 5] >> (nn & 31)) & 1u)) x += g.sel_lam;
+          if (g.sel_lam != 0.f)
+            x = bias_bonus(x, g.sel_lam, pf_rb[it] + (int)((g.sel_root_bits[nn >> 5] >> (nn & 31)) & 1u));
           if (mask_eos && nn == g.sel_eos) x = -INFINITY;
           xi = nn;
         }

@@ -4,7 +4,9 @@
 //
 // Rows r = b·nb + i (utterance b, running beam i). Per decode step:
 //   beam_topk_kernel  one workgroup per row over the f32 logits row: log_softmax (max, Σexp), the
-//                     boost (root bitmap ∪ trans(state) in an LDS bitmap) and EOS mask, plus the
+//                     boost (lam·(k - d + root bit) on the vocabulary, the exact lam·n(s, v) on the
+//                     tokens of trans(state), which an LDS bitmap excludes from the vocabulary
+//                     pass; oracle/bias_ref.py) and EOS mask, plus the
 //                     beam's running score, then the row's top-K (K = 2·nb) by (score desc, token
 //                     asc). HBM-bound: 4·V bytes per row (the later passes hit L2).
 //   beam_step_kernel  one workgroup per utterance: the top-K of its nb·K row candidates (the global
@@ -75,6 +77,7 @@ __global__ __launch_bounds__(256) void beam_init_kernel(BeamArgs a) {
 __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
   if (*a.all_done) return;                    // frozen once the search has stopped
   __shared__ uint32_t bits[kBitWords];
+  __shared__ uint32_t tbits[kBitWords];       // tokens of trans(state): scored in their own pass
   __shared__ float red[4];
   __shared__ float cv[256][kTopK + 1];
   __shared__ int ci[256][kTopK + 1];
@@ -89,16 +92,20 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
   for (int v = tid; v < a.V; v += 256) s += expf(row[v] - m);
   const float lsum = logf(block_sum4(s, red));
   const bool boost = a.lam != 0.f;
+  const int st = a.state[r];
+  int rb = 0, sd = 0, sk = 0;
   if (boost) {
     const int nw = (a.V + 31) >> 5;
-    for (int k = tid; k < nw; k += 256) bits[k] = a.root_bits[k];
+    for (int k = tid; k < nw; k += 256) { bits[k] = a.root_bits[k]; tbits[k] = 0u; }
     __syncthreads();
-    const int st = a.state[r];
     for (int t = a.trans_off[st] + tid; t < a.trans_off[st + 1]; t += 256) {
       const int v = a.trans_tok[t];
-      atomicOr(&bits[v >> 5], 1u << (v & 31));
+      atomicOr(&tbits[v >> 5], 1u << (v & 31));
     }
     __syncthreads();
+    sd = a.st_depth[st];
+    sk = a.st_keep[st];
+    rb = sk - sd;
   }
   const bool mask_eos = *a.step < a.min_new;
   const float rsc = a.run_sc[r];
@@ -106,11 +113,7 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
   int li[kTopK];
 #pragma unroll
   for (int k = 0; k < kTopK; ++k) { lv[k] = -INFINITY; li[k] = 0x7fffffff; }
-  for (int v = tid; v < a.V; v += 256) {
-    float x = (row[v] - m) - lsum;                                    // log_softmax
-    if (boost && ((bits[v >> 5] >> (v & 31)) & 1u)) x = x + a.lam;    // bias boost processor
-    if (mask_eos && v == a.eos) x = -INFINITY;                         // MinNewTokens processor
-    x = x + rsc;                                                       // + running beam score
+  auto insert = [&](float x, int v) {
     if (beam_better(x, v, lv[kTopK - 1], li[kTopK - 1])) {
       float pv = x;
       int pi = v;
@@ -122,6 +125,24 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
           lv[k] = pv; li[k] = pi; pv = tv; pi = ti;
         }
       }
+    }
+  };
+  for (int v = tid; v < a.V; v += 256) {
+    float x = (row[v] - m) - lsum;                                     // log_softmax
+    if (boost) {                                                       // bias boost processor
+      if ((tbits[v >> 5] >> (v & 31)) & 1u) continue;                  // scored below
+      x = bias_bonus(x, a.lam, rb + (int)((bits[v >> 5] >> (v & 31)) & 1u));
+    }
+    if (mask_eos && v == a.eos) x = -INFINITY;                         // MinNewTokens processor
+    insert(x + rsc, v);                                                // + running beam score
+  }
+  if (boost) {   // trans(state): the exact n(s, v) = d' - d + min(k, d + 1 - d')
+    for (int t = a.trans_off[st] + tid; t < a.trans_off[st + 1]; t += 256) {
+      const int v = a.trans_tok[t];
+      const int d2 = a.st_depth[a.trans_dst[t]];
+      float x = bias_bonus((row[v] - m) - lsum, a.lam, d2 - sd + min(sk, sd + 1 - d2));
+      if (mask_eos && v == a.eos) x = -INFINITY;
+      insert(x + rsc, v);
     }
   }
 #pragma unroll

@@ -2,15 +2,18 @@
 //
 // Semantics (restating the greedy step of [tf] generation/utils.py:2894-2936 plus the build-defined
 // A8 boost, oracle/bias_ref.py):
-//   score[v] = logit[v] + lam * boosted(s, v)        boosted <=> AC-automaton delta(s, v) != root
+//   score[v] = logit[v] + lam * n(s, v)               (f32 product, f32 add: bias_bonus)
+//   n(s, v)  = d' - d + min(k, d + 1 - d')            d = depth(s), k = keep(s), d' = depth(delta(s, v))
 //   score[eos] = -inf while step < min_new_tokens     (MinNewTokens semantics, benchmark mode)
 //   tok = argmax(score), lowest index on ties (torch.argmax); finished rows emit pad;
 //   finished |= tok == eos; s <- delta(s, tok).       lam == 0 → plain greedy, bit-identical.
-// boosted(s, v) = root_child[v] >= 0  OR  v in trans(s), where trans(s) lists every token whose
-// transition from s lands deeper than depth 1 (CSR: trans_off/trans_tok/trans_dst, sorted by
-// token). The vocabulary-wide pass reads the logits once (HBM-bound, 4·V bytes per row) applying
-// the root bitmap; the per-row finalize scans only trans(s) (a handful of tokens) — valid because
-// lam >= 0 (checked on the host) so an unboosted value never beats its own boosted value.
+// delta(s, v) = trans(s) entry if v is listed (lands deeper than depth 1), else the root child
+// root_child[v] (only word-start tokens may start a match: the host leaves the others at -1), else
+// the root. So n = k - d for every token, + 1 on the root children (the root bitmap), and the exact
+// value on the few tokens of trans(s). The vocabulary-wide pass (or the LM-head epilogue) reads the
+// logits once applying lam·(rowbase + root bit), rowbase = k - d of the row's state; the per-row
+// finalize re-scores only trans(s) — exact because lam >= 0 (checked on the host) and n on a trans
+// token is never below the vocabulary-pass value, so an underestimated copy never wins.
 #include "common.h"
 #include "kernels.h"
 
@@ -24,11 +27,12 @@ __global__ __launch_bounds__(256) void select_partial_kernel(SelectArgs a) {
   const int v0 = c * chunk, v1 = min(a.V, v0 + chunk);
   const float* row = a.logits + (long)m * a.ld;
   const bool mask_eos = *a.step < a.min_new;
+  const int rb = a.rowbase[m];
   float bv = -INFINITY;
   int bi = 0x7fffffff;
   for (int v = v0 + threadIdx.x; v < v1; v += 256) {
     float x = row[v];
-    if (a.lam != 0.f && ((a.root_bits[v >> 5] >> (v & 31)) & 1u)) x += a.lam;
+    if (a.lam != 0.f) x = bias_bonus(x, a.lam, rb + (int)((a.root_bits[v >> 5] >> (v & 31)) & 1u));
     if (mask_eos && v == a.eos) x = -INFINITY;
     if (better(x, v, bv, bi)) { bv = x; bi = v; }
   }
@@ -69,10 +73,11 @@ __global__ __launch_bounds__(64) void select_finalize_kernel(SelectArgs a) {
   const int t0 = a.trans_off[s], t1 = a.trans_off[s + 1];
   if (a.lam != 0.f) {
     const float* row = a.logits + (long)m * a.ld;
+    const int d = a.st_depth[s], k = a.st_keep[s];
     for (int t = t0 + lane; t < t1; t += 64) {
       const int v = a.trans_tok[t];
-      if (a.root_child[v] >= 0) continue;     // already boosted in the vocabulary pass
-      float x = row[v] + a.lam;
+      const int d2 = a.st_depth[a.trans_dst[t]];
+      float x = bias_bonus(row[v], a.lam, d2 - d + min(k, d + 1 - d2));
       if (mask_eos && v == a.eos) x = -INFINITY;
       if (better(x, v, bv, bi)) { bv = x; bi = v; }
     }
@@ -96,6 +101,7 @@ __global__ __launch_bounds__(64) void select_finalize_kernel(SelectArgs a) {
   if (lane == 0) {
     if (dst < 0) dst = (tok >= 0 && tok < a.V && a.root_child[tok] >= 0) ? a.root_child[tok] : 0;
     a.state[m] = dst;
+    a.rowbase[m] = a.st_keep[dst] - a.st_depth[dst];
     a.next_ids[m] = tok;
     a.out_ids[(long)m * a.out_ld + step] = tok;
     const bool nf = fin || tok == a.eos;

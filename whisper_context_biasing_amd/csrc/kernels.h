@@ -13,7 +13,7 @@ namespace wcb {
 struct LaunchTimer {
   hipEvent_t start = nullptr, stop = nullptr;
   int n = 0;
-  const void* fn = nullptr;   // first kernel of the scope and its grid in threads (rocprofv3's Grid_Size)
+  const void* fn = nullptr;   // first kernel of the scope and its total grid in threads (rocprofv3)
   long grid = 0;
 };
 inline thread_local LaunchTimer g_launch_timer;
@@ -24,7 +24,8 @@ inline thread_local LaunchTimer g_launch_timer;
     if (lt_.stop) {                                                                                  \
       if (!lt_.n) {                                                                                  \
         lt_.fn = reinterpret_cast<const void*>(K);                                                   \
-        lt_.grid = (long)dim3(G).x * dim3(B).x;                                                      \
+        const dim3 g_ = dim3(G), b_ = dim3(B);                                                       \
+        lt_.grid = (long)g_.x * g_.y * g_.z * b_.x * b_.y * b_.z;                                    \
       }                                                                                              \
       hipExtLaunchKernelGGL(K, G, B, SH, S, lt_.n ? nullptr : lt_.start, lt_.stop, 0, __VA_ARGS__);  \
       ++lt_.n;                                                                                       \
@@ -61,6 +62,7 @@ struct GemmArgs {
   int st_nb = 0;                   // 16-column blocks per row (d / 16)
   float* sel_val = nullptr; int* sel_idx = nullptr;   // LM head: per-(row, workgroup) argmax partial
   const uint32_t* sel_root_bits = nullptr; float sel_lam = 0.f;
+  const int* sel_rowbase = nullptr;   // per row k - d of its bias state: bonus lam·(base + root bit)
   int sel_eos = -1; const int* sel_step = nullptr; int sel_min_new = 0;
   // grouped A (skinny path, block-diagonal weights): the A row of output column block n0 starts
   // (n0 / a_grp_n) · a_grp_off elements further (q'_h = W_k,hᵀ q_h: K = 64 columns of head h)
@@ -153,7 +155,9 @@ struct SelectArgs {
   float lam = 0.f; const uint32_t* root_bits = nullptr;
   const int* trans_off = nullptr; const int* trans_tok = nullptr; const int* trans_dst = nullptr;
   const int* root_child = nullptr;
+  const int* st_depth = nullptr; const int* st_keep = nullptr;   // per automaton state
   int* state = nullptr; int* finished = nullptr;
+  int* rowbase = nullptr;            // per row k - d of the new state (read by the next LM head)
   int eos = 0, pad = 0; int min_new = 0;
   int* step = nullptr;               // device counter of generated tokens (read + incremented)
   int* pos = nullptr;                // device decoder position (incremented)
@@ -180,6 +184,7 @@ struct BeamArgs {
   float lam = 0.f, len_pen = 1.f;
   const uint32_t* root_bits = nullptr; const int* root_child = nullptr;
   const int* trans_off = nullptr; const int* trans_tok = nullptr; const int* trans_dst = nullptr;
+  const int* st_depth = nullptr; const int* st_keep = nullptr;
   int* step = nullptr; int* pos = nullptr; int* all_done = nullptr; int* ticket = nullptr;
   int* next_ids = nullptr; int* state = nullptr;        // [R]
   float* run_sc = nullptr; int* run_seq = nullptr;      // [R], [R][Lt-P]

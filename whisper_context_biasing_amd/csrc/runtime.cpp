@@ -124,6 +124,7 @@ struct wcb_bias {
   uint64_t id = 0;                  // decode-graph cache key (never reused, unlike the address)
   wcb_handle* owner = nullptr;      // the handle whose decode graphs may hold these device buffers
   DevBuf root_bits, root_child, trans_off, trans_tok, trans_dst;
+  DevBuf st_depth, st_keep;         // per state: trie depth, deepest completed phrase on its path
 };
 
 // Decode state of one in-flight generate call. Two contexts (one per cross-K/V buffer) let call
@@ -466,6 +467,8 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     HIPCHK(hipMemcpy(eb->trans_off.p, off.data(), 8, hipMemcpyHostToDevice));
     eb->trans_tok.ensure(4);
     eb->trans_dst.ensure(4);
+    eb->st_depth.ensure(4);   // root: depth 0, keep 0 (zeroed)
+    eb->st_keep.ensure(4);
     h->empty_bias = std::move(eb);
     *out = h.release();
   });
@@ -793,7 +796,7 @@ void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode
   const DecCtx& D0 = h->dc[h->nctx - 1];   // every context is sized together
   const size_t xbuf = xmode ? (size_t)clips * S * d * e : 2 * L * (size_t)clips * S * d * e;
   const size_t need[] = {xbuf, 2 * L * (size_t)B * T * d * e, (size_t)B * d * 4,
-                         (size_t)B * h->d.ffn * e, (size_t)B * h->d.vocab * 4, (size_t)(I_NEXT + 3 * B + 16) * 4,
+                         (size_t)B * h->d.ffn * e, (size_t)B * h->d.vocab * 4, (size_t)(I_NEXT + 4 * B + 16) * 4,
                          (size_t)B * out_ld * 4};
   const DevBuf* have[] = {&h->xkv2[h->nctx - 1], &D0.kvself, &D0.dx, &D0.dffn, &D0.logits, &D0.ints, &D0.outbuf};
   bool grow = false;
@@ -977,6 +980,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       lm.sel_val = D.part_val.as<float>() + (size_t)b0 * D.nchunk;
       lm.sel_idx = D.part_idx.as<int>() + (size_t)b0 * D.nchunk;
       lm.sel_root_bits = c.bias->root_bits.as<uint32_t>(); lm.sel_lam = c.lam;
+      lm.sel_rowbase = ints + I_NEXT + 3 * c.B + b0;   // per row k - d of its state (select_finalize)
       lm.sel_eos = h->d.eos_token_id; lm.sel_step = ints + I_STEP; lm.sel_min_new = c.min_new;
     }
     dgemm(h, "lm_head", lm, st_);
@@ -1025,7 +1029,8 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     s.root_bits = c.bias->root_bits.as<uint32_t>();
     s.trans_off = c.bias->trans_off.as<int>(); s.trans_tok = c.bias->trans_tok.as<int>();
     s.trans_dst = c.bias->trans_dst.as<int>(); s.root_child = c.bias->root_child.as<int>();
-    s.state = next_ids + B; s.finished = next_ids + 2 * B;
+    s.st_depth = c.bias->st_depth.as<int>(); s.st_keep = c.bias->st_keep.as<int>();
+    s.state = next_ids + B; s.finished = next_ids + 2 * B; s.rowbase = next_ids + 3 * B;
     s.eos = h->d.eos_token_id; s.pad = h->d.pad_token_id; s.min_new = c.min_new;
     s.step = ints + I_STEP; s.pos = pos; s.next_ids = next_ids;
     s.out_ids = D.outbuf.as<int>(); s.out_ld = c.out_ld;
@@ -1120,7 +1125,7 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     // ---- decode stream
     HIPCHK(hipStreamWaitEvent(D.hs, h->ev_xkv[buf], 0));
     int* ints = D.ints.as<int>();
-    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 3 * R) * 4, D.hs));
+    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 4 * R) * 4, D.hs));
     if (prefix) {   // one prefix row shared by every decoder row (forced_ld = 0 below)
       if ((size_t)P * 4 > D.forced.bytes) { quiesce(h); D.forced.ensure((size_t)P * 4); }
       write_i32(D.forced.as<int>(), prefix, P, D.hs);
@@ -1141,6 +1146,7 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
       bm.lam = cfg->bias_boost; bm.len_pen = 1.f;
       bm.root_bits = bs->root_bits.as<uint32_t>(); bm.root_child = bs->root_child.as<int>();
       bm.trans_off = bs->trans_off.as<int>(); bm.trans_tok = bs->trans_tok.as<int>(); bm.trans_dst = bs->trans_dst.as<int>();
+      bm.st_depth = bs->st_depth.as<int>(); bm.st_keep = bs->st_keep.as<int>();
       bm.step = ints + I_STEP; bm.pos = ints + I_POS; bm.all_done = ints + I_DONE; bm.ticket = ints + I_TICKET;
       bm.next_ids = ints + I_NEXT; bm.state = ints + I_NEXT + R;
       bm.out_ids = D.outbuf.as<int>(); bm.out_ld = out_ld; bm.out_len = ints + I_UNFIN;
@@ -1267,7 +1273,7 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
     HIPCHK(hipEventRecord(h->ev_xkv[buf], h->he));
     HIPCHK(hipStreamWaitEvent(D.hs, h->ev_xkv[buf], 0));
     int* ints = D.ints.as<int>();
-    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 3 * B) * 4, D.hs));
+    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 4 * B) * 4, D.hs));
     gather_col(ints + I_NEXT, dec_ids, B, T, 0, D.hs);
     // forced column T is never read: feed positions 0..T-1 (advance reads column pos+1 < T except last)
     HIPCHK(hipMemsetAsync(D.forced.p, 0, (size_t)B * (T + 1) * 4, D.hs));
@@ -1285,13 +1291,15 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
 }
 
 // ------------------------------------------------------------------------------ bias automaton
-int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets, int n_phrases, wcb_bias** out) {
+int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets, int n_phrases,
+                    const uint8_t* word_start, wcb_bias** out) {
   return guarded(h, [&] {
     REQUIRE(h && out && n_phrases >= 0 && (n_phrases == 0 || (tokens && offsets)), "bad argument");
     const int V = h->d.vocab;
     // trie
     std::vector<std::map<int, int>> ch(1);
     std::vector<int> depth(1, 0);
+    std::vector<char> end(1, 0);
     for (int p = 0; p < n_phrases; ++p) {
       int s = 0;
       REQUIRE(offsets[p + 1] >= offsets[p], "offsets must be non-decreasing");
@@ -1302,6 +1310,7 @@ int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets
         if (it == ch[s].end()) {
           ch.emplace_back();
           depth.push_back(depth[s] + 1);
+          end.push_back(0);
           const int nn = (int)ch.size() - 1;
           ch[s][v] = nn;
           s = nn;
@@ -1309,17 +1318,23 @@ int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets
           s = it->second;
         }
       }
+      if (s) end[s] = 1;
     }
     const int ns = (int)ch.size();
-    std::vector<int> fail(ns, 0), order;
+    std::vector<int> fail(ns, 0), keep(ns, 0), order;
     order.reserve(ns);
     std::deque<int> q;
-    for (auto& kv : ch[0]) { fail[kv.second] = 0; q.push_back(kv.second); }
+    for (auto& kv : ch[0]) {
+      fail[kv.second] = 0;
+      keep[kv.second] = end[kv.second] ? 1 : 0;
+      q.push_back(kv.second);
+    }
     while (!q.empty()) {
       const int s = q.front();
       q.pop_front();
       order.push_back(s);
       for (auto& kv : ch[s]) {
+        keep[kv.second] = end[kv.second] ? depth[kv.second] : keep[s];
         int f = fail[s];
         while (f && !ch[f].count(kv.first)) f = fail[f];
         auto it = ch[f].find(kv.first);
@@ -1339,9 +1354,14 @@ int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets
         if (depth[kv.second] >= 2) { tok.push_back(kv.first); dst.push_back(kv.second); }
       off[s + 1] = (int)tok.size();
     }
+    // root children: a match may START only at a word-start token (word_start == null: any token)
     std::vector<uint32_t> bits((V + 31) / 32, 0u);
     std::vector<int> rc(V, -1);
-    for (auto& kv : ch[0]) { bits[kv.first >> 5] |= 1u << (kv.first & 31); rc[kv.first] = kv.second; }
+    for (auto& kv : ch[0])
+      if (!word_start || word_start[kv.first]) {
+        bits[kv.first >> 5] |= 1u << (kv.first & 31);
+        rc[kv.first] = kv.second;
+      }
     auto b = std::make_unique<wcb_bias>();
     b->n_states = ns;
     b->vocab = V;
@@ -1360,6 +1380,10 @@ int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets
       HIPCHK(hipMemcpy(b->trans_tok.p, tok.data(), tok.size() * 4, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(b->trans_dst.p, dst.data(), dst.size() * 4, hipMemcpyHostToDevice));
     }
+    b->st_depth.ensure((size_t)ns * 4);
+    b->st_keep.ensure((size_t)ns * 4);
+    HIPCHK(hipMemcpy(b->st_depth.p, depth.data(), (size_t)ns * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(b->st_keep.p, keep.data(), (size_t)ns * 4, hipMemcpyHostToDevice));
     h->biases.push_back(b.get());
     *out = b.release();
   });
@@ -1385,7 +1409,8 @@ void wcb_bias_destroy(wcb_bias* b) {
       }
     h->biases.erase(std::remove(h->biases.begin(), h->biases.end(), b), h->biases.end());
   }
-  for (DevBuf* x : {&b->root_bits, &b->root_child, &b->trans_off, &b->trans_tok, &b->trans_dst}) x->release();
+  for (DevBuf* x : {&b->root_bits, &b->root_child, &b->trans_off, &b->trans_tok, &b->trans_dst, &b->st_depth, &b->st_keep})
+    x->release();
   delete b;
 }
 

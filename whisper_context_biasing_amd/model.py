@@ -67,9 +67,11 @@ class BiasList:
         toks = np.asarray([t for p in phrases for t in p] or [0], dtype=np.int32)
         offs = np.zeros(len(phrases) + 1, dtype=np.int32)
         offs[1:] = np.cumsum([len(p) for p in phrases]) if phrases else []
+        ws = model.word_start
         h = C.c_void_p()
         _lib.check(lib.wcb_bias_create(model._h, toks.ctypes.data, offs.ctypes.data, len(phrases),
-                                       C.byref(h)), model._h, "wcb_bias_create")
+                                       ws.ctypes.data if ws is not None else None, C.byref(h)),
+                   model._h, "wcb_bias_create")
         self._h = h
         self._lib = lib   # held so the destructor still works during interpreter shutdown
         self.n_phrases = len(phrases)
@@ -112,6 +114,7 @@ class WhisperCB:
         # accumulate one V-sized automaton per distinct batch)
         self._bias_cache: "OrderedDict[tuple, BiasList]" = OrderedDict()
         self.bias_cache_size = 8
+        self._word_start: Optional[np.ndarray] = None
         self._loaded = False
 
     # ------------------------------------------------------------------ construction / weights
@@ -196,6 +199,22 @@ class WhisperCB:
         return enc
 
     # ------------------------------------------------------------------------------ biasing
+    @property
+    def word_start(self) -> Optional[np.ndarray]:
+        """[vocab] uint8 mask of the tokens a bias match may start at (None = every token)."""
+        return self._word_start
+
+    def set_word_start(self, mask) -> None:
+        """Word-start gate of the bias boost: for a BPE vocabulary, True on the tokens that begin a word
+        (a leading space), e.g. `[t.startswith("\u0120") for t in tokenizer.convert_ids_to_tokens(range(V))]`.
+        None disables the gate. Cached automata are rebuilt."""
+        if mask is not None:
+            mask = np.ascontiguousarray(np.asarray(mask, dtype=bool).astype(np.uint8))
+            if mask.shape != (self.dims.vocab,):
+                raise ValueError(f"word_start must have shape ({self.dims.vocab},), got {mask.shape}")
+        self._word_start = mask
+        self._bias_cache.clear()
+
     def bias_list(self, phrases: Sequence[Sequence[int]]) -> BiasList:
         key = tuple(tuple(int(t) for t in p) for p in phrases)
         b = self._bias_cache.get(key)

@@ -5,8 +5,11 @@
 * Bias lists: phrases sampled with `random.Random(7)` from the 9,884 unique lowercased
   `bias_words` of the reference's `data/medical-united-syn-med-75-jsonl/{dev,test}.jsonl`
   (extracted once into `data/bias_phrases.json`; the reference itself never travels).
-  The Whisper BPE is unavailable offline, so token ids are synthetic: phrase token length =
-  clamp(round(len(chars)/3.5), 1, 16), ids from a seeded hash of the phrase in [0, eot).
+  The Whisper BPE is unavailable offline, so token ids are synthetic: each word of a phrase gets
+  max(1, round(len(word)/3.5)) tokens (at most 16 per phrase) drawn from a seeded hash of the
+  phrase; a word's first token is a word-start token, the rest are continuation tokens.
+* Word starts: `synth_word_start(eot)` marks a seeded half of [0, eot) as word-start tokens (the
+  role of the leading-space tokens of a BPE vocabulary; oracle/bias_ref.py's gate).
 """
 from __future__ import annotations
 
@@ -14,6 +17,7 @@ import hashlib
 import json
 import os
 import random
+from functools import lru_cache
 from typing import List
 
 import numpy as np
@@ -48,13 +52,70 @@ def sample_bias_phrases(n: int, seed: int = 7) -> List[str]:
     return random.Random(seed).sample(pool, n)
 
 
+@lru_cache(maxsize=8)
+def _word_start_ids(eot: int):
+    ws = np.random.Generator(np.random.PCG64(20240611)).random(eot) < 0.5
+    return np.flatnonzero(ws), np.flatnonzero(~ws), ws
+
+
+def synth_word_start(eot: int, vocab: int = 0) -> np.ndarray:
+    """[max(vocab, eot)] bool: the synthetic word-start tokens (a seeded half of [0, eot); the special
+    tokens from eot on are not word starts)."""
+    ws = _word_start_ids(eot)[2]
+    out = np.zeros(max(vocab, eot), dtype=bool)
+    out[:eot] = ws
+    return out
+
+
 def phrase_token_ids(phrase: str, eot: int) -> List[int]:
-    n = int(min(max(round(len(phrase) / 3.5), 1), 16))
     h = hashlib.sha256(("phrase:" + phrase).encode()).digest()
     rng = np.random.Generator(np.random.PCG64(int.from_bytes(h[:8], "little")))
-    return [int(v) for v in rng.integers(0, eot, size=n)]
+    starts, conts, _ = _word_start_ids(eot)
+    out: List[int] = []
+    for word in phrase.split() or [phrase]:
+        n = max(1, int(round(len(word) / 3.5)))
+        out.append(int(starts[rng.integers(0, len(starts))]))
+        out.extend(int(conts[i]) for i in rng.integers(0, len(conts), size=n - 1))
+    return out[:16]
 
 
 def synth_bias_list(n: int, eot: int, seed: int = 7) -> List[List[int]]:
     """Token-id sequences of `n` sampled phrases (the bias list fed to the boost operator)."""
     return [phrase_token_ids(p, eot) for p in sample_bias_phrases(n, seed)]
+
+
+def runner_up_phrases(model, mel, n_tokens: int, lam: float, word_start=None):
+    """Bias phrases the boost can actually place (the bench's biased-WER workload): for every clip, the
+    step of the lam = 0 greedy decode whose top-1/top-2 logit gap is smallest among those below `lam`
+    (first step excluded) whose runner-up token r may start a match (`word_start`), and the phrase
+    [r, n] with n the greedy token after r (the decode teacher-forced through r). Returns
+    (plain_ids [B, n_tokens] int64, phrases, targets) with targets[i] = (clip, step) of phrase i.
+    Runs on the GPU through the model's own generate / forward; untimed setup."""
+    import torch
+
+    dims = model.dims
+    plain = model.generate(mel, max_length=n_tokens, min_new_tokens=n_tokens)
+    B = plain.shape[0]
+    sot = torch.full((B, 1), dims.decoder_start_token_id, dtype=plain.dtype, device=plain.device)
+    logits = model.forward(mel, decoder_input_ids=torch.cat([sot, plain[:, :-1]], 1)).logits
+    top2, idx2 = logits.topk(2, dim=-1)                                   # [B, T, 2]
+    gap = (top2[..., 0] - top2[..., 1]).float()
+    ru = idx2[..., 1]
+    ok = (gap < lam) & (ru != dims.eos_token_id)
+    ok[:, 0] = False
+    if word_start is not None:
+        ok &= torch.as_tensor(np.asarray(word_start, dtype=bool), device=ru.device)[ru]
+    gap = torch.where(ok, gap, torch.full_like(gap, float("inf")))
+    t = gap.argmin(dim=1)
+    keep = ok.gather(1, t[:, None])[:, 0]
+    r = ru.gather(1, t[:, None])[:, 0]
+    forced = torch.cat([sot, plain], 1).clone()                          # [SOT, ids[:t], r, ...]
+    forced[torch.arange(B, device=forced.device), t + 1] = r
+    nxt = model.forward(mel, decoder_input_ids=forced).logits            # causal: later tokens are ignored
+    n1 = nxt[torch.arange(B, device=nxt.device), t + 1].argmax(-1)
+    phrases, targets = [], []
+    for b in range(B):
+        if bool(keep[b]):
+            phrases.append([int(r[b]), int(n1[b])])
+            targets.append((b, int(t[b])))
+    return plain.cpu().numpy().astype(np.int64), phrases, targets
