@@ -92,17 +92,17 @@ def cpu_baseline(size: str, n_tokens: int, n_phr: int, boost: float, seed: int =
                       f"(OMP_NUM_THREADS), host has {os.cpu_count()} logical CPUs"}
 
 
-def _pmc_traffic(kernel: str, grid: int):
-    """HBM bytes per launch of (kernel symbol, grid) from the committed rocprofv3 PMC passes
-    (profiles/*pmc*.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2 (gfx950 correction) +
-    WRITE_SIZE), or None."""
+def _pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` (symbol, every grid it runs at) from the committed rocprofv3
+    PMC passes (profiles/*pmc*.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2 (gfx950
+    correction) + WRITE_SIZE), or None."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
-        e = d.get("kernels", {}).get(f"{kernel}|{grid}")
+        e = d.get("symbols", {}).get(kernel)
         if e:
             return e["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
     return None
@@ -254,11 +254,11 @@ def main():
                           "launches_per_step": v["launches"] / prof_steps,
                           "bytes_per_launch": v["bytes"] / v["launches"], "flops_per_launch": v["flops"] / v["launches"],
                           "total_ms_per_step": round(v["ms"] / prof_steps, 3)}
-        # dominant = the (kernel symbol, grid) with the most time per step — rocprofv3's grouping, so
-        # classes sharing one kernel instance and grid (e.g. dec_out / dec_xo) are summed as it sums them
+        # dominant = the kernel symbol with the most time per step — rocprofv3 --stats' grouping, so the
+        # classes one kernel instance serves (e.g. dec_qkv / dec_xq / dec_fc1) are summed as it sums them
         groups = {}
         for k, c in classes.items():
-            gk = f'{c["kernel"]}|{c["grid"]}'
+            gk = c["kernel"]
             g = groups.setdefault(gk, {"classes": [], "ms": 0.0, "launches": 0.0, "bytes": 0.0, "flops": 0.0})
             g["classes"].append(k)
             g["ms"] += c["total_ms_per_step"]
@@ -272,7 +272,7 @@ def main():
         avg_ms = g["ms"] / g["launches"]
         per = (g["flops"] if c["bound"] == "mfma" else g["bytes"]) / g["launches"]
         ach = per / (avg_ms * 1e-3) / (1e12 if c["bound"] == "mfma" else 1e9)
-        roof = dict(c, **{"class": "+".join(g["classes"]), "achieved": round(ach, 1),
+        roof = dict(c, **{"class": "+".join(sorted(g["classes"])), "achieved": round(ach, 1), "grid": None,
                           "frac": round(ach / c["peak"], 4), "avg_launch_ms": round(avg_ms, 5),
                           "launches_per_step": g["launches"], "bytes_per_launch": g["bytes"] / g["launches"],
                           "flops_per_launch": g["flops"] / g["launches"], "total_ms_per_step": round(g["ms"], 3),
@@ -280,7 +280,7 @@ def main():
                                     f"serialised profiling pass of {prof_steps} step(s); rocprofv3 trace of the "
                                     "same command: profiles/ (tools/check_roofline.py compares the two)"})
         c2 = (args.model, args.batch, args.num_beams, args.dtype, args.new_tokens) == ("small", 32, 1, "bf16", 64)
-        tr = _pmc_traffic(roof["kernel"], roof["grid"]) if c2 else None
+        tr = _pmc_traffic(roof["kernel"]) if c2 else None
         if tr:
             roof["traffic"], roof["traffic_source"] = tr
         others = {k: v for k, v in classes.items() if k not in g["classes"]}

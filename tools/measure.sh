@@ -21,7 +21,6 @@ python tools/prof_summary.py "$(ls "$O"/trace/*kernel_trace.csv "$O"/trace/*/*ke
 cat "$O/kernel_summary.txt" | head -25
 python tools/pmc_traffic.py "$O/pmc_fetch" "$O/pmc_write" "$O/pmc_traffic.json" > /dev/null
 TRACE="$(ls "$O"/trace/*kernel_trace.csv "$O"/trace/*/*kernel_trace.csv 2>/dev/null | head -1)"
-python tools/check_roofline.py "$O/bench_default.json" "$TRACE" > "$O/check_default.json"; cat "$O/check_default.json"
-python tools/check_roofline.py "$O/trace_bench.json" "$TRACE" > "$O/check_traced.json"; cat "$O/check_traced.json"
 STATS="$(ls "$O"/trace/*kernel_stats.csv "$O"/trace/*/*kernel_stats.csv 2>/dev/null | head -1)"
 cp "$STATS" "$O/kernel_stats.csv"
+python tools/check_roofline.py "$O/bench_default.json" "$O/kernel_stats.csv" > "$O/check_default.json"; cat "$O/check_default.json"

@@ -42,6 +42,17 @@ def main():
                      "bench's launch shapes (batch 32, fewer tokens)",
            "correction": "FETCH_SIZE(KB) x 1024 x 2 (gfx950 wide-read undercount) + WRITE_SIZE(KB) x 1024",
            "kernels": {}}
+    # per symbol over every grid it runs at (bench.py's roofline groups as rocprofv3 --stats does)
+    sym = collections.defaultdict(lambda: [[], []])
+    for k in set(fetch) & set(write):
+        sym[k.split("|")[0]][0].extend(fetch[k])
+        sym[k.split("|")[0]][1].extend(write[k])
+    res["symbols"] = {}
+    for k, (f, w) in sorted(sym.items(), key=lambda kv: -sum(kv[1][0]))[:top]:
+        fb = sum(f) / len(f) * 1024 * 2
+        wb = sum(w) / len(w) * 1024
+        res["symbols"][k] = {"launches": len(f), "read_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+                             "hbm_bytes_per_launch": fb + wb}
     keys = sorted(set(fetch) & set(write), key=lambda k: -sum(fetch[k]))[:top]
     for k in keys:
         f, w = fetch[k], write[k]
