@@ -146,7 +146,8 @@ int wcb_op_layernorm(int dtype, const float* x, const float* w, const float* b, 
 int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H, int Sq,
                      int Sk, int flash, void* stream);
 /* decode attention in the runtime's layout: q/o [B][H*64], K/V head-major [B][H][Sk][64]; one query
- * per (row, head), nsplit key chunks (split-KV), kernel variant (k_attn.hip launch_decode). */
+ * per (row, head), nsplit key chunks (split-KV), kernel variant (k_attn.hip launch_decode; 6 = the
+ * one-token self-attention kernel, nsplit 1). */
 int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H,
                             int Sk, int nsplit, int variant, void* stream);
 

@@ -241,8 +241,8 @@ def test_gemm_ring_encoder_shapes(dt, M, N, K, act, resid):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f32"])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
-@pytest.mark.parametrize("Sk,split", [(1500, 1), (1500, 4), (37, 1), (1, 3)])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("Sk,split", [(1500, 1), (1500, 4), (37, 1), (1, 3), (64, 1), (65, 1), (200, 1)])
 def test_decode_attention_variants(dt, variant, Sk, split):
     """Every cross-attention kernel variant in the runtime's head-major K/V layout, with and without
     split-KV (variant 0 = the two-pass kernel beam search over precomputed K/V runs), vs fp64."""

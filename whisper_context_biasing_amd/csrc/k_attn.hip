@@ -310,8 +310,84 @@ __global__ __launch_bounds__(NW * 64) void attn_decode2p_kernel(AttnArgs a) {
   }
 }
 
+// Decoder self-attention of one new token (Sq = 1, no split, keys in place): one wave per (row,
+// head). The first 64 keys' K and V rows are requested together with the key count (which lives in
+// device memory: the step graph is replayed) — one memory round trip instead of a dependent pair;
+// rows past the count (clamped to the cache capacity kv_rows) are loaded and masked. Longer
+// contexts continue in 64-key chunks with an online softmax. 8 lanes per key (16 B each), 8 keys
+// per load, 8 loads of K and of V per lane in flight.
+template <typename T>
+__global__ __launch_bounds__(64) void attn_self_kernel(AttnArgs a) {
+  const int b = blockIdx.y / a.H, h = blockIdx.y % a.H, lane = threadIdx.x;
+  const int seg = lane & 7, kg = lane >> 3;
+  const long base = (long)((a.row0 + b) / a.b_div) * a.k_sb + (long)h * a.k_sh + seg * 8;
+  const T* kb = reinterpret_cast<const T*>(a.k) + base;
+  const T* vb = reinterpret_cast<const T*>(a.v) + base;
+  const T* q = reinterpret_cast<const T*>(a.q) + (long)b * a.q_Sb * a.ldq + h * 64;
+  const int cap = a.kv_rows - 1;
+  float qv[8], kv[8][8], vv[8][8];
+  load8f<T>(q + seg * 8, qv);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) load8f<T>(kb + (long)min(u * 8 + kg, cap) * a.k_sk, kv[u]);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) load8f<T>(vb + (long)min(u * 8 + kg, cap) * a.k_sk, vv[u]);
+  const int nk = a.nkeys_dev ? (*a.nkeys_dev + a.nkeys_add) : a.nkeys;
+  float m = -INFINITY, l = 0.f;
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < nk; j0 += 64) {
+    if (j0) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) load8f<T>(kb + (long)min(min(j0 + u * 8 + kg, nk - 1), cap) * a.k_sk, kv[u]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) load8f<T>(vb + (long)min(min(j0 + u * 8 + kg, nk - 1), cap) * a.k_sk, vv[u]);
+    }
+    float sc[8];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d = fmaf(qv[e], kv[u][e], d);
+#pragma unroll
+      for (int x = 1; x < 8; x <<= 1) d += __shfl_xor(d, x, 64);
+      sc[u] = (j0 + u * 8 + kg < nk) ? d : -INFINITY;
+      mx = fmaxf(mx, sc[u]);
+    }
+    const float mn = fmaxf(m, wave_max(mx));
+    const float r = __expf(m - mn);   // 0 on the first chunk (m = -inf)
+    l *= r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] *= r;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float p = (j0 + u * 8 + kg < nk) ? __expf(sc[u] - mn) : 0.f;
+      if (seg == 0) l += p;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = fmaf(p, vv[u][e], o[e]);
+    }
+    m = mn;
+  }
+  l = wave_sum(l);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o[e] += __shfl_xor(o[e], 8, 64);
+    o[e] += __shfl_xor(o[e], 16, 64);
+    o[e] += __shfl_xor(o[e], 32, 64);
+  }
+  if (kg == 0) {
+    float r[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = o[e] / l;
+    store8<T>(reinterpret_cast<T*>(a.o) + (long)b * a.o_Sb * a.ldo + h * 64 + seg * 8, r);
+  }
+}
+
 template <typename T>
 static void launch_decode(const AttnArgs& b, dim3 grid, int variant, hipStream_t s) {
+  if (b.kv_rows > 0 && !b.phys && b.Sq == 1 && b.nsplit == 1) {   // decoder self-attention, one new token
+    WCB_LAUNCH(attn_self_kernel<T>, dim3(1, grid.y), dim3(64), 0, s, b);
+    return;
+  }
   if (b.phys) {   // beam-search self-attention: keys through the row map
     WCB_LAUNCH((attn_decode_kernel<T, 4, 8, true>), grid, dim3(256), 0, s, b);
     return;

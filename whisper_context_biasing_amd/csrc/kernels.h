@@ -117,6 +117,8 @@ struct AttnArgs {
   // cache row that computed key j) : (row0 + b) / b_div (beams sharing one clip's cross K/V)
   int row0 = 0, b_div = 1;
   const int* phys = nullptr; long phys_ld = 0;
+  int kv_rows = 0;   // > 0: K/V rows allocated per (row, head) — the one-token self-attention kernel
+                     // loads the first keys before the device key count arrives, clamped to this
 };
 void attention_decode(DType t, const AttnArgs& a, hipStream_t s);   // VALU, any T, any Sq
 bool attention_flash(DType t, const AttnArgs& a, hipStream_t s);    // MFMA encoder (16-bit T)

@@ -184,9 +184,10 @@ struct wcb_handle {
   int xenc_split = 8;   // key ranges per row of the encoder-space kernel (rows x ranges workgroups)
   int xenc_variant = 1; // attn_xenc kernel variant (k_xenc.hip)
   int xqk = 0;          // 1: one GEMM LN(x) → q' with W_k,hᵀW_q,h precombined (WCB_XQK; measured slower: 14 MB per layer)
-  // decoder LayerNorm input: 1 = the T-typed copy of the residual stream (half the bytes per
-  // projection workgroup; statistics still from the f32 rows), 0 = the f32 rows (WCB_LN16)
-  int ln16 = 0;
+  // decoder LayerNorm input of the fused LN projections: 1 = the T-typed copy of the residual stream
+  // the producers write beside the f32 rows (half the bytes per projection workgroup; C2 decode 1.066
+  // vs 1.110 ms/token), 0 = the f32 rows (f32 mode). WCB_LN16 overrides.
+  int ln16 = 1;
   int steps_per_graph = 8;   // decode steps captured per replayed graph (WCB_STEPS_PER_GRAPH)
   // decode projections on gemm_dec_kernel (K supported): the LayerNorm consumers compute their row
   // statistics from the rows they load, so the producers publish no per-16-column partial sums
@@ -888,7 +889,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     a.k = cache0; a.v = cache0 + (size_t)B * H * T * 64 * e;
     a.k_sb = (long)H * T * 64; a.k_sh = (long)T * 64; a.k_sk = 64;
     a.row0 = b0; a.phys = c.phys; a.phys_ld = T;
-    a.o = datt; a.ldo = d; a.o_Sb = 1; a.B = nb; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1;
+    a.o = datt; a.ldo = d; a.o_Sb = 1; a.B = nb; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1; a.kv_rows = T;
     {
       const double t_keys = c.host_pos >= 0 ? c.host_pos + 1 : 0;   // keys this step (eager pass)
       h->timed("dec_self_attn", 4.0 * nb * H * t_keys * 64, nb * H * t_keys * 128.0 * e, st_,
@@ -1545,6 +1546,7 @@ int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void*
     a.k = k; a.v = v; a.k_sb = (long)H * Sk * 64; a.k_sh = (long)Sk * 64; a.k_sk = 64;
     a.o = o; a.ldo = (long)H * 64; a.o_Sb = 1; a.B = B; a.H = H; a.nkeys = Sk;
     a.variant = variant;
+    if (variant == 6) a.kv_rows = Sk;   // the one-token self-attention kernel (speculative first keys)
     static DevBuf part, ticket;
     if (nsplit > 1) {
       a.nsplit = nsplit;
