@@ -1025,7 +1025,8 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
     static const int dec_mf = [] { const char* v = getenv("WCB_DEC_MF"); return v ? atoi(v) : 0; }();
     if (dec_enabled()) {
       // 16-row workgroups up to 64 rows (measured C2: 1.074 vs 1.147 ms/token with 32-row workgroups)
-      const bool mf1 = dec_mf == 1 || (dec_mf == 0 && g.M <= 64) || g.K >= 4096;
+      // The LM head walks the vocabulary persistently: 32-row workgroups read every weight tile once
+      const bool mf1 = dec_mf == 1 || (dec_mf == 0 && g.M <= 64 && !(g.sel_val && g.M > 16)) || g.K >= 4096;
       const bool ok = mf1 ? launch_dec_mf<T, 1>(g, s) : launch_dec_mf<T, 2>(g, s);
       if (ok) return;
     }

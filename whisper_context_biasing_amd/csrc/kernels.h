@@ -89,7 +89,7 @@ void embed(DType t, const void* emb, const void* pos_emb, const int* ids, const 
            float* stats, int M, int d, hipStream_t s, void* x16 = nullptr, int V = 1 << 30);
 // LM-head argmax partials per row: gemm_dec_kernel walks the vocabulary with kDecWalkers workgroups
 // per row block and writes one partial per walker; the older skinny kernel one per 64 columns.
-constexpr int kDecWalkers = 256;
+constexpr int kDecWalkers = 512;
 bool gemm_dec_supported(DType t, int K);
 int lm_head_partials(DType t, int K, int vocab);
 
