@@ -185,3 +185,46 @@ def test_c5_large_v3_f16_beam5_5000_phrase_boost():
     """C5 at reduced batch: full-depth large-v3 (128 mel bins), beam 5, fp16 with the encoder clamp,
     5000 phrases (lambda 2), high-margin recipe: identical to the oracle."""
     check_beam5_boost("large-v3", "f16", 5000, 1)
+
+
+# ------------------------------------------------------------------ prompt-conditioned decode (causal prefill)
+@pytest.mark.parametrize("size,recipe,seed,dtype", [("micro", "diverse", 0, "f32"), ("small", "margin", 1, "f32"),
+                                                    ("small", "margin", 1, "bf16")])
+def test_prompt_prefill_matches_reference_golden(size, recipe, seed, dtype):
+    """The reference's biasing prompt (`<|startofprev|>` + tokens, data_utils/data_loader.py:182-366) as
+    prompt_ids: the prompt runs through the causal prefill pass (all prompt positions of every row in
+    one decoder pass, KV cache written, causal self-attention), then greedy / beam-5 decode. Against
+    the reference's own generate(prompt_ids=...) outputs: token-exact (f32 and the high-margin bf16),
+    margin-gated on the diverse recipe's near-ties."""
+    g = np.load(os.path.join(GOLD, f"prompt_{size}_{recipe}_s{seed}.npz"))
+    meta = eval(str(g["meta"][0]), {})
+    dims = get_dims(size)
+    m = model(size, seed, recipe, dtype)
+    x = mel_of(dims, meta["B"])
+    prompt = [int(v) for v in g["prompt_ids"]]
+    ids = m.generate(x, max_length=meta["n_tokens"], prompt_ids=prompt).cpu().numpy()
+    if recipe == "margin" or dtype == "f32":
+        assert ids.shape == g["greedy_ids"].shape and np.array_equal(ids, g["greedy_ids"]), (ids, g["greedy_ids"])
+    else:
+        gated_equal(ids, g["greedy_ids"], g["greedy_margin"])
+    if recipe == "margin":
+        b = m.generate(x, max_length=meta["beam_len"], num_beams=5, prompt_ids=prompt).cpu().numpy()
+        assert b.shape == g["beam5_ids"].shape and np.array_equal(b, g["beam5_ids"]), (b, g["beam5_ids"])
+
+
+def test_forward_teacher_forcing_is_one_prefill_pass_per_chunk():
+    """wcb_forward = causal prefill of all T positions: logits of every position equal the oracle's
+    teacher-forced decoder (f32), for T beyond one prefill pass (several chunks at B = 40)."""
+    dims = get_dims("micro")
+    m = model("micro", 0, "diverse", "f32")
+    om = W.OracleModel.from_dims(dims, weights("micro", 0, "diverse"))
+    B, T = 40, 13                                   # 256 // 40 = 6 positions per pass: 3 passes
+    x = mel_of(dims, B)
+    rng = np.random.default_rng(3)
+    dec = np.concatenate([np.full((B, 1), dims.decoder_start_token_id), rng.integers(0, 50000, (B, T - 1))], 1)
+    out = m.forward(x, decoder_input_ids=torch.from_numpy(dec))
+    got = out.logits.cpu().numpy()
+    enc = om.encode(x.numpy())
+    h = om.decode_tokens(dec, 0, {}, om.cross_kv(enc))
+    ref = om.lm_head(h)
+    np.testing.assert_allclose(got, ref, atol=2e-3, rtol=1e-3)

@@ -104,7 +104,8 @@ WCB_DEV float epi_store1(const GemmArgs& g, int m, int n, float v) {
     const int n2 = n - g.n_split;
     const int hh = n2 >> 6, dd = n2 & 63;
     const int kv = hh / g.hs_H, h = hh % g.hs_H;
-    const long off = ((((long)kv * g.hs_B + m) * g.hs_H + h) * g.kv_T + *g.pos) * 64 + dd;
+    const int rps = g.kv_rps > 1 ? g.kv_rps : 1;   // prefill: rows (cache row, position) row-major
+    const long off = ((((long)kv * g.hs_B + m / rps) * g.hs_H + h) * g.kv_T + *g.pos + m % rps) * 64 + dd;
     reinterpret_cast<T*>(g.kv_out)[off] = DT<T>::fromf(v);
     return v;
   }
@@ -603,7 +604,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
         const int n2 = nn - g.n_split;
         const int hh = n2 >> 6, dd = n2 & 63;
         const int kv = hh / g.hs_H, h = hh % g.hs_H;
-        const long off = ((((long)kv * g.hs_B + row) * g.hs_H + h) * g.kv_T + pos_v) * 64 + dd;
+        const int rps = g.kv_rps > 1 ? g.kv_rps : 1;
+        const long off = ((((long)kv * g.hs_B + row / rps) * g.hs_H + h) * g.kv_T + pos_v + row % rps) * 64 + dd;
         reinterpret_cast<T*>(g.kv_out)[off] = DT<T>::fromf(v);
       } else if (g.mode == 1) {
         v = epi_store1<T>(g, row, nn, v);
@@ -847,7 +849,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
           const int n2 = nn - g.n_split;
           const int hh = n2 >> 6, dd = n2 & 63;
           const int kv = hh / g.hs_H, h = hh % g.hs_H;
-          const long off = ((((long)kv * g.hs_B + row) * g.hs_H + h) * g.kv_T + pos_v) * 64 + dd;
+          const int rps = g.kv_rps > 1 ? g.kv_rps : 1;
+          const long off = ((((long)kv * g.hs_B + row / rps) * g.hs_H + h) * g.kv_T + pos_v + row % rps) * 64 + dd;
           reinterpret_cast<T*>(g.kv_out)[off] = DT<T>::fromf(v);
         } else if (!g.sel_val || g.out) {
           const long off = c_row(g, row) + nn;

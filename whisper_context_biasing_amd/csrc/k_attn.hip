@@ -40,7 +40,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const unsigned long long t_start = a.stamp.base ? stamp_now() : 0;
   const int seg = lane & 7, kg = lane >> 3;
-  const int nk_all = a.nkeys_dev ? (*a.nkeys_dev + a.nkeys_add) : a.nkeys;
+  const int nk_all = (a.nkeys_dev ? (*a.nkeys_dev + a.nkeys_add) : a.nkeys) + (a.causal ? i : 0);
   const int per = (nk_all + nsplit - 1) / nsplit;
   const int j_lo = chunk * per, j_hi = min(nk_all, j_lo + per);
   const int nk = max(j_hi - j_lo, 0);
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode2p_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const unsigned long long t_start = a.stamp.base ? stamp_now() : 0;
   const int seg = lane & 7, kg = lane >> 3;
-  const int nk_all = a.nkeys_dev ? (*a.nkeys_dev + a.nkeys_add) : a.nkeys;
+  const int nk_all = (a.nkeys_dev ? (*a.nkeys_dev + a.nkeys_add) : a.nkeys) + (a.causal ? i : 0);
   const int per = (nk_all + nsplit - 1) / nsplit;
   const int j_lo = chunk * per, j_hi = min(nk_all, j_lo + per);
   const int nk = max(j_hi - j_lo, 0);

@@ -82,9 +82,9 @@ void layernorm(DType t, const float* x, const float* w, const float* b, void* y,
 template <typename T>
 __global__ __launch_bounds__(256) void embed_kernel(const T* __restrict__ emb, const T* __restrict__ pemb, const int* __restrict__ ids,
                                                     const int* __restrict__ pos, float* __restrict__ x, float* __restrict__ st,
-                                                    int M, int d, T* __restrict__ x16, int V) {
+                                                    int M, int d, T* __restrict__ x16, int V, int rps) {
   const int row = blockIdx.x;
-  const int p = *pos;
+  const int p = *pos + row % rps;
   const int raw = ids[row];
   const long id = raw >= 0 && raw < V ? raw : 0;   // never index past the table (ids are produced on device)
   for (int c0 = 0; c0 < d; c0 += 256) {
@@ -106,14 +106,15 @@ __global__ __launch_bounds__(256) void embed_kernel(const T* __restrict__ emb, c
 }
 
 void embed(DType t, const void* emb, const void* pemb, const int* ids, const int* pos, float* x, float* st, int M,
-           int d, hipStream_t s, void* x16, int V) {
+           int d, hipStream_t s, void* x16, int V, int rps) {
+  rps = rps > 1 ? rps : 1;
   switch (t) {
     case kBF16: WCB_LAUNCH(embed_kernel<bf16_t>, dim3(M), dim3(256), 0, s, (const bf16_t*)emb,
-                                   (const bf16_t*)pemb, ids, pos, x, st, M, d, (bf16_t*)x16, V); break;
+                                   (const bf16_t*)pemb, ids, pos, x, st, M, d, (bf16_t*)x16, V, rps); break;
     case kF16: WCB_LAUNCH(embed_kernel<f16_t>, dim3(M), dim3(256), 0, s, (const f16_t*)emb,
-                                  (const f16_t*)pemb, ids, pos, x, st, M, d, (f16_t*)x16, V); break;
+                                  (const f16_t*)pemb, ids, pos, x, st, M, d, (f16_t*)x16, V, rps); break;
     case kF32: WCB_LAUNCH(embed_kernel<float>, dim3(M), dim3(256), 0, s, (const float*)emb,
-                                  (const float*)pemb, ids, pos, x, st, M, d, (float*)x16, V); break;
+                                  (const float*)pemb, ids, pos, x, st, M, d, (float*)x16, V, rps); break;
   }
 }
 

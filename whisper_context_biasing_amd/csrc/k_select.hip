@@ -14,6 +14,8 @@
 // logits once applying lam·(rowbase + root bit), rowbase = k - d of the row's state; the per-row
 // finalize re-scores only trans(s) — exact because lam >= 0 (checked on the host) and n on a trans
 // token is never below the vocabulary-pass value, so an underestimated copy never wins.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -120,6 +122,22 @@ __global__ __launch_bounds__(64) void select_finalize_kernel(SelectArgs a) {
     }
   }
 }
+
+// Causal prefill (runtime.cpp prefill): the token ids of positions *pos .. *pos + np - 1 of every
+// row, rows (row, position) row-major; ld 0 = one prefix shared by every row.
+__global__ void prefill_ids_kernel(int* ids, const int* src, int R, int np, int ld, const int* pos) {
+  const int p = *pos;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < R * np; i += gridDim.x * blockDim.x)
+    ids[i] = src[(long)(i / np) * ld + p + i % np];
+}
+void prefill_ids(int* ids, const int* src, int R, int np, int ld, const int* pos, hipStream_t s) {
+  const int grid = std::min((R * np + 255) / 256, 256);
+  WCB_LAUNCH(prefill_ids_kernel, dim3(grid), dim3(256), 0, s, ids, src, R, np, ld, pos);
+}
+__global__ void add_i32_kernel(int* p, int v) {
+  if (threadIdx.x == 0) *p += v;
+}
+void add_i32(int* p, int v, hipStream_t s) { WCB_LAUNCH(add_i32_kernel, dim3(1), dim3(64), 0, s, p, v); }
 
 // Teacher forcing / prompt prefill: next_ids[b] = forced[b·ld + (*pos) + 1]; pos += 1.
 __global__ void advance_forced_kernel(int* next_ids, const int* forced, int M, int ld, int* pos) {

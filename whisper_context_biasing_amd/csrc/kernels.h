@@ -56,6 +56,7 @@ struct GemmArgs {
   int hs_S = 0, hs_H = 0, hs_B = 0;        // mode 1: [g][B][H][S][64]; mode 2: rows of the cache
   const int* pos = nullptr; int kv_T = 0;  // mode 2: cache position (device) and cache length
   void* kv_out = nullptr; int n_split = 0; // mode 2: columns >= n_split go to the cache
+  int kv_rps = 0;                          // mode 2 prefill: row m → cache row m / kv_rps, position *pos + m % kv_rps
   // decode-step fusions (skinny path)
   const float* st_in = nullptr;    // LN row statistics partials [M][st_nb][2] (Σx, Σx²) of A
   float* st_out = nullptr;         // partials of the written f32 rows (residual GEMMs, NF = 1)
@@ -86,7 +87,10 @@ void layernorm(DType t, const float* x, const float* w, const float* b, void* y,
 
 // x[r][:] = emb[ids[r]][:] + pos_emb[*pos + r_pos][:] (f32 out), r_pos = r % rows_per_seq.
 void embed(DType t, const void* emb, const void* pos_emb, const int* ids, const int* pos, float* x,
-           float* stats, int M, int d, hipStream_t s, void* x16 = nullptr, int V = 1 << 30);
+           float* stats, int M, int d, hipStream_t s, void* x16 = nullptr, int V = 1 << 30, int rps = 1);
+// prefill: ids[r·np + t] = src[r·ld + *pos + t] (ld 0: one prefix row shared by every row)
+void prefill_ids(int* ids, const int* src, int R, int np, int ld, const int* pos, hipStream_t s);
+void add_i32(int* p, int v, hipStream_t s);   // *p += v (one thread)
 // LM-head argmax partials per row: gemm_dec_kernel walks the vocabulary with kDecWalkers workgroups
 // per row block and writes one partial per walker; the older skinny kernel one per 64 columns.
 constexpr int kDecWalkers = 512;
@@ -117,6 +121,7 @@ struct AttnArgs {
   // cache row that computed key j) : (row0 + b) / b_div (beams sharing one clip's cross K/V)
   int row0 = 0, b_div = 1;
   const int* phys = nullptr; long phys_ld = 0;
+  int causal = 0;    // decode kernels, Sq > 1 (prefill): query i sees the first nkeys(+dev) + i keys
   int kv_rows = 0;   // > 0: K/V rows allocated per (row, head) — the one-token self-attention kernel
                      // loads the first keys before the device key count arrives, clamped to this
 };

@@ -136,7 +136,7 @@ struct DecCtx {
   hipStream_t sub[kMaxSub] = {};                // row-group chains (fork/join inside the step graph)
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSub] = {};
   int dec_B = 0, dec_T = 0;
-  DevBuf kvself, dx, dx16, dh, dq, dqp, du, datt, dffn, dstats, xpart, xml, xticket, logits, part_val, part_idx, ints,
+  DevBuf kvself, dx, dx16, dh, dq, dqp, du, datt, dffn, dstats, xpart, xml, xticket, logits, part_val, part_idx, ints, pids,
       outbuf, forced, beam;
   int nchunk = 64;
   hipGraphExec_t gexec = nullptr;               // captured decode step
@@ -791,13 +791,19 @@ void drop_graphs(wcb_handle* h) {
   }
 }
 
-// decode workspace: B decoder rows (clips x beams) reading `clips` encoder outputs
-void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode) {
+// positions per prefill pass: up to kPrefillRows activation rows (bounds the row workspaces)
+constexpr int kPrefillRows = 256;
+int prefill_chunk(int R) { return std::max(1, kPrefillRows / std::max(R, 1)); }
+
+// decode workspace: B decoder rows (clips x beams) reading `clips` encoder outputs; activation
+// buffers for `rows` >= B rows (a prefill pass carries several positions per decoder row)
+void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode, int rows = 0) {
+  rows = std::max(rows, B);
   const size_t e = esize(h->d.dtype), d = h->d.d_model, L = h->d.n_layers, S = h->S();
   const DecCtx& D0 = h->dc[h->nctx - 1];   // every context is sized together
   const size_t xbuf = xmode ? (size_t)clips * S * d * e : 2 * L * (size_t)clips * S * d * e;
-  const size_t need[] = {xbuf, 2 * L * (size_t)B * T * d * e, (size_t)B * d * 4,
-                         (size_t)B * h->d.ffn * e, (size_t)B * h->d.vocab * 4, (size_t)(I_NEXT + 4 * B + 16) * 4,
+  const size_t need[] = {xbuf, 2 * L * (size_t)B * T * d * e, (size_t)rows * d * 4,
+                         (size_t)rows * h->d.ffn * e, (size_t)B * h->d.vocab * 4, (size_t)(I_NEXT + 4 * B + 16) * 4,
                          (size_t)B * out_ld * 4};
   const DevBuf* have[] = {&h->xkv2[h->nctx - 1], &D0.kvself, &D0.dx, &D0.dffn, &D0.logits, &D0.ints, &D0.outbuf};
   bool grow = false;
@@ -811,18 +817,19 @@ void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode
     D.kvself.ensure(need[1]);
     D.dec_B = std::max(D.dec_B, B);
     D.dec_T = std::max(D.dec_T, T);
-    D.dx.ensure((size_t)B * d * 4);
-    D.dx16.ensure((size_t)B * d * e);
-    D.dh.ensure((size_t)B * d * e);
-    D.dq.ensure((size_t)B * d * e);
-    D.datt.ensure((size_t)B * d * e);
-    D.dffn.ensure((size_t)B * h->d.ffn * e);
-    D.dstats.ensure((size_t)B * (d / 16) * 2 * 4);
-    D.xpart.ensure(std::max((size_t)B * h->H() * kXSplit * 66, (size_t)B * h->xenc_split * h->H() * d) * 4);
-    D.xml.ensure((size_t)B * h->xenc_split * h->H() * 2 * 4);
-    D.dqp.ensure((size_t)B * h->H() * d * e);
-    D.du.ensure((size_t)B * h->H() * d * e);
-    D.xticket.ensure((size_t)B * h->H() * 4);     // zeroed on allocation; combiners reset their slot
+    D.dx.ensure((size_t)rows * d * 4);
+    D.dx16.ensure((size_t)rows * d * e);
+    D.dh.ensure((size_t)rows * d * e);
+    D.dq.ensure((size_t)rows * d * e);
+    D.datt.ensure((size_t)rows * d * e);
+    D.dffn.ensure((size_t)rows * h->d.ffn * e);
+    D.dstats.ensure((size_t)rows * (d / 16) * 2 * 4);
+    D.xpart.ensure(std::max((size_t)rows * h->H() * kXSplit * 66, (size_t)rows * h->xenc_split * h->H() * d) * 4);
+    D.xml.ensure((size_t)rows * h->xenc_split * h->H() * 2 * 4);
+    D.dqp.ensure((size_t)rows * h->H() * d * e);
+    D.du.ensure((size_t)rows * h->H() * d * e);
+    D.xticket.ensure((size_t)rows * h->H() * 4);     // zeroed on allocation; combiners reset their slot
+    D.pids.ensure((size_t)rows * 4);
     D.logits.ensure((size_t)B * h->d.vocab * 4);
     D.nchunk = lm_head_partials(h->dt, (int)d, h->d.vocab);   // argmax partials per row of the LM head
     D.part_val.ensure((size_t)B * D.nchunk * 4);
@@ -852,6 +859,7 @@ struct StepCfg {
   int host_pos = -1;                   // decoder position of this step when known on the host (eager)
   const int* phys = nullptr;           // beam search: cache row of every key position [B][T]
   const BeamArgs* beam = nullptr;      // beam search selection (replaces the greedy select)
+  int rps = 1;                         // positions per decoder row in this pass (> 1: causal prefill)
 };
 
 // Decoder layers + LM head for rows [b0, b0 + nb) of the batch on stream `st_`: WhisperDecoder.forward
@@ -864,82 +872,87 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
   const size_t e = esize(h->d.dtype);
   int* ints = D.ints.as<int>();
   int* pos = ints + I_POS;
-  float* x = D.dx.as<float>() + (size_t)b0 * d;
-  char* x16 = (char*)D.dx16.p + (size_t)b0 * d * e;       // T copy of x: the LN-fused A operand
+  // prefill (c.rps > 1): every decoder row carries rps consecutive positions, rows (row, position)
+  // row-major; b0 / nb count decoder rows (KV-cache rows), r0 / M activation rows
+  const int rps = c.rps > 1 ? c.rps : 1, r0 = b0 * rps, M = nb * rps;
+  float* x = D.dx.as<float>() + (size_t)r0 * d;
+  char* x16 = (char*)D.dx16.p + (size_t)r0 * d * e;       // T copy of x: the LN-fused A operand
   const void* lna = h->ln16 ? x16 : nullptr;
   const int nbk = d / 16;
-  float* st = D.dstats.as<float>() + (size_t)b0 * nbk * 2;
+  float* st = D.dstats.as<float>() + (size_t)r0 * nbk * 2;
   float* st_pub = h->dec_gemm ? nullptr : st;   // LN partial sums only for the older skinny consumers
-  char* dq = (char*)D.dq.p + (size_t)b0 * d * e;
-  char* datt = (char*)D.datt.p + (size_t)b0 * d * e;
-  char* dffn = (char*)D.dffn.p + (size_t)b0 * h->d.ffn * e;
+  char* dq = (char*)D.dq.p + (size_t)r0 * d * e;
+  char* datt = (char*)D.datt.p + (size_t)r0 * d * e;
+  char* dffn = (char*)D.dffn.p + (size_t)r0 * h->d.ffn * e;
   const size_t cache_l = 2 * (size_t)B * H * T * 64;   // elements per layer (K then V)
   const int clips = c.clips ? c.clips : B;
   const size_t xkv_l = 2 * (size_t)clips * H * S * 64;
   for (int l = 0; l < L; ++l) {
     const LayerW& w = h->dec[l];
     char* cache = (char*)D.kvself.p + (l * cache_l + (size_t)b0 * H * T * 64) * e;
-    GemmArgs q = drow(x, d, w.qkv_w, nb, 3 * d, d, dq, d);   // LayerNorm fused (f32 A rows)
+    GemmArgs q = drow(x, d, w.qkv_w, M, 3 * d, d, dq, d);    // LayerNorm fused (f32 A rows)
     q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nbk; q.ln_a16 = lna;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
+    q.kv_rps = rps;
     dgemm(h, "dec_qkv", q, st_);
     AttnArgs a;
-    a.q = dq; a.ldq = d; a.q_Sb = 1; a.Sq = 1;
+    a.q = dq; a.ldq = d; a.q_Sb = rps; a.Sq = rps; a.causal = rps > 1;
     const char* cache0 = (char*)D.kvself.p + l * cache_l * e;   // K/V rows addressed absolutely
     a.k = cache0; a.v = cache0 + (size_t)B * H * T * 64 * e;
     a.k_sb = (long)H * T * 64; a.k_sh = (long)T * 64; a.k_sk = 64;
     a.row0 = b0; a.phys = c.phys; a.phys_ld = T;
-    a.o = datt; a.ldo = d; a.o_Sb = 1; a.B = nb; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1; a.kv_rows = T;
+    a.o = datt; a.ldo = d; a.o_Sb = rps; a.B = nb; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1;
+    a.kv_rows = rps == 1 ? T : 0;
     {
       const double t_keys = c.host_pos >= 0 ? c.host_pos + 1 : 0;   // keys this step (eager pass)
       h->timed("dec_self_attn", 4.0 * nb * H * t_keys * 64, nb * H * t_keys * 128.0 * e, st_,
                [&] { attention_decode(h->dt, a, st_); });
     }
-    GemmArgs o = drow(datt, d, w.o_w, nb, d, d, x, d);
+    GemmArgs o = drow(datt, d, w.o_w, M, d, d, x, d);
     o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st_pub; o.st_nb = nbk; o.out16 = x16;
     dgemm(h, "dec_out", o, st_);
     if (c.xmode == 1) {
       // cross attention in encoder space: q'_h = W_k,hᵀ q_h (block-diagonal GEMM, K = 64), one pass
       // over the encoder output per layer for all heads, range combine + W_v,h + b_v
-      char* dqp = (char*)D.dqp.p + (size_t)b0 * H * d * e;
+      char* dqp = (char*)D.dqp.p + (size_t)r0 * H * d * e;
       if (w.xqk_w) {   // q' = (W_k,hᵀ W_q,h) LN(x) + W_k,hᵀ b_q,h: one GEMM
-        GemmArgs xq = drow(x, d, w.xqk_w, nb, H * d, d, dqp, (long)H * d);
+        GemmArgs xq = drow(x, d, w.xqk_w, M, H * d, d, dqp, (long)H * d);
         xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
         xq.bias = w.xqk_b;
         dgemm(h, "dec_xq", xq, st_);
       } else {
-        GemmArgs xq = drow(x, d, w.xq_w, nb, d, d, dq, d);
+        GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
         xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
         xq.bias = w.xq_b;
         dgemm(h, "dec_xq", xq, st_);
-        GemmArgs kq = drow(dq, d, w.xkt_w, nb, H * d, 64, dqp, (long)H * d);
+        GemmArgs kq = drow(dq, d, w.xkt_w, M, H * d, 64, dqp, (long)H * d);
         kq.a_grp_n = d; kq.a_grp_off = 64;
         dgemm(h, "dec_kq", kq, st_);
       }
       XencArgs xa;
       xa.enc = h->xkv2[c.buf].p; xa.enc_sb = (long)S * d;
-      xa.row0 = b0; xa.rows_per_enc = c.nb;   // beams of a clip share its encoder output
-      xa.qp = dqp; xa.rows = nb; xa.H = H; xa.D = d; xa.S = S; xa.nsplit = h->xenc_split;
+      xa.row0 = r0; xa.rows_per_enc = c.nb * rps;   // beams (and prefill positions) of a clip share its encoder output
+      xa.qp = dqp; xa.rows = M; xa.H = H; xa.D = d; xa.S = S; xa.nsplit = h->xenc_split;
       xa.variant = h->xenc_variant;
-      xa.part = D.xpart.as<float>() + (size_t)b0 * h->xenc_split * H * d;
-      xa.ml = D.xml.as<float>() + (size_t)b0 * h->xenc_split * H * 2;
+      xa.part = D.xpart.as<float>() + (size_t)r0 * h->xenc_split * H * d;
+      xa.ml = D.xml.as<float>() + (size_t)r0 * h->xenc_split * H * 2;
       if (h->prof_stamps) {
         xa.stamp.base = h->stamps.as<unsigned long long>() + (size_t)c.buf * h->stamp_slots() * 2 * kStampSub;
         xa.stamp.pos = pos;
         xa.stamp.stride = L * wcb_handle::kMaxSub; xa.stamp.idx = l * wcb_handle::kMaxSub + chain;
       }
       // algorithmic bytes: every distinct clip's encoder output once (beams of a clip share it)
-      h->timed("dec_xattn", 4.0 * nb * H * (double)S * d, (double)nb / c.nb * S * d * e, st_,
+      h->timed("dec_xattn", 4.0 * M * H * (double)S * d, (double)nb / c.nb * S * d * e, st_,
                [&] { xenc_attention(h->dt, xa, st_); });
-      char* du = (char*)D.du.p + (size_t)b0 * H * d * e;
-      h->timed("dec_xmerge", 0, (double)nb * H * d * (h->xenc_split * 4.0 + e), st_,
+      char* du = (char*)D.du.p + (size_t)r0 * H * d * e;
+      h->timed("dec_xmerge", 0, (double)M * H * d * (h->xenc_split * 4.0 + e), st_,
                [&] { xenc_merge(h->dt, xa, du, (long)H * d, st_); });
-      GemmArgs vg = drow(du, (long)H * d, w.xv_w, nb, d, d, datt, d);   // o_h = W_v,h u_h + b_v,h
+      GemmArgs vg = drow(du, (long)H * d, w.xv_w, M, d, d, datt, d);    // o_h = W_v,h u_h + b_v,h
       vg.a_grp_n = 64; vg.a_grp_off = d; vg.bias = w.xv_b;
       dgemm(h, "dec_vg", vg, st_);
     } else {
       // cross attention over the precomputed encoder K/V
-      GemmArgs xq = drow(x, d, w.xq_w, nb, d, d, dq, d);
+      GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
       xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
       xq.bias = w.xq_b;
       dgemm(h, "dec_xq", xq, st_);
@@ -947,34 +960,35 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       const char* xkv = (const char*)h->xkv2[c.buf].p + l * xkv_l * e;
       xa.q = dq; xa.ldq = d; xa.q_Sb = 1; xa.Sq = 1;
       xa.k = xkv; xa.v = xkv + (size_t)clips * H * S * 64 * e;
-      xa.row0 = b0; xa.b_div = c.nb;           // beams of a clip share its cross K/V
+      xa.row0 = r0; xa.b_div = c.nb * rps;     // beams (and prefill positions) of a clip share its cross K/V
       xa.k_sb = (long)H * S * 64; xa.k_sh = (long)S * 64; xa.k_sk = 64;
-      xa.o = datt; xa.ldo = d; xa.o_Sb = 1; xa.B = nb; xa.H = H; xa.nkeys = S;
-      xa.nsplit = h->xsplit; xa.part = D.xpart.as<float>() + (size_t)b0 * H * kXSplit * 66;
-      xa.ticket = D.xticket.as<int>() + (size_t)b0 * H;
+      xa.o = datt; xa.ldo = d; xa.o_Sb = 1; xa.B = M; xa.H = H; xa.nkeys = S;
+      xa.nsplit = h->xsplit; xa.part = D.xpart.as<float>() + (size_t)r0 * H * kXSplit * 66;
+      xa.ticket = D.xticket.as<int>() + (size_t)r0 * H;
       xa.variant = h->xvariant;   // fixed per handle: the same clip decodes alike in any batch
       if (h->prof_stamps) {
         xa.stamp.base = h->stamps.as<unsigned long long>() + (size_t)c.buf * h->stamp_slots() * 2 * kStampSub;
         xa.stamp.pos = pos;
         xa.stamp.stride = L * wcb_handle::kMaxSub; xa.stamp.idx = l * wcb_handle::kMaxSub + chain;
       }
-      h->timed("dec_xattn", 4.0 * nb * H * (double)S * 64, (double)nb / c.nb * H * S * 128.0 * e, st_,
+      h->timed("dec_xattn", 4.0 * M * H * (double)S * 64, (double)nb / c.nb * H * S * 128.0 * e, st_,
                [&] { attention_decode(h->dt, xa, st_); });
     }
-    GemmArgs xo = drow(datt, d, w.xo_w, nb, d, d, x, d);
+    GemmArgs xo = drow(datt, d, w.xo_w, M, d, d, x, d);
     xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st_pub; xo.st_nb = nbk; xo.out16 = x16;
     dgemm(h, "dec_xo", xo, st_);
     // MLP
-    GemmArgs f1 = drow(x, d, w.fc1_w, nb, h->d.ffn, d, dffn, h->d.ffn);
+    GemmArgs f1 = drow(x, d, w.fc1_w, M, h->d.ffn, d, dffn, h->d.ffn);
     f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nbk; f1.ln_a16 = lna;
     f1.bias = w.fc1_b; f1.act = 1;
     dgemm(h, "dec_fc1", f1, st_);
-    GemmArgs f2 = drow(dffn, h->d.ffn, w.fc2_w, nb, d, h->d.ffn, x, d);
+    GemmArgs f2 = drow(dffn, h->d.ffn, w.fc2_w, M, d, h->d.ffn, x, d);
     f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st_pub; f2.st_nb = nbk; f2.out16 = x16;
     dgemm(h, "dec_fc2", f2, st_);
   }
   if (c.lm_head) {
-    GemmArgs lm = drow(x, d, h->tok_emb, nb, h->d.vocab, d, c.logits_out + (size_t)b0 * c.logits_ld, c.logits_ld);
+    GemmArgs lm = drow(x, d, h->tok_emb, M, h->d.vocab, d, c.logits_out + (size_t)b0 * c.logits_ld, c.logits_ld);
+    if (rps > 1) { lm.ldc = h->d.vocab; lm.c_Mb = rps; lm.c_strideB = c.logits_ld; }   // row (b, t) → b·ld + t·V
     lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b; lm.st_in = st; lm.st_nb = nbk; lm.ln_a16 = lna;
     lm.out_f32 = 1;
     if (c.select && !c.beam) {   // argmax partials with the root boost + EOS mask fused into the LM head
@@ -1044,6 +1058,29 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
   }
 }
 
+// Causal prefill of np positions (*pos .. *pos + np - 1) of every decoder row in ONE pass of the
+// decoder (prompt tokens / teacher forcing): ids from src[row·ld + position] (ld 0: one prefix shared
+// by every row), rows (row, position) row-major, the KV cache written at those positions, the
+// self-attention causal over the cache, the cross-attention rows mapped to their clip; LM head on
+// every row when c.lm_head. Advances *pos by np. Eager (its shapes change with np).
+void prefill_step(wcb_handle* h, StepCfg c, int np, const int* src, int ld) {
+  DecCtx& D = h->dc[c.buf];
+  const int d = h->d.d_model, R = c.B, M = R * np;
+  int* ints = D.ints.as<int>();
+  int* pos = ints + I_POS;
+  c.rps = np;
+  c.select = false;
+  c.phys = nullptr;   // prompt keys: every row's own cache row (beam_init's identity map)
+  c.beam = nullptr;
+  h->timed("dec_embed", 0, (double)M * d * (2.0 * esize(h->d.dtype) + 4), D.hs, [&] {
+    prefill_ids(D.pids.as<int>(), src, R, np, ld, pos, D.hs);
+    embed(h->dt, h->tok_emb, h->dec_pos, D.pids.as<int>(), pos, D.dx.as<float>(), nullptr, M, d, D.hs, D.dx16.p,
+          h->d.vocab, np);
+  });
+  decode_rows(h, c, 0, R, 0, D.hs);
+  add_i32(pos, np, D.hs);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1102,7 +1139,7 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     }
     ensure_enc_ws(h, B);
     const int xm = nb > 1 ? h->beam_xmode : h->xmode;   // this call's cross-attention formulation
-    ensure_dec_ws(h, B, R, Tc, out_ld, xm);
+    ensure_dec_ws(h, B, R, Tc, out_ld, xm, P > 1 ? R * std::min(prefill_chunk(R), P - 1) : R);
     const int buf = h->gen_count++ % h->nctx;
     DecCtx& D = h->dc[buf];
     // beam state [R] / [R][max_new] / [R][Tc] / [R][K] / [B][2] in one buffer
@@ -1159,7 +1196,13 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     sc.nb = nb;
     sc.xmode = xm;
     if (nb > 1) { sc.phys = bm.phys; sc.beam = &bm; }
-    for (int p = 0; p + 1 < P; ++p) decode_step(h, sc);   // prompt prefill, teacher-forced
+    // prompt positions 0 .. P-2 in causal prefill passes, then the last prompt token is the first
+    // decode step's input
+    for (int p0 = 0, np; p0 + 1 < P; p0 += np) {
+      np = std::min(prefill_chunk(R), P - 1 - p0);
+      prefill_step(h, sc, np, D.forced.as<int>(), 0);
+    }
+    if (P > 1) gather_col(ints + I_NEXT, D.forced.as<int>(), R, 0, P - 1, D.hs);
     sc.lm_head = true;
     sc.select = true;
     char key[256];
@@ -1256,10 +1299,9 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
     REQUIRE(B <= 64, "batch > 64 per handle");
     REQUIRE(T <= h->d.n_text_ctx, "decoder_input_ids longer than max_target_positions");
     ensure_enc_ws(h, B);
-    ensure_dec_ws(h, B, B, T, 1, h->xmode);
+    ensure_dec_ws(h, B, B, T, 1, h->xmode, B * std::min(prefill_chunk(B), T));
     const int buf = h->gen_count++ % h->nctx;
     DecCtx& D = h->dc[buf];
-    if ((size_t)B * (T + 1) * 4 > D.forced.bytes) { quiesce(h); D.forced.ensure((size_t)B * (T + 1) * 4); }
     sync_in(h, stream, h->he);
     HIPCHK(hipStreamWaitEvent(h->he, h->ev_dec[buf], 0));
     const size_t enc_bytes = (size_t)B * h->S() * h->d.d_model * esize(h->d.dtype);
@@ -1275,16 +1317,13 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
     HIPCHK(hipStreamWaitEvent(D.hs, h->ev_xkv[buf], 0));
     int* ints = D.ints.as<int>();
     HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 4 * B) * 4, D.hs));
-    gather_col(ints + I_NEXT, dec_ids, B, T, 0, D.hs);
-    // forced column T is never read: feed positions 0..T-1 (advance reads column pos+1 < T except last)
-    HIPCHK(hipMemsetAsync(D.forced.p, 0, (size_t)B * (T + 1) * 4, D.hs));
-    HIPCHK(hipMemcpy2DAsync(D.forced.p, (size_t)(T + 1) * 4, dec_ids, (size_t)T * 4, (size_t)T * 4, B,
-                            hipMemcpyDeviceToDevice, D.hs));
-    for (int t = 0; t < T; ++t) {
-      StepCfg sc{B, T, 1, buf, true, false, logits + (size_t)t * h->d.vocab, (long)T * h->d.vocab, nullptr, 0.f, 0,
-                 D.forced.as<int>(), T + 1};
+    // teacher forcing = causal prefill of all T positions, logits of every position
+    for (int p0 = 0, np; p0 < T; p0 += np) {
+      np = std::min(prefill_chunk(B), T - p0);
+      StepCfg sc{B, T, 1, buf, true, false, logits + (size_t)p0 * h->d.vocab, (long)T * h->d.vocab, nullptr, 0.f,
+                 0, nullptr, 0};
       sc.xmode = h->xmode;
-      decode_step(h, sc);
+      prefill_step(h, sc, np, dec_ids, T);
     }
     HIPCHK(hipEventRecord(h->ev_dec[buf], D.hs));
     sync_out(h, stream, D.hs);
