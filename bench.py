@@ -156,7 +156,7 @@ def main():
     dims = get_dims(args.model)
     # ---- weights: rank 0 generates, one RCCL broadcast of the packed bf16 blob over xGMI
     t0 = time.perf_counter()
-    sd = broadcast_weights(dims, dev, seed=0)
+    sd = broadcast_weights(dims, dev, seed=0, views=True)   # device views: no host round trip
     if world > 1:
         torch.cuda.synchronize()
         log(f"rank {rank}: weights broadcast in {time.perf_counter() - t0:.3f} s")
@@ -353,7 +353,7 @@ def main():
                                    f"{'greedy' if args.num_beams == 1 else f'beam-{args.num_beams}'} decode, "
                                    f"{args.bias_phrases}-phrase bias boost lambda={args.boost}",
                        "num_beams": args.num_beams, "global_batch": world * B, "parallelism": f"utterance-dp{world}",
-                       "hipgraph_decode": use_graph, "batches_in_flight": (int(os.environ.get("WCB_DECODE_CTX", "2")) + 1) if overlap else 1},
+                       "hipgraph_decode": use_graph, "batches_in_flight": 3 if overlap else 1},
             "rtf": round(1.0 / (value / world), 6),
             "roofline": roof,
             "roofline_other": others or None,

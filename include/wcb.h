@@ -57,12 +57,33 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out);
 void wcb_destroy(wcb_handle* h);
 const char* wcb_last_error(const wcb_handle* h);
 
-/* replaces from_pretrained / load_state_dict: one HF state-dict tensor (host f32, C order).
- * Names follow the reference's state dict (model.encoder.layers.{i}.self_attn.q_proj.weight, ...).
- * proj_out.weight is tied to model.decoder.embed_tokens.weight (models/whisper_medical.py:14). */
+/* alternative formulations the tests compare (defaults are fixed per model; no environment variables):
+ *   "xmode" 0/1        decoder cross-attention over per-layer K/V, or in encoder space (before finalize)
+ *   "beam_xmode" 0/1   the same for beam search (before finalize)
+ *   "group_rows" n     decoder rows per layer chain (16..512)
+ *   "xenc_variant" v   encoder-space kernel variant, "xvariant" v  K/V cross-attention kernel variant */
+int wcb_set_option(wcb_handle* h, const char* name, int value);
+
+/* replaces from_pretrained / load_state_dict: one HF state-dict tensor (host f32, C order), staged
+ * on the device. Names follow the reference's state dict (model.encoder.layers.{i}.self_attn.q_proj.weight,
+ * ...). proj_out.weight is tied to model.decoder.embed_tokens.weight (models/whisper_medical.py:14). */
 int wcb_set_weight(wcb_handle* h, const char* name, const float* data, const int64_t* shape, int ndim);
-/* repack every tensor into the device layout (fused QKV, q pre-scaled, im2col conv weights,
- * all-layer cross-KV projection) and upload; host copies are released. */
+
+/* a BORROWED device tensor (e.g. a torch CUDA tensor or a view into an RCCL-broadcast blob) */
+typedef struct wcb_tensor_view {
+  const char* name;     /* HF state-dict name */
+  const void* data;     /* device pointer of element [0,...,0] */
+  int dtype;            /* wcb_dtype of the elements */
+  int ndim;             /* 1..4 */
+  int64_t shape[4];
+  int64_t stride[4];    /* in elements */
+} wcb_tensor_view;
+/* stages n device tensors without a host round trip (gathered and widened to f32 on the device, on
+ * `stream`); the views are not read after the call returns. Mixes freely with wcb_set_weight. */
+int wcb_load_weights(wcb_handle* h, const wcb_tensor_view* views, int n, void* stream);
+/* build the device layouts from the staged tensors on the device (fused QKV with q pre-scaled,
+ * im2col conv weights, W_k,hᵀ panels, all-layer cross-KV stack), rounded once to the model dtype;
+ * staging buffers are released. */
 int wcb_finalize_weights(wcb_handle* h);
 
 /* replaces WhisperFeatureExtractor.__call__ (data_utils/data_loader.py:171-172):
@@ -156,7 +177,7 @@ int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void*
  * q [B][H*64] (pre-scaled by 1/8), enc [B][S][d], wkt = W_k repacked [H][d][64] (element (h,c,i) =
  * W_k[h*64+i][c]), wv [d][d] (HF layout), bv f32 [d]; nsplit key ranges per row (1..16). 16-bit dtypes. */
 int wcb_op_cross_attention_enc(int dtype, const void* q, const void* enc, const void* wkt, const void* wv,
-                               const float* bv, void* o, int B, int H, int S, int nsplit, void* stream);
+                               const float* bv, void* o, int B, int H, int S, int nsplit, int variant, void* stream);
 
 /* Bias-weighted cross entropy — replaces the loss block of
  * WhisperForConditionalGenerationWeightCE.forward (models/whisper_medical.py:113-156): weight

@@ -4,7 +4,7 @@
 * boost / MinNewTokens / prompt prefix / more than 64 rows (row groups): identical to the oracle
   (oracle/beam_np.py) in f32 mode — parity vs the reference unpinned for the boost (no reference code).
 * bf16, both cross-attention formulations for beams (default: precomputed per-clip cross-K/V shared by
-  the beams, b_div; WCB_BEAM_XMODE=1: encoder space, rows_per_enc = beams): batch invariance (every utterance
+  the beams, b_div; option beam_xmode = 1: encoder space, rows_per_enc = beams): batch invariance (every utterance
   decoded alone gives the same beams as in the batch: the row maps and the shared encoder rows are
   exact) and identical to the oracle on the high-margin recipe.
 """
@@ -38,30 +38,12 @@ def case(size, seed, recipe, B):
     return _CASES[key]
 
 
-class _env:
-    """Set environment variables the library reads when a handle is created."""
-    def __init__(self, **kv):
-        self.kv, self.old = kv, {}
-
-    def __enter__(self):
-        for k, v in self.kv.items():
-            self.old[k] = os.environ.get(k)
-            os.environ[k] = v
-
-    def __exit__(self, *a):
-        for k, v in self.old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-
 def model(size, seed, recipe, dtype, beam_xmode="0"):
     key = (size, seed, recipe, dtype, beam_xmode)
     if key not in _MODELS:
         dims = get_dims(size)
-        with _env(WCB_BEAM_XMODE=beam_xmode):
-            _MODELS[key] = WhisperCB.from_state_dict(dims, make_weights(dims, seed=seed, recipe=recipe), dtype=dtype)
+        _MODELS[key] = WhisperCB.from_state_dict(dims, make_weights(dims, seed=seed, recipe=recipe), dtype=dtype,
+                                                 options={"beam_xmode": int(beam_xmode)})
     return _MODELS[key]
 
 
@@ -109,10 +91,10 @@ def test_beam_natural_eos_matches_oracle_f32():
 @pytest.mark.parametrize("group_rows", ["512", "64"])
 def test_beam_row_groups_match_oracle_f32(group_rows):
     """16 clips x 5 beams = 80 decoder rows: one 80-row chain (default), or two row groups on
-    parallel streams (WCB_GROUP_ROWS=64)."""
+    parallel streams (option group_rows = 64)."""
     dims, om, mel, enc = case("micro", 0, "diverse", 16)
-    with _env(WCB_GROUP_ROWS=group_rows):
-        m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=0, recipe="diverse"), dtype="f32")
+    m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=0, recipe="diverse"), dtype="f32",
+                                  options={"group_rows": int(group_rows)})
     ids = m.generate(torch.from_numpy(mel), max_length=16, num_beams=5).cpu().numpy()
     ref = generate_beam(om, enc=enc, num_beams=5, max_length=16)
     assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
@@ -140,13 +122,13 @@ def test_beam_bf16_batch_invariant_and_high_margin(beam_xmode):
     assert ids.shape == ref.shape and np.array_equal(ids, ref), (ids, ref)
 
 
-def _one_layer(size, seed, recipe, B, dtype, beam_xmode="0"):
+def _one_layer(size, seed, recipe, B, dtype, beam_xmode="0", group_rows=512):
     dims = get_dims(size, n_layers=1)
     sd = make_weights(dims, seed=seed, recipe=recipe)
     om = W.OracleModel.from_dims(dims, sd)
     mel = W.log_mel(synth_batch(B), dims.n_mel)
-    with _env(WCB_BEAM_XMODE=beam_xmode):
-        return dims, om, mel, WhisperCB.from_state_dict(dims, sd, dtype=dtype)
+    return dims, om, mel, WhisperCB.from_state_dict(dims, sd, dtype=dtype,
+                                                    options={"beam_xmode": int(beam_xmode), "group_rows": group_rows})
 
 
 def _batch_invariant(m, x, **kw):
@@ -176,8 +158,8 @@ def test_beam_c3_shape_bf16_row_groups(beam_xmode, group_rows):
     """C3 shape (medium layer: d = 1024; per-clip cross-K/V or encoder-space cross-attention) with 13
     clips x 5 beams = 65 decoder rows (two row groups): batch-invariant, and identical to the oracle on
     the high-margin recipe."""
-    with _env(WCB_GROUP_ROWS=group_rows):   # one 65-row chain, or two chains on parallel streams
-        dims, om, mel, m = _one_layer("medium", 1, "margin", 13, "bf16", beam_xmode)
+    # one 65-row chain, or two chains of row groups
+    dims, om, mel, m = _one_layer("medium", 1, "margin", 13, "bf16", beam_xmode, int(group_rows))
     x = torch.from_numpy(mel)
     ids = _batch_invariant(m, x, max_length=8, num_beams=5)
     ref = generate_beam(om, mel=mel, num_beams=5, max_length=8)

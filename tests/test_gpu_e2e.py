@@ -151,15 +151,7 @@ def test_greedy_bf16_kv_formulation_high_margin_exact():
     g = np.load(os.path.join(GOLD, "model_tiny.en_margin_s1.npz"))
     ref = g["greedy_ids"]
     dims, sd, om, mel, enc = case("tiny.en", 1, "margin", ref.shape[0])
-    old = os.environ.get("WCB_XMODE")
-    os.environ["WCB_XMODE"] = "0"
-    try:
-        m = WhisperCB.from_state_dict(dims, sd, dtype="bf16")
-    finally:
-        if old is None:
-            os.environ.pop("WCB_XMODE")
-        else:
-            os.environ["WCB_XMODE"] = old
+    m = WhisperCB.from_state_dict(dims, sd, dtype="bf16", options={"xmode": 0})
     ids = m.generate(torch.from_numpy(mel), max_length=ref.shape[1]).cpu().numpy()
     assert np.array_equal(ids, ref)
 
@@ -208,3 +200,44 @@ def test_generate_splits_batches_above_64_clips():
     assert ids.shape == (70, w) and np.array_equal(ids, np.concatenate([pad(a), pad(b)]))
     beams = m.generate(mel[:70], max_length=6, num_beams=8).cpu().numpy()   # 512 / 8 = 64 clips per call
     assert beams.shape[0] == 70
+
+
+def test_device_weight_views_match_host_upload():
+    """wcb_load_weights: the state dict as borrowed device tensors (bf16 blob views, f32 and f16
+    tensors, non-contiguous strides) stages on the device without a host round trip and yields the
+    same model as the host f32 upload: identical greedy ids and bit-identical logits (f32 mode)."""
+    dims, sd, om, mel, enc = case("micro", 0, "diverse", 2)
+    host = WhisperCB.from_state_dict(dims, sd, dtype="f32")
+    dev = {}
+    for i, (n, a) in enumerate(sd.items()):
+        t = torch.from_numpy(np.asarray(a, dtype=np.float32)).cuda()
+        if i % 3 == 1 and t.dim() == 2:
+            t = t.t().contiguous().t()                 # same values, column-major strides
+        elif i % 3 == 2:
+            t = t.to(torch.float16) if np.all(np.asarray(a, np.float32) == np.asarray(a, np.float16)) else t
+        dev[n] = t
+    viewed = WhisperCB.from_state_dict(dims, dev, dtype="f32")
+    x = torch.from_numpy(mel)
+    a = host.generate(x, max_length=12, min_new_tokens=12).cpu().numpy()
+    b = viewed.generate(x, max_length=12, min_new_tokens=12).cpu().numpy()
+    assert np.array_equal(a, b)
+    ids = torch.from_numpy(np.concatenate([np.full((2, 1), dims.decoder_start_token_id), a[:, :5]], 1))
+    la = host.forward(x, decoder_input_ids=ids).logits
+    lb = viewed.forward(x, decoder_input_ids=ids).logits
+    assert torch.equal(la, lb)
+
+
+def test_broadcast_blob_views_load_without_host_copy():
+    """The bench's path: the packed bf16 blob (what the RCCL broadcast delivers) unpacked as device
+    views and loaded through wcb_load_weights equals loading the same bf16-rounded values from host."""
+    from whisper_context_biasing_amd.shard import pack_state_dict, unpack_state_dict, unpack_state_dict_views
+    dims = get_dims("micro")
+    sd = make_weights(dims, seed=0, recipe="diverse")
+    flat = pack_state_dict(dims, sd).cuda()
+    views = unpack_state_dict_views(dims, flat)
+    assert all(v.is_cuda and v.dtype == torch.bfloat16 for v in views.values())
+    m1 = WhisperCB.from_state_dict(dims, views, dtype="bf16")
+    m2 = WhisperCB.from_state_dict(dims, unpack_state_dict(dims, flat), dtype="bf16")
+    x = torch.from_numpy(W.log_mel(synth_batch(2), dims.n_mel))
+    assert np.array_equal(m1.generate(x, max_length=10, min_new_tokens=10).cpu().numpy(),
+                          m2.generate(x, max_length=10, min_new_tokens=10).cpu().numpy())

@@ -172,14 +172,15 @@ def test_log_mel_matches_oracle(n_mel):
     assert np.abs(got_s - ref_s).max() < 2e-4
 
 
-def _xattn_enc(dt, q, enc, wk, wv, bv, nsplit):
+def _xattn_enc(dt, q, enc, wk, wv, bv, nsplit, variant=1):
     lib = _lib.load()
     B, S, d = enc.shape
     H = d // 64
     wkt = wk.view(H, 64, d).transpose(1, 2).contiguous()     # [H][d][64]: (h, c, i) = W_k[h*64+i][c]
     o = torch.empty(B, d, dtype=enc.dtype, device="cuda")
     _lib.check(lib.wcb_op_cross_attention_enc(DT[dt][1], q.data_ptr(), enc.data_ptr(), wkt.data_ptr(), wv.data_ptr(),
-                                              bv.data_ptr(), o.data_ptr(), B, H, S, nsplit, _s()), None, "xattn_enc")
+                                              bv.data_ptr(), o.data_ptr(), B, H, S, nsplit, variant, _s()), None,
+               "xattn_enc")
     torch.cuda.synchronize()
     return o
 
@@ -188,11 +189,10 @@ def _xattn_enc(dt, q, enc, wk, wv, bv, nsplit):
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
 @pytest.mark.parametrize("d,B,S,nsplit", [(768, 32, 1500, 8), (768, 5, 1500, 1), (384, 3, 1500, 16), (64, 2, 1500, 3),
                                           (1024, 2, 1500, 8), (512, 4, 100, 4), (768, 3, 37, 2), (384, 1, 1, 1)])
-def test_cross_attention_encoder_space(dt, d, B, S, nsplit, variant, monkeypatch):
+def test_cross_attention_encoder_space(dt, d, B, S, nsplit, variant):
     """Encoder-space cross-attention (k_xenc.hip, both chunk-ring variants) vs the K/V formulation of the
     reference ([tf] modeling_whisper.py:284-356): K = enc W_kᵀ (no bias), V = enc W_vᵀ + b_v, softmax(q Kᵀ) V
     in fp64."""
-    monkeypatch.setenv("WCB_XENC_VARIANT", variant)
     g = torch.Generator(device="cpu").manual_seed(d + B * 7 + S)
     H = d // 64
     tdt = DT[dt][0]
@@ -201,7 +201,7 @@ def test_cross_attention_encoder_space(dt, d, B, S, nsplit, variant, monkeypatch
     wk = (torch.randn(d, d, generator=g) / d ** 0.5 * 2).to(tdt).cuda()
     wv = (torch.randn(d, d, generator=g) / d ** 0.5).to(tdt).cuda()
     bv = torch.randn(d, generator=g).float().cuda()
-    o = _xattn_enc(dt, q, enc, wk, wv, bv, nsplit)
+    o = _xattn_enc(dt, q, enc, wk, wv, bv, nsplit, int(variant))
     K = enc.double() @ wk.double().T
     V = enc.double() @ wv.double().T + bv.double()
     qh = q.double().view(B, 1, H, 64).transpose(1, 2)
@@ -213,7 +213,7 @@ def test_cross_attention_encoder_space(dt, d, B, S, nsplit, variant, monkeypatch
     tol = 3e-2 if dt == "bf16" else 5e-3
     err = (o.double() - ref).abs().max().item()
     assert err < tol * max(1.0, ref.abs().max().item()), err
-    assert torch.equal(_xattn_enc(dt, q, enc, wk, wv, bv, nsplit), o)   # deterministic
+    assert torch.equal(_xattn_enc(dt, q, enc, wk, wv, bv, nsplit, int(variant)), o)   # deterministic
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])

@@ -28,6 +28,11 @@ class WcbGenCfg(C.Structure):
                 ("bias_boost", C.c_float), ("use_graph", C.c_int), ("async_out", C.c_int)]
 
 
+class WcbTensorView(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("data", C.c_void_p), ("dtype", C.c_int), ("ndim", C.c_int),
+                ("shape", C.c_int64 * 4), ("stride", C.c_int64 * 4)]
+
+
 # name -> (restype, argtypes)
 _P = C.c_void_p
 SIGNATURES = {
@@ -35,6 +40,7 @@ SIGNATURES = {
     "wcb_destroy": (None, [_P]),
     "wcb_last_error": (C.c_char_p, [_P]),
     "wcb_set_weight": (C.c_int, [_P, C.c_char_p, _P, C.POINTER(C.c_int64), C.c_int]),
+    "wcb_load_weights": (C.c_int, [_P, C.POINTER(WcbTensorView), C.c_int, _P]),
     "wcb_finalize_weights": (C.c_int, [_P]),
     "wcb_log_mel": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int64, _P, _P]),
     "wcb_encode": (C.c_int, [_P, _P, C.c_int, _P, _P]),
@@ -65,7 +71,8 @@ SIGNATURES = {
     "wcb_op_attention": (C.c_int, [C.c_int, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.c_int, _P]),
     "wcb_op_cross_attention_enc": (C.c_int, [C.c_int, _P, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int,
-                                             C.c_int, _P]),
+                                             C.c_int, C.c_int, _P]),
+    "wcb_set_option": (C.c_int, [_P, C.c_char_p, C.c_int]),
 }
 
 

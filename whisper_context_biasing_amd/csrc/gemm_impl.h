@@ -1003,11 +1003,6 @@ static void launch_skinny_k(const GemmArgs& g, hipStream_t s) {
 template <typename T, int MF, int NF>
 static bool launch_skinny_mf(const GemmArgs& g, hipStream_t s) {
   const int K = g.K;
-  // WCB_SK_NW: preferred waves per workgroup where an instance exists for K (experiments)
-  static const int sk_nw = [] { const char* v = getenv("WCB_SK_NW"); return v ? atoi(v) : 0; }();
-#define WCB_SKP(nw, ks) if (sk_nw == nw && K == nw * ks * 32) { launch_skinny_k<T, MF, NF, nw, ks>(g, s); return true; }
-  WCB_SKP(4, 6) WCB_SKP(12, 2) WCB_SKP(8, 12) WCB_SKP(12, 8) WCB_SKP(4, 24)
-#undef WCB_SKP
 #define WCB_SK(nw, ks) if (K == nw * ks * 32) { launch_skinny_k<T, MF, NF, nw, ks>(g, s); return true; }
   WCB_SK(1, 1) WCB_SK(1, 2) WCB_SK(2, 2) WCB_SK(4, 2) WCB_SK(4, 3) WCB_SK(4, 4) WCB_SK(8, 2)
   WCB_SK(8, 3) WCB_SK(8, 4) WCB_SK(8, 5) WCB_SK(8, 6) WCB_SK(16, 4) WCB_SK(16, 5) WCB_SK(16, 6)
@@ -1016,41 +1011,27 @@ static bool launch_skinny_mf(const GemmArgs& g, hipStream_t s) {
   return false;
 }
 
-static inline bool dec_enabled() {
-  static const int on = [] { const char* v = getenv("WCB_DEC"); return v ? atoi(v) : 1; }();
-  return on != 0;
-}
-
 template <typename T>
 static void gemm_t(const GemmArgs& g, hipStream_t s) {
   if ((g.M <= 64 || g.mode == 2 || g.ln_w || g.skinny) && g.mode != 1 && !g.addrow) {
-    // decode GEMM: WCB_DEC_MF=1 / 2 forces 16- / 32-row workgroups; WCB_DEC=0 keeps the older skinny kernel
-    static const int dec_mf = [] { const char* v = getenv("WCB_DEC_MF"); return v ? atoi(v) : 0; }();
-    if (dec_enabled()) {
-      // 16-row workgroups up to 64 rows (measured C2: 1.074 vs 1.147 ms/token with 32-row workgroups)
-      // The LM head walks the vocabulary persistently: 32-row workgroups read every weight tile once
-      const bool mf1 = dec_mf == 1 || (dec_mf == 0 && g.M <= 64 && !(g.sel_val && g.M > 16)) || g.K >= 4096;
-      const bool ok = mf1 ? launch_dec_mf<T, 1>(g, s) : launch_dec_mf<T, 2>(g, s);
-      if (ok) return;
-    }
+    // decode GEMM (K in its table; else the older skinny kernel below): 16-row workgroups up to 64
+    // rows (measured C2: 1.074 vs 1.147 ms/token with 32-row workgroups); the LM head walks the
+    // vocabulary persistently with 32-row workgroups, reading every weight tile once
+    const bool mf1 = (g.M <= 64 && !(g.sel_val && g.M > 16)) || g.K >= 4096;
+    const bool ok = mf1 ? launch_dec_mf<T, 1>(g, s) : launch_dec_mf<T, 2>(g, s);
+    if (ok) return;
   }
   if (g.M <= 64 || g.mode == 2 || g.ln_w || g.skinny) {
     // rows per workgroup: up to 16·sk_mf; larger M is split over grid.y (more workgroups, less A
-    // traffic per CU) — WCB_SK_MF = 1, 2 or 4 overrides the automatic choice
+    // traffic per CU)
     // Default (auto): 16 rows per workgroup up to 32 rows (C2 greedy: measured best), 32 up to 160
     // (C5 80 beam rows: 983 -> 1075 audio-s/s), 64 beyond (C3 320 beam rows: 2217 -> 2437): with many
     // rows the A re-read per column block, not the weight stream, dominates
-    static const int sk_mf = [] { const char* v = getenv("WCB_SK_MF"); return v ? atoi(v) : 0; }();
-    const int mf = sk_mf <= 0 ? (g.M <= 32 ? 1 : g.M <= 160 ? 2 : 4)
-                              : (g.M <= 16 || sk_mf <= 1 ? 1 : (g.M <= 32 || sk_mf == 2) ? 2 : 4);
+    const int mf = g.M <= 32 ? 1 : g.M <= 160 ? 2 : 4;
     bool ok;
     if (g.sel_val) {   // LM head: 64 columns per workgroup (A re-read 4x less), fused argmax partial
-      // WCB_LM_MF: rows per workgroup for the LM head alone (its 79.7 MB weight stream is re-read by
-      // every row block, from another XCD's L2 or HBM). The argmax-partial epilogue needs BNC = 64.
-      static const int lm_mf = [] { const char* v = getenv("WCB_LM_MF"); return v ? atoi(v) : 0; }();
-      const int lmf = lm_mf <= 0 ? mf : (g.M <= 16 || lm_mf <= 1) ? 1 : (g.M <= 32 || lm_mf == 2) ? 2 : 4;
-      if (lmf == 1) ok = launch_skinny_mf<T, 1, 4>(g, s);
-      else if (lmf == 2) ok = launch_skinny_mf<T, 2, 4>(g, s);
+      if (mf == 1) ok = launch_skinny_mf<T, 1, 4>(g, s);
+      else if (mf == 2) ok = launch_skinny_mf<T, 2, 4>(g, s);
       else ok = launch_skinny_mf<T, 4, 4>(g, s);
     } else if (mf == 1) ok = launch_skinny_mf<T, 1, 1>(g, s);
     else if (mf == 2) ok = launch_skinny_mf<T, 2, 1>(g, s);
@@ -1058,20 +1039,14 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
     if (!ok) fprintf(stderr, "wcb: no skinny GEMM instance for K=%d\n", g.K);
     return;
   }
-  // 16-bit encoder-size GEMMs: the LDS-ring kernel (tile by WCB_GEMM_TILE for experiments);
-  // f32 ("exact" mode) and small shapes: the two-stage tile kernel, 128x128 (4 waves 2x2) when N
-  // fills it, else 128x64.
-  // Default: 256x256 (2 stages) when N allows it (measured 1128 vs 990 TFLOP/s at 48000x2304x768
-  // class shapes), else 256x128 (3 stages).
-  static const int variant = [] { const char* v = getenv("WCB_GEMM_TILE"); return v ? atoi(v) : -1; }();
+  // 16-bit encoder-size GEMMs: the LDS-ring kernel, 256x256 (2 stages) when N allows it (measured
+  // 1128 vs 990 TFLOP/s at 48000x2304x768 class shapes), else 256x128 (3 stages); f32 ("exact"
+  // mode) and small shapes: the two-stage tile kernel, 128x128 (4 waves 2x2) when N fills it, else 128x64.
   if constexpr (sizeof(T) == 2) {
-    if (variant != 0 && g.N % 128 == 0 && g.M >= 4096) {
-      switch (variant < 0 ? (g.N % 256 == 0 ? 2 : 1) : variant) {
-        case 2: launch_ring<T, 256, 256, 2, 4, 2>(g, s); return;
-        case 3: launch_ring<T, 128, 128, 2, 2, 4>(g, s); return;
-        case 4: launch_ring<T, 128, 256, 2, 4, 3>(g, s); return;
-        default: launch_ring<T, 256, 128, 4, 2, 3>(g, s); return;
-      }
+    if (g.N % 128 == 0 && g.M >= 4096) {
+      if (g.N % 256 == 0) launch_ring<T, 256, 256, 2, 4, 2>(g, s);
+      else launch_ring<T, 256, 128, 4, 2, 3>(g, s);
+      return;
     }
   }
   if (g.N % 128 == 0) launch_tile<T, 128, 128, 2, 2>(g, s);

@@ -1,6 +1,5 @@
 // GEMM dispatch by element type; kernels and tiling live in gemm_impl.h.
 #include <algorithm>
-#include <cstdlib>
 
 #include "kernels.h"
 
@@ -10,9 +9,8 @@ void gemm_f16(const GemmArgs& g, hipStream_t s);
 void gemm_f32(const GemmArgs& g, hipStream_t s);
 
 bool gemm_dec_supported(DType t, int K) {
-  static const int on = [] { const char* v = getenv("WCB_DEC"); return v ? atoi(v) : 1; }();
   (void)t;
-  return on && (K == 64 || K == 128 || K == 256 || K == 384 || K == 512 || K == 768 || K == 1024 || K == 1280);
+  return K == 64 || K == 128 || K == 256 || K == 384 || K == 512 || K == 768 || K == 1024 || K == 1280;
 }
 
 int lm_head_partials(DType t, int K, int vocab) {

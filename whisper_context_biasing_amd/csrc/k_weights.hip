@@ -1,0 +1,73 @@
+// Weight staging and repacking on the device (wcb_load_weights / wcb_finalize_weights).
+//
+// Every parameter is staged as a dense f32 device tensor: borrowed device views (any of f32 / bf16 /
+// f16, strided, up to 4-D) are gathered by view_to_f32_kernel without leaving the GPU; host arrays
+// (wcb_set_weight) are copied up once. wcb_finalize_weights then builds the owned layouts (fused
+// QKV, conv im2col order, the W_k,hᵀ panels, the cross-K/V stack, ...) with repack_kernel: a 3-D
+// strided gather with a scale, rounded once to the model dtype — the same round-to-nearest-even the
+// host packing used, so weights are bit-identical whichever way they arrived.
+#include <algorithm>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace wcb {
+
+template <typename S>
+__global__ __launch_bounds__(256) void view_to_f32_kernel(const S* __restrict__ src, WeightView v, float* __restrict__ dst) {
+  const long n = v.shape[0] * v.shape[1] * v.shape[2] * v.shape[3];
+  for (long o = blockIdx.x * 256L + threadIdx.x; o < n; o += (long)gridDim.x * 256) {
+    long r = o;
+    const long i3 = r % v.shape[3]; r /= v.shape[3];
+    const long i2 = r % v.shape[2]; r /= v.shape[2];
+    const long i1 = r % v.shape[1];
+    const long i0 = r / v.shape[1];
+    dst[o] = DT<S>::tof(src[i0 * v.stride[0] + i1 * v.stride[1] + i2 * v.stride[2] + i3 * v.stride[3]]);
+  }
+}
+
+void view_to_f32(DType t, const void* src, const WeightView& v, float* dst, hipStream_t s) {
+  const long n = v.shape[0] * v.shape[1] * v.shape[2] * v.shape[3];
+  const int grid = (int)std::min<long>((n + 255) / 256, 4096);
+  switch (t) {
+    case kBF16: WCB_LAUNCH(view_to_f32_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)src, v, dst); break;
+    case kF16: WCB_LAUNCH(view_to_f32_kernel<f16_t>, dim3(grid), dim3(256), 0, s, (const f16_t*)src, v, dst); break;
+    case kF32: WCB_LAUNCH(view_to_f32_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)src, v, dst); break;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void repack_kernel(RepackArgs a) {
+  const long n = (long)a.n[0] * a.n[1] * a.n[2];
+  for (long o = blockIdx.x * 256L + threadIdx.x; o < n; o += (long)gridDim.x * 256) {
+    const long i2 = o % a.n[2], i1 = (o / a.n[2]) % a.n[1], i0 = o / ((long)a.n[1] * a.n[2]);
+    const float v = a.src[i0 * a.s[0] + i1 * a.s[1] + i2 * a.s[2]] * a.scale;
+    reinterpret_cast<T*>(a.dst)[i0 * a.t[0] + i1 * a.t[1] + i2 * a.t[2]] = DT<T>::fromf(v);
+  }
+}
+
+void repack(DType t, const RepackArgs& a, hipStream_t s) {
+  const long n = (long)a.n[0] * a.n[1] * a.n[2];
+  const int grid = (int)std::min<long>((n + 255) / 256, 4096);
+  switch (t) {
+    case kBF16: WCB_LAUNCH(repack_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, a); break;
+    case kF16: WCB_LAUNCH(repack_kernel<f16_t>, dim3(grid), dim3(256), 0, s, a); break;
+    case kF32: WCB_LAUNCH(repack_kernel<float>, dim3(grid), dim3(256), 0, s, a); break;
+  }
+}
+
+// *count += #{i : a[i] != (b ? b[i] : 0)} (tied-weight and zero-bias checks)
+__global__ __launch_bounds__(256) void count_diff_kernel(const float* a, const float* b, long n, int* count) {
+  int c = 0;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) c += a[i] != (b ? b[i] : 0.f);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, c);
+}
+
+void count_diff(const float* a, const float* b, long n, int* count, hipStream_t s) {
+  const int grid = (int)std::min<long>((n + 255) / 256, 1024);
+  WCB_LAUNCH(count_diff_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, a, b, n, count);
+}
+
+}  // namespace wcb

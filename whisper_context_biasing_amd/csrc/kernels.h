@@ -218,6 +218,15 @@ struct WceArgs {
 };
 void weighted_ce(const WceArgs& a, hipStream_t s);
 
+// weight staging / repacking (k_weights.hip)
+struct WeightView { long shape[4] = {1, 1, 1, 1}; long stride[4] = {0, 0, 0, 0}; };   // elements
+void view_to_f32(DType t, const void* src, const WeightView& v, float* dst, hipStream_t s);   // dense f32
+// dst[i0·t0 + i1·t1 + i2·t2] = T(scale · src[i0·s0 + i1·s1 + i2·s2]) over n0 × n1 × n2 (T = model dtype or f32)
+struct RepackArgs { void* dst = nullptr; const float* src = nullptr; int n[3] = {1, 1, 1}; long s[3] = {0, 0, 0};
+                    long t[3] = {0, 0, 0}; float scale = 1.f; };
+void repack(DType t, const RepackArgs& a, hipStream_t s);
+void count_diff(const float* a, const float* b, long n, int* count, hipStream_t s);   // b null: nonzeros
+
 void fill_i32(int* p, int v, long n, hipStream_t s);
 // dst[0..n) = host values, passed by value in the kernel arguments (stream-ordered, no host buffer
 // lifetime or pageable-copy ordering to worry about)

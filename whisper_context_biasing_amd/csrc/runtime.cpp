@@ -53,25 +53,6 @@ constexpr int kXSplit = 8;   // max cross-attention key chunks per (row, head) (
 int esize(int dt) { return dt == WCB_F32 ? 4 : 2; }
 
 // host f32 → device element bits
-void pack_elems(int dt, const float* src, size_t n, std::vector<uint8_t>& out) {
-  out.resize(n * esize(dt));
-  if (dt == WCB_F32) {
-    memcpy(out.data(), src, n * 4);
-  } else if (dt == WCB_BF16) {
-    uint16_t* o = reinterpret_cast<uint16_t*>(out.data());
-    for (size_t i = 0; i < n; ++i) {
-      uint32_t u;
-      memcpy(&u, src + i, 4);
-      if ((u & 0x7fffffffu) > 0x7f800000u) { o[i] = uint16_t((u >> 16) | 0x40); continue; }
-      u += 0x7FFFu + ((u >> 16) & 1u);
-      o[i] = uint16_t(u >> 16);
-    }
-  } else {
-    _Float16* o = reinterpret_cast<_Float16*>(out.data());
-    for (size_t i = 0; i < n; ++i) o[i] = (_Float16)src[i];
-  }
-}
-
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -81,7 +62,9 @@ struct DevBuf {
     p = nullptr;
     bytes = 0;
     HIPCHK(hipMalloc(&p, b));
-    HIPCHK(hipMemset(p, 0, b));
+    // zeroed and complete before any (non-blocking) library stream can touch it
+    HIPCHK(hipMemsetAsync(p, 0, b, nullptr));
+    HIPCHK(hipStreamSynchronize(nullptr));
     bytes = b;
   }
   void release() {
@@ -104,8 +87,6 @@ struct LayerW {
   float *ln2_w = nullptr, *ln2_b = nullptr;
   // encoder-space cross-attention (k_xenc.hip): W_k,hᵀ repacked [H][d][64], W_v [d][d], b_v
   void* xkt_w = nullptr; void* xv_w = nullptr; float* xv_b = nullptr;
-  // q'_h straight from the normalised residual: W_qk,h = W_k,hᵀ W_q,h ([H·d][d]), b_qk,h = W_k,hᵀ b_q,h
-  void* xqk_w = nullptr; float* xqk_b = nullptr;
 };
 
 struct ProfEntry {
@@ -183,7 +164,6 @@ struct wcb_handle {
   int group_rows = 512;
   int xenc_split = 8;   // key ranges per row of the encoder-space kernel (rows x ranges workgroups)
   int xenc_variant = 1; // attn_xenc kernel variant (k_xenc.hip)
-  int xqk = 0;          // 1: one GEMM LN(x) → q' with W_k,hᵀW_q,h precombined (WCB_XQK; measured slower: 14 MB per layer)
   // decoder LayerNorm input of the fused LN projections: 1 = the T-typed copy of the residual stream
   // the producers write beside the f32 rows (half the bytes per projection workgroup; C2 decode 1.066
   // vs 1.110 ms/token), 0 = the f32 rows (f32 mode). WCB_LN16 overrides.
@@ -192,7 +172,7 @@ struct wcb_handle {
   // decode projections on gemm_dec_kernel (K supported): the LayerNorm consumers compute their row
   // statistics from the rows they load, so the producers publish no per-16-column partial sums
   bool dec_gemm = false;
-  std::map<std::string, std::vector<float>> host_w;
+  std::map<std::string, DevBuf> staged;   // every parameter as a dense f32 device tensor until finalize
   std::vector<DevBuf> owned;
   bool ready = false;
   int dbg_enc_layers = -1;   // debug: run only this many encoder layers (-1 = all)
@@ -234,26 +214,20 @@ struct wcb_handle {
     HIPCHK(hipMemcpy(owned.back().p, src, bytes, hipMemcpyHostToDevice));
     return owned.back().p;
   }
-  void* upload_t(const std::vector<float>& v) {
-    std::vector<uint8_t> b;
-    pack_elems(d.dtype, v.data(), v.size(), b);
-    return upload(b.data(), b.size());
-  }
   float* upload_f(const std::vector<float>& v) { return reinterpret_cast<float*>(upload(v.data(), v.size() * 4)); }
-
-  std::vector<float>& W(const std::string& name, size_t expect) {
-    auto it = host_w.find(name);
-    if (it == host_w.end()) throw WcbError(WCB_ERR_STATE, "missing weight " + name);
-    if (it->second.size() != expect)
-      throw WcbError(WCB_ERR_ARG, "weight " + name + " has " + std::to_string(it->second.size()) +
-                                      " elements, expected " + std::to_string(expect));
-    return it->second;
+  void* own(size_t bytes) {
+    owned.emplace_back();
+    owned.back().ensure(bytes);
+    return owned.back().p;
   }
-  std::vector<float> Wopt(const std::string& name, size_t n) {
-    auto it = host_w.find(name);
-    if (it == host_w.end()) return std::vector<float>(n, 0.f);
-    if (it->second.size() != n) throw WcbError(WCB_ERR_ARG, "bad size for " + name);
-    return it->second;
+  // staged parameter `name` (f32 device), element count checked
+  const float* W(const std::string& name, size_t expect) {
+    auto it = staged.find(name);
+    if (it == staged.end()) throw WcbError(WCB_ERR_STATE, "missing weight " + name);
+    if (it->second.bytes != expect * 4)
+      throw WcbError(WCB_ERR_ARG, "weight " + name + " has " + std::to_string(it->second.bytes / 4) +
+                                      " elements, expected " + std::to_string(expect));
+    return it->second.as<float>();
   }
 
   // ---------------------------------------------------------------- profiling helpers
@@ -387,14 +361,10 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     h->device = device;
     // The decode chain is latency-bound and the encoder of the next batch runs beside it: decode
     // streams get the highest priority so their workgroups dispatch ahead of encoder tiles.
-    if (const char* ns = getenv("WCB_DECODE_SPLIT")) h->n_sub = std::max(1, std::min(atoi(ns), (int)wcb_handle::kMaxSub));
     int prio_lo = 0, prio_hi = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    const char* pe = getenv("WCB_PRIO");   // 0: all normal, 1: decode high, 2: decode high + encoder low
-    const int pmode = pe ? atoi(pe) : 1;
-    const int dprio = pmode >= 1 ? prio_hi : 0, eprio = pmode >= 2 ? prio_lo : 0;
-    HIPCHK(hipStreamCreateWithPriority(&h->he, hipStreamNonBlocking, eprio));
-    if (const char* nc = getenv("WCB_DECODE_CTX")) h->nctx = std::max(1, std::min(atoi(nc), (int)wcb_handle::kMaxCtx));
+    const int dprio = prio_hi;
+    HIPCHK(hipStreamCreateWithPriority(&h->he, hipStreamNonBlocking, 0));
     for (int ci = 0; ci < h->nctx; ++ci) {
       DecCtx& D = h->dc[ci];
       HIPCHK(hipStreamCreateWithPriority(&D.hs, hipStreamNonBlocking, dprio));
@@ -410,19 +380,9 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     }
     HIPCHK(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming));
-    if (const char* xs = getenv("WCB_XSPLIT")) h->xsplit = std::max(1, std::min(atoi(xs), kXSplit));
     h->xvariant = desc->n_heads >= 20 ? 1 : 0;
-    if (const char* xv = getenv("WCB_XVARIANT")) h->xvariant = atoi(xv);
     h->xmode = xenc_supported(h->dt, desc->d_model) ? 1 : 0;
-    if (const char* xm = getenv("WCB_XMODE")) h->xmode = (atoi(xm) != 0 && h->xmode) ? 1 : 0;
     h->beam_xmode = 0;
-    if (const char* gr = getenv("WCB_GROUP_ROWS")) h->group_rows = std::max(16, std::min(atoi(gr), 512));
-    if (const char* bx = getenv("WCB_BEAM_XMODE")) h->beam_xmode = (atoi(bx) != 0 && h->xmode) ? 1 : 0;
-    if (const char* xs = getenv("WCB_XENC_SPLIT")) h->xenc_split = std::max(1, std::min(atoi(xs), kXencMaxSplit));
-    if (const char* xv = getenv("WCB_XENC_VARIANT")) h->xenc_variant = atoi(xv);
-    if (const char* xq = getenv("WCB_XQK")) h->xqk = atoi(xq);
-    if (const char* l16 = getenv("WCB_LN16")) h->ln16 = atoi(l16);
-    if (const char* sg = getenv("WCB_STEPS_PER_GRAPH")) h->steps_per_graph = std::max(1, std::min(atoi(sg), 64));
     if (h->dt == kF32) h->ln16 = 0;   // f32 "exact" mode: the copy would be the f32 rows themselves
     h->dec_gemm = gemm_dec_supported(h->dt, desc->d_model);
     // DFT table [416 cols][416 k]: col 2b = win·cos(2πbk/400), col 2b+1 = −win·sin(2πbk/400)
@@ -462,7 +422,8 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     const int nw = (desc->vocab + 31) / 32;
     eb->root_bits.ensure((size_t)nw * 4);
     eb->root_child.ensure((size_t)desc->vocab * 4);
-    HIPCHK(hipMemset(eb->root_child.p, 0xff, (size_t)desc->vocab * 4));
+    HIPCHK(hipMemsetAsync(eb->root_child.p, 0xff, (size_t)desc->vocab * 4, nullptr));
+    HIPCHK(hipStreamSynchronize(nullptr));
     std::vector<int> off = {0, 0};
     eb->trans_off.ensure(8);
     HIPCHK(hipMemcpy(eb->trans_off.p, off.data(), 8, hipMemcpyHostToDevice));
@@ -509,12 +470,76 @@ void wcb_destroy(wcb_handle* h) {
   delete h;
 }
 
+namespace {
+void quiesce(wcb_handle* h);
+void drop_graphs(wcb_handle* h);
+}  // namespace
+
+int wcb_set_option(wcb_handle* h, const char* name, int value) {
+  return guarded(h, [&] {
+    REQUIRE(h && name, "bad argument");
+    const std::string n = name;
+    if (n == "xmode" || n == "beam_xmode") {
+      REQUIRE(!h->ready, "option " + n + " selects the weight layouts: set it before wcb_finalize_weights");
+      REQUIRE(value == 0 || value == 1, "option " + n + ": 0 or 1");
+      // encoder space only where the kernel exists (16-bit, d <= 1024): elsewhere the K/V formulation
+      if (n == "xmode") h->xmode = value && xenc_supported(h->dt, h->d.d_model);
+      else h->beam_xmode = value && h->xmode;
+      if (!h->xmode) h->beam_xmode = 0;
+    } else if (n == "group_rows") {
+      REQUIRE(value >= 16 && value <= 512, "option group_rows: 16..512");
+      h->group_rows = value;
+    } else if (n == "xenc_variant") {
+      REQUIRE(value >= 0 && value <= 3, "option xenc_variant: 0..3");
+      h->xenc_variant = value;
+    } else if (n == "xvariant") {
+      REQUIRE(value >= 0 && value <= 5, "option xvariant: 0..5");
+      h->xvariant = value;
+    } else {
+      throw WcbError(WCB_ERR_ARG, "unknown option " + n);
+    }
+    quiesce(h);
+    drop_graphs(h);   // captured decode steps baked the old configuration in
+  });
+}
+
 int wcb_set_weight(wcb_handle* h, const char* name, const float* data, const int64_t* shape, int ndim) {
   return guarded(h, [&] {
     REQUIRE(h && name && data && shape && ndim >= 1, "null argument");
     size_t n = 1;
     for (int i = 0; i < ndim; ++i) n *= (size_t)shape[i];
-    h->host_w[name] = std::vector<float>(data, data + n);
+    HIPCHK(hipSetDevice(h->device));
+    DevBuf& b = h->staged[name];
+    b.release();
+    b.ensure(n * 4);
+    HIPCHK(hipMemcpy(b.p, data, n * 4, hipMemcpyHostToDevice));
+  });
+}
+
+int wcb_load_weights(wcb_handle* h, const wcb_tensor_view* views, int n, void* stream) {
+  return guarded(h, [&] {
+    REQUIRE(h && (views || n == 0) && n >= 0, "bad argument");
+    HIPCHK(hipSetDevice(h->device));
+    const hipStream_t s = (hipStream_t)stream;
+    for (int k = 0; k < n; ++k) {
+      const wcb_tensor_view& v = views[k];
+      REQUIRE(v.name && v.data && v.ndim >= 1 && v.ndim <= 4, "bad tensor view");
+      REQUIRE(v.dtype == WCB_F32 || v.dtype == WCB_BF16 || v.dtype == WCB_F16, "tensor view dtype");
+      WeightView w;   // right-aligned into 4 dims
+      size_t cnt = 1;
+      for (int i = 0; i < v.ndim; ++i) {
+        REQUIRE(v.shape[i] >= 1, "tensor view shape");
+        w.shape[4 - v.ndim + i] = v.shape[i];
+        w.stride[4 - v.ndim + i] = v.stride[i];
+        cnt *= (size_t)v.shape[i];
+      }
+      DevBuf& b = h->staged[v.name];
+      b.release();
+      b.ensure(cnt * 4);
+      view_to_f32(DType(v.dtype), v.data, w, b.as<float>(), s);
+      HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(s));   // the borrowed views are not read after return
   });
 }
 
@@ -522,55 +547,76 @@ int wcb_finalize_weights(wcb_handle* h) {
   return guarded(h, [&] {
     REQUIRE(h, "null handle");
     HIPCHK(hipSetDevice(h->device));
-    const int d = h->d.d_model, L = h->d.n_layers, F = h->d.ffn, V = h->d.vocab, nm = h->d.n_mel;
-    const size_t dd = (size_t)d * d;
+    const int d = h->d.d_model, L = h->d.n_layers, F = h->d.ffn, V = h->d.vocab, nm = h->d.n_mel, H = h->H();
+    const size_t dd = (size_t)d * d, e = esize(h->d.dtype);
+    HIPCHK(hipStreamSynchronize(h->he));
+    const hipStream_t st = h->he;
+    // owned model-dtype / f32 tensors built from the staged f32 parameters on the device
+    auto rp = [&](bool f32, void* dst, const float* src, std::initializer_list<int> n, std::initializer_list<long> sv,
+                  std::initializer_list<long> tv, float scale = 1.f) {
+      RepackArgs a;
+      a.dst = dst; a.src = src; a.scale = scale;
+      std::copy(n.begin(), n.end(), a.n);
+      std::copy(sv.begin(), sv.end(), a.s);
+      std::copy(tv.begin(), tv.end(), a.t);
+      repack(f32 ? kF32 : h->dt, a, st);
+    };
+    auto dense = [&](bool f32, const float* src, size_t cnt, float scale = 1.f) -> void* {
+      void* p = h->own(cnt * (f32 ? 4 : e));
+      rp(f32, p, src, {1, 1, (int)cnt}, {0, 0, 1}, {0, 0, 1}, scale);
+      return p;
+    };
+    auto T_ = [&](const std::string& name, size_t cnt, float scale = 1.f) { return dense(false, h->W(name, cnt), cnt, scale); };
+    auto F_ = [&](const std::string& name, size_t cnt, float scale = 1.f) {
+      return reinterpret_cast<float*>(dense(true, h->W(name, cnt), cnt, scale));
+    };
+    DevBuf check;
+    check.ensure(4);
     // conv1: W1[o][c][k] → [o][k·n_mel + c], K padded to a multiple of 64 with zeros
-    {
-      const auto& w1 = h->W("model.encoder.conv1.weight", (size_t)d * nm * 3);
-      h->k1pad = (3 * nm + 63) / 64 * 64;
-      std::vector<float> p((size_t)d * h->k1pad, 0.f);
-      for (int o = 0; o < d; ++o)
-        for (int c = 0; c < nm; ++c)
-          for (int k = 0; k < 3; ++k) p[(size_t)o * h->k1pad + k * nm + c] = w1[((size_t)o * nm + c) * 3 + k];
-      h->conv1_w = h->upload_t(p);
-      h->conv1_b = h->upload_f(h->W("model.encoder.conv1.bias", d));
-      const auto& w2 = h->W("model.encoder.conv2.weight", dd * 3);
-      std::vector<float> q((size_t)d * 3 * d);
-      for (int o = 0; o < d; ++o)
-        for (int c = 0; c < d; ++c)
-          for (int k = 0; k < 3; ++k) q[(size_t)o * 3 * d + k * d + c] = w2[((size_t)o * d + c) * 3 + k];
-      h->conv2_w = h->upload_t(q);
-      h->conv2_b = h->upload_f(h->W("model.encoder.conv2.bias", d));
-      h->enc_pos = h->upload_f(h->W("model.encoder.embed_positions.weight", (size_t)h->S() * d));
-    }
+    h->k1pad = (3 * nm + 63) / 64 * 64;
+    h->conv1_w = h->own((size_t)d * h->k1pad * e);   // zeroed on allocation (the K padding)
+    rp(false, h->conv1_w, h->W("model.encoder.conv1.weight", (size_t)d * nm * 3), {d, 3, nm}, {(long)nm * 3, 1, 3},
+       {(long)h->k1pad, nm, 1});
+    h->conv1_b = F_("model.encoder.conv1.bias", d);
+    // conv2: W2[o][c][k] → [o][k·d + c]
+    h->conv2_w = h->own(dd * 3 * e);
+    rp(false, h->conv2_w, h->W("model.encoder.conv2.weight", dd * 3), {d, 3, d}, {(long)d * 3, 1, 3}, {3L * d, d, 1});
+    h->conv2_b = F_("model.encoder.conv2.bias", d);
+    h->enc_pos = F_("model.encoder.embed_positions.weight", (size_t)h->S() * d);
     auto attn_qkv = [&](const std::string& p, LayerW& lw) {
-      std::vector<float> w(3 * dd), b(3 * d, 0.f);
-      const auto& wq = h->W(p + "q_proj.weight", dd);
-      const auto& wk = h->W(p + "k_proj.weight", dd);
-      const auto& wv = h->W(p + "v_proj.weight", dd);
-      const auto bq = h->W(p + "q_proj.bias", d);
-      const auto bv = h->W(p + "v_proj.bias", d);
       // q scaling head_dim^-0.5 = 0.125 (exact power of two: folding it is bit-identical)
-      for (size_t i = 0; i < dd; ++i) { w[i] = wq[i] * 0.125f; w[dd + i] = wk[i]; w[2 * dd + i] = wv[i]; }
-      for (int i = 0; i < d; ++i) { b[i] = bq[i] * 0.125f; b[2 * d + i] = bv[i]; }
-      lw.qkv_w = h->upload_t(w);
-      lw.qkv_b = h->upload_f(b);
-      lw.o_w = h->upload_t(h->W(p + "out_proj.weight", dd));
-      lw.o_b = h->upload_f(h->W(p + "out_proj.bias", d));
+      lw.qkv_w = h->own(3 * dd * e);
+      rp(false, lw.qkv_w, h->W(p + "q_proj.weight", dd), {1, 1, (int)dd}, {0, 0, 1}, {0, 0, 1}, 0.125f);
+      rp(false, (char*)lw.qkv_w + dd * e, h->W(p + "k_proj.weight", dd), {1, 1, (int)dd}, {0, 0, 1}, {0, 0, 1});
+      rp(false, (char*)lw.qkv_w + 2 * dd * e, h->W(p + "v_proj.weight", dd), {1, 1, (int)dd}, {0, 0, 1}, {0, 0, 1});
+      lw.qkv_b = reinterpret_cast<float*>(h->own(3 * (size_t)d * 4));   // k has no bias: zeros
+      rp(true, lw.qkv_b, h->W(p + "q_proj.bias", d), {1, 1, d}, {0, 0, 1}, {0, 0, 1}, 0.125f);
+      rp(true, lw.qkv_b + 2 * d, h->W(p + "v_proj.bias", d), {1, 1, d}, {0, 0, 1}, {0, 0, 1});
+      lw.o_w = T_(p + "out_proj.weight", dd);
+      lw.o_b = F_(p + "out_proj.bias", d);
     };
     auto mlp = [&](const std::string& p, LayerW& lw) {
-      lw.ln1_w = h->upload_f(h->W(p + "self_attn_layer_norm.weight", d));
-      lw.ln1_b = h->upload_f(h->W(p + "self_attn_layer_norm.bias", d));
-      lw.ln2_w = h->upload_f(h->W(p + "final_layer_norm.weight", d));
-      lw.ln2_b = h->upload_f(h->W(p + "final_layer_norm.bias", d));
-      lw.fc1_w = h->upload_t(h->W(p + "fc1.weight", (size_t)F * d));
-      lw.fc1_b = h->upload_f(h->W(p + "fc1.bias", F));
-      lw.fc2_w = h->upload_t(h->W(p + "fc2.weight", (size_t)d * F));
-      lw.fc2_b = h->upload_f(h->W(p + "fc2.bias", d));
+      lw.ln1_w = F_(p + "self_attn_layer_norm.weight", d);
+      lw.ln1_b = F_(p + "self_attn_layer_norm.bias", d);
+      lw.ln2_w = F_(p + "final_layer_norm.weight", d);
+      lw.ln2_b = F_(p + "final_layer_norm.bias", d);
+      lw.fc1_w = T_(p + "fc1.weight", (size_t)F * d);
+      lw.fc1_b = F_(p + "fc1.bias", F);
+      lw.fc2_w = T_(p + "fc2.weight", (size_t)d * F);
+      lw.fc2_b = F_(p + "fc2.bias", d);
+    };
+    auto zero_bias = [&](const std::string& name) {   // Whisper's encoder_attn.k_proj has no bias
+      auto it = h->staged.find(name);
+      if (it == h->staged.end()) return;
+      count_diff(it->second.as<float>(), nullptr, (long)(it->second.bytes / 4), check.as<int>(), st);
     };
     h->enc.assign(L, LayerW{});
     h->dec.assign(L, LayerW{});
-    std::vector<float> xkv_w((size_t)2 * L * dd), xkv_b((size_t)2 * L * d, 0.f);
+    const bool kv_stack = h->xmode == 0 || h->beam_xmode == 0;
+    if (kv_stack) {
+      h->xkv_w = h->own((size_t)2 * L * dd * e);
+      h->xkv_b = reinterpret_cast<float*>(h->own((size_t)2 * L * d * 4));   // k rows: zero bias
+    }
     for (int i = 0; i < L; ++i) {
       const std::string pe = "model.encoder.layers." + std::to_string(i) + ".";
       attn_qkv(pe + "self_attn.", h->enc[i]);
@@ -579,79 +625,49 @@ int wcb_finalize_weights(wcb_handle* h) {
       attn_qkv(pd + "self_attn.", h->dec[i]);
       mlp(pd, h->dec[i]);
       LayerW& lw = h->dec[i];
-      std::vector<float> wq = h->W(pd + "encoder_attn.q_proj.weight", dd);
-      std::vector<float> bq = h->W(pd + "encoder_attn.q_proj.bias", d);
-      for (auto& v : wq) v *= 0.125f;
-      for (auto& v : bq) v *= 0.125f;
-      lw.xq_w = h->upload_t(wq);
-      lw.xq_b = h->upload_f(bq);
-      lw.xo_w = h->upload_t(h->W(pd + "encoder_attn.out_proj.weight", dd));
-      lw.xo_b = h->upload_f(h->W(pd + "encoder_attn.out_proj.bias", d));
-      lw.lnx_w = h->upload_f(h->W(pd + "encoder_attn_layer_norm.weight", d));
-      lw.lnx_b = h->upload_f(h->W(pd + "encoder_attn_layer_norm.bias", d));
-      // cross K/V projection of every layer fused into one [2·L·d][d] weight: rows (l, k|v, d)
-      const auto& wk = h->W(pd + "encoder_attn.k_proj.weight", dd);
-      const auto& wv = h->W(pd + "encoder_attn.v_proj.weight", dd);
-      const auto& bv = h->W(pd + "encoder_attn.v_proj.bias", d);
-      REQUIRE(h->host_w.count(pd + "encoder_attn.k_proj.bias") == 0 ||
-                  std::all_of(h->host_w[pd + "encoder_attn.k_proj.bias"].begin(),
-                              h->host_w[pd + "encoder_attn.k_proj.bias"].end(), [](float v) { return v == 0.f; }),
-              "encoder_attn.k_proj has no bias in Whisper ([tf] modeling_whisper.py:279)");
+      lw.xq_w = T_(pd + "encoder_attn.q_proj.weight", dd, 0.125f);
+      lw.xq_b = F_(pd + "encoder_attn.q_proj.bias", d, 0.125f);
+      lw.xo_w = T_(pd + "encoder_attn.out_proj.weight", dd);
+      lw.xo_b = F_(pd + "encoder_attn.out_proj.bias", d);
+      lw.lnx_w = F_(pd + "encoder_attn_layer_norm.weight", d);
+      lw.lnx_b = F_(pd + "encoder_attn_layer_norm.bias", d);
+      const float* wk = h->W(pd + "encoder_attn.k_proj.weight", dd);
+      const float* wv = h->W(pd + "encoder_attn.v_proj.weight", dd);
+      const float* bv = h->W(pd + "encoder_attn.v_proj.bias", d);
+      zero_bias(pd + "encoder_attn.k_proj.bias");
       if (h->xmode == 1) {
         // W_k,hᵀ: [H][d][64], element (h, c, i) = W_k[h·64 + i][c] (K = 64 contiguous for the MFMA)
-        const int H = h->H();
-        std::vector<float> wkt(dd);
-        for (int hh = 0; hh < H; ++hh)
-          for (int c = 0; c < d; ++c)
-            for (int ii = 0; ii < 64; ++ii) wkt[((size_t)hh * d + c) * 64 + ii] = wk[(size_t)(hh * 64 + ii) * d + c];
-        lw.xkt_w = h->upload_t(wkt);
-        lw.xv_w = h->upload_t(wv);
-        lw.xv_b = h->upload_f(bv);
-        if (h->xqk) {
-          // W_qk[h·d + c][n] = Σ_i W_k[h·64 + i][c] · W_q[h·64 + i][n] (q rows pre-scaled), one head per
-          // host thread; rounded to the model dtype once
-          std::vector<float> wqk((size_t)H * dd, 0.f), bqk((size_t)H * d, 0.f);
-          std::vector<std::thread> th;
-          for (int hh = 0; hh < H; ++hh)
-            th.emplace_back([&, hh] {
-              for (int ii = 0; ii < 64; ++ii) {
-                const float* qr = wq.data() + (size_t)(hh * 64 + ii) * d;
-                const float* kr = wk.data() + (size_t)(hh * 64 + ii) * d;
-                for (int c = 0; c < d; ++c) {
-                  const float a = kr[c];
-                  float* o = wqk.data() + ((size_t)hh * d + c) * d;
-                  for (int n = 0; n < d; ++n) o[n] += a * qr[n];
-                  bqk[(size_t)hh * d + c] += a * bq[hh * 64 + ii];
-                }
-              }
-            });
-          for (auto& t : th) t.join();
-          lw.xqk_w = h->upload_t(wqk);
-          lw.xqk_b = h->upload_f(bqk);
-        }
+        lw.xkt_w = h->own(dd * e);
+        rp(false, lw.xkt_w, wk, {H, d, 64}, {64L * d, 1, d}, {(long)d * 64, 64, 1});
+        lw.xv_w = dense(false, wv, dd);
+        lw.xv_b = reinterpret_cast<float*>(dense(true, bv, d));
       }
-      if (h->xmode == 0 || h->beam_xmode == 0) {
-        std::copy(wk.begin(), wk.end(), xkv_w.begin() + (size_t)(2 * i) * dd);
-        std::copy(wv.begin(), wv.end(), xkv_w.begin() + (size_t)(2 * i + 1) * dd);
-        std::copy(bv.begin(), bv.end(), xkv_b.begin() + (size_t)(2 * i + 1) * d);
+      if (kv_stack) {   // cross K/V projection of every layer fused into one [2·L·d][d] weight: rows (l, k|v, d)
+        rp(false, (char*)h->xkv_w + (size_t)(2 * i) * dd * e, wk, {1, 1, (int)dd}, {0, 0, 1}, {0, 0, 1});
+        rp(false, (char*)h->xkv_w + (size_t)(2 * i + 1) * dd * e, wv, {1, 1, (int)dd}, {0, 0, 1}, {0, 0, 1});
+        rp(true, h->xkv_b + (size_t)(2 * i + 1) * d, bv, {1, 1, d}, {0, 0, 1}, {0, 0, 1});
       }
     }
-    if (h->xmode == 0 || h->beam_xmode == 0) {
-      h->xkv_w = h->upload_t(xkv_w);
-      h->xkv_b = h->upload_f(xkv_b);
+    h->enc_ln_w = F_("model.encoder.layer_norm.weight", d);
+    h->enc_ln_b = F_("model.encoder.layer_norm.bias", d);
+    h->dec_ln_w = F_("model.decoder.layer_norm.weight", d);
+    h->dec_ln_b = F_("model.decoder.layer_norm.bias", d);
+    h->tok_emb = T_("model.decoder.embed_tokens.weight", (size_t)V * d);
+    h->dec_pos = T_("model.decoder.embed_positions.weight", (size_t)h->d.n_text_ctx * d);
+    int bad_bias = 0, untied = 0;
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpy(&bad_bias, check.p, 4, hipMemcpyDeviceToHost));
+    REQUIRE(bad_bias == 0, "encoder_attn.k_proj has no bias in Whisper ([tf] modeling_whisper.py:279)");
+    if (h->staged.count("proj_out.weight")) {   // tied to the embedding (models/whisper_medical.py:14)
+      HIPCHK(hipMemsetAsync(check.p, 0, 4, st));
+      const size_t n = (size_t)V * d;
+      count_diff(h->W("proj_out.weight", n), h->W("model.decoder.embed_tokens.weight", n), (long)n, check.as<int>(), st);
+      HIPCHK(hipStreamSynchronize(st));
+      HIPCHK(hipMemcpy(&untied, check.p, 4, hipMemcpyDeviceToHost));
+      REQUIRE(untied == 0, "proj_out.weight must be tied to model.decoder.embed_tokens.weight");
     }
-    h->enc_ln_w = h->upload_f(h->W("model.encoder.layer_norm.weight", d));
-    h->enc_ln_b = h->upload_f(h->W("model.encoder.layer_norm.bias", d));
-    h->dec_ln_w = h->upload_f(h->W("model.decoder.layer_norm.weight", d));
-    h->dec_ln_b = h->upload_f(h->W("model.decoder.layer_norm.bias", d));
-    h->tok_emb = h->upload_t(h->W("model.decoder.embed_tokens.weight", (size_t)V * d));
-    h->dec_pos = h->upload_t(h->W("model.decoder.embed_positions.weight", (size_t)h->d.n_text_ctx * d));
-    if (h->host_w.count("proj_out.weight")) {
-      const auto& po = h->host_w["proj_out.weight"];
-      const auto& te = h->host_w["model.decoder.embed_tokens.weight"];
-      REQUIRE(po == te, "proj_out.weight must be tied to model.decoder.embed_tokens.weight");
-    }
-    h->host_w.clear();
+    HIPCHK(hipGetLastError());
+    h->staged.clear();
     h->ready = true;
   });
 }
@@ -915,20 +931,13 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       // cross attention in encoder space: q'_h = W_k,hᵀ q_h (block-diagonal GEMM, K = 64), one pass
       // over the encoder output per layer for all heads, range combine + W_v,h + b_v
       char* dqp = (char*)D.dqp.p + (size_t)r0 * H * d * e;
-      if (w.xqk_w) {   // q' = (W_k,hᵀ W_q,h) LN(x) + W_k,hᵀ b_q,h: one GEMM
-        GemmArgs xq = drow(x, d, w.xqk_w, M, H * d, d, dqp, (long)H * d);
-        xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
-        xq.bias = w.xqk_b;
-        dgemm(h, "dec_xq", xq, st_);
-      } else {
-        GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
-        xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
-        xq.bias = w.xq_b;
-        dgemm(h, "dec_xq", xq, st_);
-        GemmArgs kq = drow(dq, d, w.xkt_w, M, H * d, 64, dqp, (long)H * d);
-        kq.a_grp_n = d; kq.a_grp_off = 64;
-        dgemm(h, "dec_kq", kq, st_);
-      }
+      GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
+      xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
+      xq.bias = w.xq_b;
+      dgemm(h, "dec_xq", xq, st_);
+      GemmArgs kq = drow(dq, d, w.xkt_w, M, H * d, 64, dqp, (long)H * d);
+      kq.a_grp_n = d; kq.a_grp_off = 64;
+      dgemm(h, "dec_kq", kq, st_);
       XencArgs xa;
       xa.enc = h->xkv2[c.buf].p; xa.enc_sb = (long)S * d;
       xa.row0 = r0; xa.rows_per_enc = c.nb * rps;   // beams (and prefill positions) of a clip share its encoder output
@@ -1487,8 +1496,9 @@ int wcb_profile_enable(wcb_handle* h, int enable) {
       const size_t sb = (size_t)h->nctx * h->stamp_slots() * 16 * kStampSub;   // one region per decode context
       h->stamps.ensure(sb);
       h->stamp_acc.ensure(16);
-      HIPCHK(hipMemset(h->stamps.p, 0, sb));
-      HIPCHK(hipMemset(h->stamp_acc.p, 0, 16));
+      HIPCHK(hipMemsetAsync(h->stamps.p, 0, sb, nullptr));
+      HIPCHK(hipMemsetAsync(h->stamp_acc.p, 0, 16, nullptr));
+      HIPCHK(hipStreamSynchronize(nullptr));
     }
   });
 }
@@ -1600,7 +1610,7 @@ int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void*
 }
 
 int wcb_op_cross_attention_enc(int dtype, const void* q, const void* enc, const void* wkt, const void* wv,
-                               const float* bv, void* o, int B, int H, int S, int nsplit, void* stream) {
+                               const float* bv, void* o, int B, int H, int S, int nsplit, int variant, void* stream) {
   return guarded(nullptr, [&] {
     const int d = H * 64;
     REQUIRE(q && enc && wkt && wv && bv && o && B > 0 && B <= 64 && H > 0 && S > 0 && nsplit >= 1 &&
@@ -1618,7 +1628,7 @@ int wcb_op_cross_attention_enc(int dtype, const void* q, const void* enc, const 
     XencArgs xa;
     xa.enc = enc; xa.enc_sb = (long)S * d; xa.qp = qp.p; xa.rows = B; xa.H = H; xa.D = d; xa.S = S;
     xa.nsplit = nsplit; xa.part = part.as<float>(); xa.ml = ml.as<float>();
-    if (const char* v = getenv("WCB_XENC_VARIANT")) xa.variant = atoi(v);
+    xa.variant = variant;
     xenc_attention(DType(dtype), xa, (hipStream_t)stream);
     xenc_merge(DType(dtype), xa, u.p, (long)H * d, (hipStream_t)stream);
     GemmArgs vg = rowgemm(u.p, (long)H * d, wv, B, d, d, o, d);

@@ -86,7 +86,8 @@ class BiasList:
 class WhisperCB:
     main_input_name = "input_features"
 
-    def __init__(self, dims: WhisperDims, dtype: str = "bf16", device: int = 0, bias_weight: float = 10.0):
+    def __init__(self, dims: WhisperDims, dtype: str = "bf16", device: int = 0, bias_weight: float = 10.0,
+                 options: Optional[Dict[str, int]] = None):
         if not torch.cuda.is_available():
             raise _lib.WcbError("WhisperCB needs a ROCm GPU (no CPU fallback by design)")
         lib = _lib.load()
@@ -101,6 +102,8 @@ class WhisperCB:
         _lib.check(lib.wcb_create(C.byref(desc), device, C.byref(h)), None, "wcb_create")
         self._h = h
         self._lib = lib
+        for k, v in (options or {}).items():   # wcb_set_option: alternative formulations (tests)
+            _lib.check(lib.wcb_set_option(h, k.encode(), int(v)), h, f"wcb_set_option({k})")
         self.config = SimpleNamespace(use_cache=True, suppress_tokens=[], forced_decoder_ids=None,
                                       decoder_start_token_id=dims.decoder_start_token_id,
                                       pad_token_id=dims.pad_token_id, eos_token_id=dims.eos_token_id,
@@ -120,10 +123,10 @@ class WhisperCB:
     # ------------------------------------------------------------------ construction / weights
     @classmethod
     def from_state_dict(cls, dims_or_config, state_dict, dtype: str = "bf16", device: int = 0,
-                        bias_weight: float = 10.0) -> "WhisperCB":
+                        bias_weight: float = 10.0, options: Optional[Dict[str, int]] = None) -> "WhisperCB":
         dims = dims_or_config if isinstance(dims_or_config, WhisperDims) else (
             get_dims(dims_or_config) if isinstance(dims_or_config, str) else dims_from_hf_config(dims_or_config))
-        m = cls(dims, dtype=dtype, device=device, bias_weight=bias_weight)
+        m = cls(dims, dtype=dtype, device=device, bias_weight=bias_weight, options=options)
         m.load_state_dict(state_dict)
         return m
 
@@ -134,8 +137,22 @@ class WhisperCB:
         dims = get_dims(size)
         return cls.from_state_dict(dims, make_weights(dims, seed=seed, recipe=recipe), dtype, device)
 
+    _VIEW_DTYPES = {torch.float32: _lib.WCB_F32, torch.bfloat16: _lib.WCB_BF16, torch.float16: _lib.WCB_F16}
+
     def load_state_dict(self, state_dict):
+        """Device tensors (this GPU; f32 / bf16 / f16, any strides) are handed over as borrowed views
+        (wcb_load_weights: gathered on the device, no host round trip); host arrays go through
+        wcb_set_weight. Then wcb_finalize_weights builds the device layouts."""
+        views, keep = [], []
         for name, t in state_dict.items():
+            if (isinstance(t, torch.Tensor) and t.is_cuda and t.device.index == self.device.index
+                    and t.dtype in self._VIEW_DTYPES and 1 <= t.dim() <= 4):
+                nm = name.encode()
+                keep.append(nm)
+                v = _lib.WcbTensorView(nm, t.data_ptr(), self._VIEW_DTYPES[t.dtype], t.dim(),
+                                       (C.c_int64 * 4)(*t.shape), (C.c_int64 * 4)(*t.stride()))
+                views.append((v, t))
+                continue
             if isinstance(t, torch.Tensor):
                 a = t.detach().to("cpu", torch.float32).contiguous().numpy()
             else:
@@ -143,6 +160,10 @@ class WhisperCB:
             shape = (C.c_int64 * a.ndim)(*a.shape)
             _lib.check(self._lib.wcb_set_weight(self._h, name.encode(), a.ctypes.data, shape, a.ndim),
                        self._h, f"wcb_set_weight({name})")
+        if views:
+            arr = (_lib.WcbTensorView * len(views))(*[v for v, _ in views])
+            _lib.check(self._lib.wcb_load_weights(self._h, arr, len(views), _stream(self.device)), self._h,
+                       "wcb_load_weights")
         _lib.check(self._lib.wcb_finalize_weights(self._h), self._h, "wcb_finalize_weights")
         self._loaded = True
         return self

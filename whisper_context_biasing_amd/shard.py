@@ -32,6 +32,19 @@ def pack_state_dict(dims: WhisperDims, sd: Dict[str, np.ndarray], dtype=torch.bf
                       for n, _ in param_shapes(dims)]).to(dtype)
 
 
+def unpack_state_dict_views(dims: WhisperDims, flat: torch.Tensor) -> Dict[str, torch.Tensor]:
+    """Views of every parameter into the packed blob, on the blob's device (no copy): on a GPU rank
+    they feed wcb_load_weights directly."""
+    out, off = {}, 0
+    for n, shape in param_shapes(dims):
+        k = int(np.prod(shape))
+        out[n] = flat[off:off + k].view(*shape)
+        off += k
+    if off != flat.numel():
+        raise ValueError(f"packed blob has {flat.numel()} elements, parameters need {off}")
+    return out
+
+
 def unpack_state_dict(dims: WhisperDims, flat: torch.Tensor) -> Dict[str, np.ndarray]:
     host = flat.float().cpu().numpy()
     out, off = {}, 0
@@ -45,9 +58,11 @@ def unpack_state_dict(dims: WhisperDims, flat: torch.Tensor) -> Dict[str, np.nda
 
 
 def broadcast_weights(dims: WhisperDims, device: torch.device, seed: int = 0, src: int = 0,
-                      dtype=torch.bfloat16) -> Dict[str, np.ndarray]:
+                      dtype=torch.bfloat16, views: bool = False) -> Dict[str, np.ndarray]:
     """Rank `src` materialises the seeded weights; one broadcast of the packed blob to every rank.
-    Without an initialised process group this is just the local materialisation."""
+    Without an initialised process group this is just the local materialisation. `views`: return
+    device views into the received blob (WhisperCB.load_state_dict hands them to wcb_load_weights
+    without a host round trip) instead of host arrays."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     n_el = sum(int(np.prod(s)) for _, s in param_shapes(dims))
@@ -57,7 +72,7 @@ def broadcast_weights(dims: WhisperDims, device: torch.device, seed: int = 0, sr
         flat = torch.empty(n_el, dtype=dtype, device=device)
     if world > 1:
         dist.broadcast(flat, src=src)
-    return unpack_state_dict(dims, flat)
+    return unpack_state_dict_views(dims, flat) if views else unpack_state_dict(dims, flat)
 
 
 def max_over_ranks(value: float, device: torch.device) -> float:
