@@ -260,3 +260,28 @@ def test_decode_attention_variants(dt, variant, Sk, split):
     ref = (p @ v.double()).view(B, H * 64)
     tol = 1e-5 if dt == "f32" else 1e-2
     assert (o.double() - ref).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("n_mel", [80, 128])
+def test_log_mel_matches_reference_golden(n_mel):
+    """The GPU front end against the reference's own feature extractor outputs (tests/golden/mel_golden.npz,
+    WhisperFeatureExtractor run by make_golden.py): the same bar the numpy oracle meets (2e-5 on the
+    golden slices; HF quotes 1e-5 between its CPU and GPU paths), plus the global statistics."""
+    import os
+    MEL_COLS = [slice(0, 48), slice(1476, 1524), slice(2952, 3000)]   # as tests/test_oracle_golden.py
+    from whisper_context_biasing_amd.config import get_dims
+    from whisper_context_biasing_amd.model import WhisperCB
+    from whisper_context_biasing_amd.synth import synth_clip
+    gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "mel_golden.npz"))
+    m = WhisperCB(get_dims("large-v3" if n_mel == 128 else "micro"), dtype="f32")
+    for clip in range(4):
+        pcm = synth_clip(clip, n_samples=5 * 16000) if clip == 2 else synth_clip(clip)
+        if clip == 3:
+            pcm = (pcm * 0.001).astype(np.float32)
+        mel = m.log_mel(torch.from_numpy(pcm)[None]).cpu().numpy()[0]
+        got = np.concatenate([mel[:, s] for s in MEL_COLS], axis=1)
+        err = np.abs(got - gold[f"mel{n_mel}_clip{clip}_slices"]).max()
+        assert err < 2e-5, (clip, err)
+        st = gold[f"mel{n_mel}_clip{clip}_stats"]
+        assert abs(mel.max() - st[2]) < 1e-5 and abs(mel.min() - st[3]) < 1e-4, (clip, mel.max(), mel.min(), st)
+        assert abs(mel.sum(dtype=np.float64) - st[0]) < 1e-5 * mel.size

@@ -122,6 +122,8 @@ struct DecCtx {
   int nchunk = 64;
   hipGraphExec_t gexec = nullptr;               // captured decode step
   hipGraphExec_t gexec_k = nullptr;             // steps_per_graph consecutive decode steps in one graph
+  int* done_h = nullptr;                        // pinned: the "all rows finished" step of the last 2 chunks
+  hipEvent_t ev_poll[2] = {};
   std::string gkey;
 };
 
@@ -369,6 +371,8 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
       DecCtx& D = h->dc[ci];
       HIPCHK(hipStreamCreateWithPriority(&D.hs, hipStreamNonBlocking, dprio));
       HIPCHK(hipEventCreateWithFlags(&D.ev_fork, hipEventDisableTiming));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.done_h), 2 * sizeof(int), hipHostMallocDefault));
+      for (hipEvent_t& e : D.ev_poll) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       for (int i = 0; i < DecCtx::kMaxSub && h->n_sub > 1; ++i) {   // row-group streams only when used
         HIPCHK(hipStreamCreateWithPriority(&D.sub[i], hipStreamNonBlocking, dprio));
         HIPCHK(hipEventCreateWithFlags(&D.ev_join[i], hipEventDisableTiming));
@@ -448,6 +452,9 @@ void wcb_destroy(wcb_handle* h) {
                       &D.logits, &D.part_val, &D.part_idx, &D.ints, &D.outbuf, &D.forced, &D.beam})
       b->release();
     if (D.ev_fork) (void)hipEventDestroy(D.ev_fork);
+    for (hipEvent_t e : D.ev_poll)
+      if (e) (void)hipEventDestroy(e);
+    if (D.done_h) (void)hipHostFree(D.done_h);
     for (int i = 0; i < DecCtx::kMaxSub; ++i) {
       if (D.ev_join[i]) (void)hipEventDestroy(D.ev_join[i]);
       if (D.sub[i]) (void)hipStreamDestroy(D.sub[i]);
@@ -1240,6 +1247,10 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
       }
       D.gkey = key;
     }
+    // Natural-EOS mode (reference decoding) polls the device "all finished" step one chunk behind:
+    // chunk k+1 is queued before the host waits for chunk k's flag, so the GPU never idles on the
+    // host (at most one chunk of extra steps after the last row finished; the output is cut at it).
+    int pending = -1;   // slot of the chunk whose flag is in flight
     h->timed_wall("decode_loop", D.hs, [&] {
       while (steps < max_new) {
         const int n = std::min(chunk, max_new - steps);
@@ -1257,9 +1268,18 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
         }
         steps += n;
         if (fixed_len) continue;
-        HIPCHK(hipMemcpyAsync(&done, ints + I_DONE, 4, hipMemcpyDeviceToHost, D.hs));
-        HIPCHK(hipStreamSynchronize(D.hs));
-        if (done > 0) break;
+        const int slot = (pending + 1) & 1;
+        HIPCHK(hipMemcpyAsync(D.done_h + slot, ints + I_DONE, 4, hipMemcpyDeviceToHost, D.hs));
+        HIPCHK(hipEventRecord(D.ev_poll[slot], D.hs));
+        if (pending >= 0) {
+          HIPCHK(hipEventSynchronize(D.ev_poll[pending]));
+          if (D.done_h[pending] > 0) { done = D.done_h[pending]; break; }
+        }
+        pending = slot;
+      }
+      if (!fixed_len && done <= 0 && pending >= 0) {
+        HIPCHK(hipEventSynchronize(D.ev_poll[pending]));
+        done = D.done_h[pending];
       }
     });
     if (done <= 0) done = steps;
