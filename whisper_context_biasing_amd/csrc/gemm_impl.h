@@ -75,6 +75,15 @@ template <typename T> WCB_DEV float gelu_t(float x) {
 // Store 8 consecutive output columns n..n+7 of row m (n % 8 == 0, all in one head for E_HEAD).
 template <typename T, int EPI>
 WCB_DEV void epi_store8(const GemmArgs& g, int m, int n, float* v) {
+  if (EPI == E_RUNTIME && g.mode == 2 && n >= g.n_split) {   // k / v of decoder rows → self-attention KV cache
+    const int n2 = n - g.n_split;
+    const int hh = n2 >> 6, dd = n2 & 63;
+    const int kv = hh / g.hs_H, h = hh % g.hs_H;
+    const int rps = g.kv_rps > 1 ? g.kv_rps : 1;
+    const long off = ((((long)kv * g.hs_B + m / rps) * g.hs_H + h) * g.kv_T + *g.pos + m % rps) * 64 + dd;
+    store8<T>(reinterpret_cast<T*>(g.kv_out) + off, v);
+    return;
+  }
   if (has<EPI>(g, E_HEAD)) {
     const int hh = n >> 6, dd = n & 63;
     const int grp = hh / g.hs_H, h = hh % g.hs_H;
@@ -980,7 +989,8 @@ static void launch_tile_e(const GemmArgs& g, hipStream_t s) {
 template <typename T, int BM, int BN, int WM, int WN>
 static void launch_tile(const GemmArgs& g, hipStream_t s) {
   const int bits = (g.bias ? E_BIAS : 0) | (g.act == 1 ? E_GELU : 0) | (g.resid ? E_RESID : 0) |
-                   (g.out_f32 ? E_F32 : 0) | (g.addrow ? E_ADDROW : 0) | (g.mode == 1 ? E_HEAD : 0);
+                   (g.out_f32 ? E_F32 : 0) | (g.addrow ? E_ADDROW : 0) | (g.mode == 1 ? E_HEAD : 0) |
+                   (g.mode == 2 ? E_RUNTIME : 0);   // KV-cache append: run-time form
   switch (bits) {   // the encoder's epilogues, specialised; anything else takes the run-time form
     case E_BIAS: launch_tile_e<T, BM, BN, WM, WN, E_BIAS>(g, s); break;                                   // QKV
     case E_BIAS | E_GELU: launch_tile_e<T, BM, BN, WM, WN, E_BIAS | E_GELU>(g, s); break;                 // fc1, conv1
@@ -1013,6 +1023,11 @@ static bool launch_skinny_mf(const GemmArgs& g, hipStream_t s) {
 
 template <typename T>
 static void gemm_t(const GemmArgs& g, hipStream_t s) {
+  if (g.tile) {   // decoder rows > 64 (beams, prefill): MFMA tiles, each weight tile read once per 128 rows
+    if (g.N % 128 == 0) launch_tile<T, 128, 128, 2, 2>(g, s);
+    else launch_tile<T, 128, 64, 2, 2>(g, s);
+    return;
+  }
   if ((g.M <= 64 || g.mode == 2 || g.ln_w || g.skinny) && g.mode != 1 && !g.addrow) {
     // decode GEMM (K in its table; else the older skinny kernel below): 16-row workgroups up to 64
     // rows (measured C2: 1.074 vs 1.147 ms/token with 32-row workgroups); the LM head walks the

@@ -57,6 +57,7 @@ struct GemmArgs {
   const int* pos = nullptr; int kv_T = 0;  // mode 2: cache position (device) and cache length
   void* kv_out = nullptr; int n_split = 0; // mode 2: columns >= n_split go to the cache
   int kv_rps = 0;                          // mode 2 prefill: row m → cache row m / kv_rps, position *pos + m % kv_rps
+  int tile = 0;                            // MFMA tile kernel for a decode-row GEMM (> 64 rows; A pre-normalised)
   // decode-step fusions (skinny path)
   const float* st_in = nullptr;    // LN row statistics partials [M][st_nb][2] (Σx, Σx²) of A
   float* st_out = nullptr;         // partials of the written f32 rows (residual GEMMs, NF = 1)

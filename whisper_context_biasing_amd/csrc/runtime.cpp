@@ -170,6 +170,7 @@ struct wcb_handle {
   // the producers write beside the f32 rows (half the bytes per projection workgroup; C2 decode 1.066
   // vs 1.110 ms/token), 0 = the f32 rows (f32 mode). WCB_LN16 overrides.
   int ln16 = 1;
+  int vocab_pad = 0;    // LM-head rows padded to a multiple of 128 (zero rows): the MFMA tile path's N
   int steps_per_graph = 8;   // decode steps captured per replayed graph (WCB_STEPS_PER_GRAPH)
   // decode projections on gemm_dec_kernel (K supported): the LayerNorm consumers compute their row
   // statistics from the rows they load, so the producers publish no per-16-column partial sums
@@ -659,7 +660,10 @@ int wcb_finalize_weights(wcb_handle* h) {
     h->enc_ln_b = F_("model.encoder.layer_norm.bias", d);
     h->dec_ln_w = F_("model.decoder.layer_norm.weight", d);
     h->dec_ln_b = F_("model.decoder.layer_norm.bias", d);
-    h->tok_emb = T_("model.decoder.embed_tokens.weight", (size_t)V * d);
+    h->vocab_pad = (V + 127) / 128 * 128;   // zero rows past V (own() zeroes): logits columns ≥ V are 0
+    h->tok_emb = h->own((size_t)h->vocab_pad * d * e);
+    rp(false, h->tok_emb, h->W("model.decoder.embed_tokens.weight", (size_t)V * d), {1, 1, (int)((size_t)V * d)},
+       {0, 0, 1}, {0, 0, 1});
     h->dec_pos = T_("model.decoder.embed_positions.weight", (size_t)h->d.n_text_ctx * d);
     int bad_bias = 0, untied = 0;
     HIPCHK(hipStreamSynchronize(st));
@@ -826,7 +830,7 @@ void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode
   const DecCtx& D0 = h->dc[h->nctx - 1];   // every context is sized together
   const size_t xbuf = xmode ? (size_t)clips * S * d * e : 2 * L * (size_t)clips * S * d * e;
   const size_t need[] = {xbuf, 2 * L * (size_t)B * T * d * e, (size_t)rows * d * 4,
-                         (size_t)rows * h->d.ffn * e, (size_t)B * h->d.vocab * 4, (size_t)(I_NEXT + 4 * B + 16) * 4,
+                         (size_t)rows * h->d.ffn * e, (size_t)B * h->vocab_pad * 4, (size_t)(I_NEXT + 4 * B + 16) * 4,
                          (size_t)B * out_ld * 4};
   const DevBuf* have[] = {&h->xkv2[h->nctx - 1], &D0.kvself, &D0.dx, &D0.dffn, &D0.logits, &D0.ints, &D0.outbuf};
   bool grow = false;
@@ -853,7 +857,7 @@ void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode
     D.du.ensure((size_t)rows * h->H() * d * e);
     D.xticket.ensure((size_t)rows * h->H() * 4);     // zeroed on allocation; combiners reset their slot
     D.pids.ensure((size_t)rows * 4);
-    D.logits.ensure((size_t)B * h->d.vocab * 4);
+    D.logits.ensure((size_t)B * h->vocab_pad * 4);
     D.nchunk = lm_head_partials(h->dt, (int)d, h->d.vocab);   // argmax partials per row of the LM head
     D.part_val.ensure((size_t)B * D.nchunk * 4);
     D.part_idx.ensure((size_t)B * D.nchunk * 4);
@@ -907,6 +911,28 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
   char* dq = (char*)D.dq.p + (size_t)r0 * d * e;
   char* datt = (char*)D.datt.p + (size_t)r0 * d * e;
   char* dffn = (char*)D.dffn.p + (size_t)r0 * h->d.ffn * e;
+  // More than 64 activation rows (beam rows, prefill passes): a LayerNorm launch into dh, then the
+  // MFMA tile GEMM — each weight tile read once per 128 rows, where the row-block decode kernel reads
+  // the weights once per 16-32 rows. Grouped (block-diagonal) products stay on the decode kernel.
+  // Only where the tile grid is wide enough to stream the weights from many CUs: the LM head, and the
+  // N >= 2048 projections (QKV, fc1) at >= 192 rows (C3: 320 beam rows); the d-wide projections keep
+  // the decode kernel (and keep writing the 16-bit residual copy its LayerNorm consumers read).
+  const bool tiled = M > 64;
+  char* dh = (char*)D.dh.p + (size_t)r0 * d * e;
+  auto proj = [&](const char* cls, GemmArgs g) {
+    const bool lm = g.W == h->tok_emb;
+    if (tiled && !g.a_grp_n && (lm || (M >= 192 && g.N >= 2048))) {
+      if (g.ln_w) {
+        const float* xa = static_cast<const float*>(g.A);
+        h->timed("dec_ln", 0, (double)M * d * (4.0 + e), st_,
+                 [&] { layernorm(h->dt, xa, g.ln_w, g.ln_b, dh, M, d, st_); });
+        g.A = dh; g.lda = d;
+        g.ln_w = g.ln_b = nullptr; g.st_in = nullptr; g.ln_a16 = nullptr;
+      }
+      g.tile = 1; g.skinny = 0;
+    }
+    dgemm(h, cls, g, st_);
+  };
   const size_t cache_l = 2 * (size_t)B * H * T * 64;   // elements per layer (K then V)
   const int clips = c.clips ? c.clips : B;
   const size_t xkv_l = 2 * (size_t)clips * H * S * 64;
@@ -917,7 +943,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nbk; q.ln_a16 = lna;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
     q.kv_rps = rps;
-    dgemm(h, "dec_qkv", q, st_);
+    proj("dec_qkv", q);
     AttnArgs a;
     a.q = dq; a.ldq = d; a.q_Sb = rps; a.Sq = rps; a.causal = rps > 1;
     const char* cache0 = (char*)D.kvself.p + l * cache_l * e;   // K/V rows addressed absolutely
@@ -933,7 +959,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     }
     GemmArgs o = drow(datt, d, w.o_w, M, d, d, x, d);
     o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st_pub; o.st_nb = nbk; o.out16 = x16;
-    dgemm(h, "dec_out", o, st_);
+    proj("dec_out", o);
     if (c.xmode == 1) {
       // cross attention in encoder space: q'_h = W_k,hᵀ q_h (block-diagonal GEMM, K = 64), one pass
       // over the encoder output per layer for all heads, range combine + W_v,h + b_v
@@ -941,10 +967,10 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
       xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
       xq.bias = w.xq_b;
-      dgemm(h, "dec_xq", xq, st_);
+      proj("dec_xq", xq);
       GemmArgs kq = drow(dq, d, w.xkt_w, M, H * d, 64, dqp, (long)H * d);
       kq.a_grp_n = d; kq.a_grp_off = 64;
-      dgemm(h, "dec_kq", kq, st_);
+      proj("dec_kq", kq);
       XencArgs xa;
       xa.enc = h->xkv2[c.buf].p; xa.enc_sb = (long)S * d;
       xa.row0 = r0; xa.rows_per_enc = c.nb * rps;   // beams (and prefill positions) of a clip share its encoder output
@@ -965,13 +991,13 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
                [&] { xenc_merge(h->dt, xa, du, (long)H * d, st_); });
       GemmArgs vg = drow(du, (long)H * d, w.xv_w, M, d, d, datt, d);    // o_h = W_v,h u_h + b_v,h
       vg.a_grp_n = 64; vg.a_grp_off = d; vg.bias = w.xv_b;
-      dgemm(h, "dec_vg", vg, st_);
+      proj("dec_vg", vg);
     } else {
       // cross attention over the precomputed encoder K/V
       GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
       xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
       xq.bias = w.xq_b;
-      dgemm(h, "dec_xq", xq, st_);
+      proj("dec_xq", xq);
       AttnArgs xa;
       const char* xkv = (const char*)h->xkv2[c.buf].p + l * xkv_l * e;
       xa.q = dq; xa.ldq = d; xa.q_Sb = 1; xa.Sq = 1;
@@ -992,19 +1018,22 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     }
     GemmArgs xo = drow(datt, d, w.xo_w, M, d, d, x, d);
     xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st_pub; xo.st_nb = nbk; xo.out16 = x16;
-    dgemm(h, "dec_xo", xo, st_);
+    proj("dec_xo", xo);
     // MLP
     GemmArgs f1 = drow(x, d, w.fc1_w, M, h->d.ffn, d, dffn, h->d.ffn);
     f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nbk; f1.ln_a16 = lna;
     f1.bias = w.fc1_b; f1.act = 1;
-    dgemm(h, "dec_fc1", f1, st_);
+    proj("dec_fc1", f1);
     GemmArgs f2 = drow(dffn, h->d.ffn, w.fc2_w, M, d, h->d.ffn, x, d);
     f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st_pub; f2.st_nb = nbk; f2.out16 = x16;
-    dgemm(h, "dec_fc2", f2, st_);
+    proj("dec_fc2", f2);
   }
   if (c.lm_head) {
     GemmArgs lm = drow(x, d, h->tok_emb, M, h->d.vocab, d, c.logits_out + (size_t)b0 * c.logits_ld, c.logits_ld);
     if (rps > 1) { lm.ldc = h->d.vocab; lm.c_Mb = rps; lm.c_strideB = c.logits_ld; }   // row (b, t) → b·ld + t·V
+    // tile path: all vocab_pad columns (zero rows past V) into a logits buffer of that row stride
+    const bool lm_tiled = tiled && rps == 1 && c.logits_ld >= h->vocab_pad;
+    if (lm_tiled) lm.N = h->vocab_pad;
     lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b; lm.st_in = st; lm.st_nb = nbk; lm.ln_a16 = lna;
     lm.out_f32 = 1;
     if (c.select && !c.beam) {   // argmax partials with the root boost + EOS mask fused into the LM head
@@ -1014,7 +1043,11 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       lm.sel_rowbase = ints + I_NEXT + 3 * c.B + b0;   // per row k - d of its state (select_finalize)
       lm.sel_eos = h->d.eos_token_id; lm.sel_step = ints + I_STEP; lm.sel_min_new = c.min_new;
     }
-    dgemm(h, "lm_head", lm, st_);
+    if (lm_tiled) {
+      proj("lm_head", lm);
+    } else {
+      dgemm(h, "lm_head", lm, st_);
+    }
   }
 }
 
@@ -1194,7 +1227,7 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
       bm.run_sc = (float*)take(0); bm.fin_sc = (float*)take(1); bm.fin_done = (int*)take(2); bm.fin_len = (int*)take(3);
       bm.run_seq = (int*)take(4); bm.fin_seq = (int*)take(5); bm.phys = (int*)take(6);
       bm.cand_val = (float*)take(7); bm.cand_tok = (int*)take(8); bm.flags = (int*)take(9);
-      bm.logits = D.logits.as<float>(); bm.ld = h->d.vocab; bm.V = h->d.vocab;
+      bm.logits = D.logits.as<float>(); bm.ld = h->vocab_pad; bm.V = h->d.vocab;
       bm.B = B; bm.nb = nb; bm.K = K; bm.P = P; bm.Lt = T; bm.T = Tc;
       bm.eos = h->d.eos_token_id; bm.pad = h->d.pad_token_id; bm.min_new = cfg->min_new_tokens;
       bm.lam = cfg->bias_boost; bm.len_pen = 1.f;
@@ -1206,7 +1239,7 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
       bm.out_ids = D.outbuf.as<int>(); bm.out_ld = out_ld; bm.out_len = ints + I_UNFIN;
       beam_init(bm, D.hs);   // before the prefill: the self-attention reads keys through bm.phys
     }
-    StepCfg sc{R, Tc, out_ld, buf, false, false, D.logits.as<float>(), (long)h->d.vocab, bs, cfg->bias_boost,
+    StepCfg sc{R, Tc, out_ld, buf, false, false, D.logits.as<float>(), (long)h->vocab_pad, bs, cfg->bias_boost,
                cfg->min_new_tokens, D.forced.as<int>(), 0};
     sc.clips = B;
     sc.nb = nb;
