@@ -132,6 +132,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=2, help="steps of the serialised roofline pass")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="wcb_set_option on the handle (alternative formulations, for sweeps)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="serialise batches (default: batch i+1's front end + encoder overlap batch i's decode)")
     args = ap.parse_args()
@@ -160,7 +162,8 @@ def main():
     if world > 1:
         torch.cuda.synchronize()
         log(f"rank {rank}: weights broadcast in {time.perf_counter() - t0:.3f} s")
-    model = WhisperCB.from_state_dict(dims, sd, dtype=args.dtype, device=local)
+    opts = {k: int(v) for k, v in (o.split("=", 1) for o in args.opt)}
+    model = WhisperCB.from_state_dict(dims, sd, dtype=args.dtype, device=local, options=opts or None)
     del sd
 
     B = args.batch

@@ -61,7 +61,8 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "xmode" 0/1        decoder cross-attention over per-layer K/V, or in encoder space (before finalize)
  *   "beam_xmode" 0/1   the same for beam search (before finalize)
  *   "group_rows" n     decoder rows per layer chain (16..512)
- *   "xenc_variant" v   encoder-space kernel variant, "xvariant" v  K/V cross-attention kernel variant */
+ *   "xenc_variant" v   encoder-space kernel variant, "xvariant" v  K/V cross-attention kernel variant
+ *   "flash_split" n    key ranges per (clip, head) of the beam-search cross-attention (flash kernel), 1..8 */
 int wcb_set_option(wcb_handle* h, const char* name, int value);
 
 /* replaces from_pretrained / load_state_dict: one HF state-dict tensor (host f32, C order), staged

@@ -122,6 +122,27 @@ def test_flash_attention(dt, S):
     assert (o.double() - ref).abs().max().item() < tol
 
 
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("B,H,Sq,Sk", [(3, 16, 5, 1500), (2, 20, 5, 1500), (4, 6, 2, 1500), (2, 4, 8, 777),
+                                       (1, 2, 16, 64), (2, 3, 17, 1500)])
+@pytest.mark.parametrize("split", [1, 4, 7])
+def test_flash_attention_query_groups(dt, B, H, Sq, Sk, split):
+    """A few query rows per K/V set (beam search: the nb beams of a clip against its cross K/V, one
+    K/V pass per (clip, head); Sq <= 16 takes the 16-queries-per-wave instance, optionally over
+    `split` key ranges merged in a fixed order) vs fp64."""
+    if split > 1 and Sq > 16:
+        pytest.skip("key split is the few-query form")
+    g = torch.Generator(device="cpu").manual_seed(B * 1000 + Sq * 10 + H)
+    q = (torch.randn(B, Sq, H * 64, generator=g) * 0.3).to(DT[dt][0]).cuda()
+    k = torch.randn(B, Sk, H * 64, generator=g).to(DT[dt][0]).cuda()
+    v = torch.randn(B, Sk, H * 64, generator=g).to(DT[dt][0]).cuda()
+    code = 1 if split == 1 else -split
+    o = _attn(dt, q, k, v, code)
+    tol = 1e-2 if dt == "bf16" else 2e-3
+    assert (o.double() - _attn_ref(q, k, v)).abs().max().item() < tol
+    assert torch.equal(_attn(dt, q, k, v, code), o)   # deterministic
+
+
 def test_flash_attention_spike():
     """Force the online-softmax rescale: one key dominates late in the sequence."""
     B, H, S = 1, 1, 1500

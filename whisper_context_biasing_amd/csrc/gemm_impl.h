@@ -105,6 +105,7 @@ WCB_DEV void epi_store8(const GemmArgs& g, int m, int n, float* v) {
   }
   if (has<EPI>(g, E_F32)) store8<float>(reinterpret_cast<float*>(g.out) + off, v);
   else store8<T>(reinterpret_cast<T*>(g.out) + off, v);
+  if (EPI == E_RUNTIME && g.out16) store8<T>(reinterpret_cast<T*>(g.out16) + off, v);   // decode: 16-bit residual copy
 }
 
 template <typename T>
@@ -324,8 +325,11 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
   for (int kt = 0; kt < nk; ++kt) {
     // tiles issued so far: kt .. min(nk, kt + NS - 1) - 1; keep the ones after kt in flight
     const int ahead = min(nk - 1 - kt, NS - 2);
-    if constexpr (NS >= 4) {
-      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * GL) : "memory");
+    if constexpr (NS >= 4) {   // up to min(NS - 2, 4) younger tiles stay in flight (vmcnt <= 63)
+      static_assert(4 * GL <= 63, "vmcnt range");
+      if (NS >= 6 && ahead >= 4) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * GL) : "memory");
+      else if (NS >= 5 && ahead == 3) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(3 * GL) : "memory");
+      else if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * GL) : "memory");
       else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(GL) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if constexpr (NS == 3) {
@@ -1023,7 +1027,19 @@ static bool launch_skinny_mf(const GemmArgs& g, hipStream_t s) {
 
 template <typename T>
 static void gemm_t(const GemmArgs& g, hipStream_t s) {
-  if (g.tile) {   // decoder rows > 64 (beams, prefill): MFMA tiles, each weight tile read once per 128 rows
+  if (g.tile) {   // decoder rows > 64 (beams, prefill): MFMA tiles, each weight tile read once per 64-128 rows
+    if constexpr (sizeof(T) == 2) {
+      // tile 2 (192+ rows, the d-wide and wide projections): 64-row tiles over a deep LDS-DMA ring, so
+      // that even N = d_model spreads over 80-320 workgroups (C3: 320 rows = 5 row tiles); 64 columns
+      // where that still fills the chip, else 32. Run-time epilogue (KV append, 16-bit residual copy).
+      if (g.tile == 2 && g.K % 64 == 0 && !g.st_out && g.mode != 1 && !g.addrow) {
+        const int mt = (g.M + 63) / 64;
+        if (g.N % 64 == 0 && mt * (g.N / 64) >= 240) launch_ring_e<T, 64, 64, 2, 2, 4, E_RUNTIME>(g, s);
+        else if (mt * ((g.N + 31) / 32) >= 240) launch_ring_e<T, 64, 32, 2, 2, 6, E_RUNTIME>(g, s);
+        else launch_ring_e<T, 32, 32, 2, 2, 6, E_RUNTIME>(g, s);
+        return;
+      }
+    }
     if (g.N % 128 == 0) launch_tile<T, 128, 128, 2, 2>(g, s);
     else launch_tile<T, 128, 64, 2, 2>(g, s);
     return;

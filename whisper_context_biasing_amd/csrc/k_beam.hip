@@ -85,11 +85,38 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
   __shared__ int wi[4], wt[4];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float* row = a.logits + (long)r * a.ld;
+  // the row as float4 (a.ld is a multiple of 4: the padded vocabulary), UB loads in flight per lane:
+  // a plain strided loop keeps one load per lane in flight and pays the cache latency per element
+  const f32x4* row4 = reinterpret_cast<const f32x4*>(row);
+  const int V4 = a.V >> 2;
+  constexpr int UB = 4;
+  auto load4 = [&](int i) -> f32x4 {   // float4 i of the row, -inf past the vocabulary
+    if (i < V4) return row4[i];
+    f32x4 x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = 4 * i + e < a.V ? row[4 * i + e] : -INFINITY;
+    return x;
+  };
+  const int n4 = (a.V + 3) >> 2;
   float m = -INFINITY;
-  for (int v = tid; v < a.V; v += 256) m = fmaxf(m, row[v]);
+  for (int i0 = tid; i0 < n4; i0 += 256 * UB) {
+    f32x4 x[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) x[u] = i0 + u * 256 < n4 ? load4(i0 + u * 256) : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int u = 0; u < UB; ++u) m = fmaxf(m, fmaxf(fmaxf(x[u][0], x[u][1]), fmaxf(x[u][2], x[u][3])));
+  }
   m = block_max4(m, red);
   float s = 0.f;
-  for (int v = tid; v < a.V; v += 256) s += expf(row[v] - m);
+  for (int i0 = tid; i0 < n4; i0 += 256 * UB) {
+    f32x4 x[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) x[u] = i0 + u * 256 < n4 ? load4(i0 + u * 256) : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int u = 0; u < UB; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += expf(x[u][e] - m);
+  }
   const float lsum = logf(block_sum4(s, red));
   const bool boost = a.lam != 0.f;
   const int st = a.state[r];
@@ -127,14 +154,24 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
       }
     }
   };
-  for (int v = tid; v < a.V; v += 256) {
-    float x = (row[v] - m) - lsum;                                     // log_softmax
-    if (boost) {                                                       // bias boost processor
-      if ((tbits[v >> 5] >> (v & 31)) & 1u) continue;                  // scored below
-      x = bias_bonus(x, a.lam, rb + (int)((bits[v >> 5] >> (v & 31)) & 1u));
-    }
-    if (mask_eos && v == a.eos) x = -INFINITY;                         // MinNewTokens processor
-    insert(x + rsc, v);                                                // + running beam score
+  for (int i0 = tid; i0 < n4; i0 += 256 * UB) {
+    f32x4 xs[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) xs[u] = i0 + u * 256 < n4 ? load4(i0 + u * 256) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < UB; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int v = 4 * (i0 + u * 256) + e;
+        if (v >= a.V) continue;
+        float x = (xs[u][e] - m) - lsum;                               // log_softmax
+        if (boost) {                                                   // bias boost processor
+          if ((tbits[v >> 5] >> (v & 31)) & 1u) continue;              // scored below
+          x = bias_bonus(x, a.lam, rb + (int)((bits[v >> 5] >> (v & 31)) & 1u));
+        }
+        if (mask_eos && v == a.eos) x = -INFINITY;                     // MinNewTokens processor
+        insert(x + rsc, v);                                            // + running beam score
+      }
   }
   if (boost) {   // trans(state): the exact n(s, v) = d' - d + min(k, d + 1 - d')
     for (int t = a.trans_off[st] + tid; t < a.trans_off[st + 1]; t += 256) {

@@ -152,6 +152,9 @@ struct wcb_handle {
   // two kernels sum in different orders): the single-pass kernel (1) for 20 heads (large-v3, C5:
   // 1076 -> 1110 audio-s/s), the two-pass kernel (0) otherwise (medium, C3: 2435 vs 2048 with 1)
   int xvariant = 0;
+  // beam-search cross-attention on the flash kernel (16-bit, the rows of a clip grouped): key ranges
+  // per (clip, head), merged by flash_merge_kernel. Fixed per handle (never from the batch).
+  int flash_split = 1;
   // Cross-attention formulation: 1 = encoder space (k_xenc.hip: the step streams the encoder output,
   // no cross-K/V precompute; 16-bit dtypes, d <= 1024), 0 = precomputed per-layer K/V (f32 "exact"
   // mode, large-v3). Fixed at create (WCB_XMODE overrides where supported).
@@ -500,6 +503,9 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "xenc_variant") {
       REQUIRE(value >= 0 && value <= 3, "option xenc_variant: 0..3");
       h->xenc_variant = value;
+    } else if (n == "flash_split") {
+      REQUIRE(value >= 1 && value <= kXSplit, "option flash_split: 1..8");
+      h->flash_split = value;
     } else if (n == "xvariant") {
       REQUIRE(value >= 0 && value <= 5, "option xvariant: 0..5");
       h->xvariant = value;
@@ -921,7 +927,11 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
   char* dh = (char*)D.dh.p + (size_t)r0 * d * e;
   auto proj = [&](const char* cls, GemmArgs g) {
     const bool lm = g.W == h->tok_emb;
-    if (tiled && !g.a_grp_n && (lm || (M >= 192 && g.N >= 2048))) {
+    // > 64 rows, 16-bit: every non-grouped projection on the 32/64-row LDS-ring tiles (tile 2; C5's
+    // 80 beam rows: 0.5 TB/s of weights on the row-block decode kernel, which holds A in registers
+    // and re-reads the weights per 32 rows)
+    const bool ring = h->dt != kF32 && !lm && !g.st_out;
+    if (tiled && !g.a_grp_n && (lm || ring || (M >= 192 && g.N >= 2048))) {
       if (g.ln_w) {
         const float* xa = static_cast<const float*>(g.A);
         h->timed("dec_ln", 0, (double)M * d * (4.0 + e), st_,
@@ -929,7 +939,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
         g.A = dh; g.lda = d;
         g.ln_w = g.ln_b = nullptr; g.st_in = nullptr; g.ln_a16 = nullptr;
       }
-      g.tile = 1; g.skinny = 0;
+      g.tile = ring ? 2 : 1; g.skinny = 0;
     }
     dgemm(h, cls, g, st_);
   };
@@ -1013,8 +1023,22 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
         xa.stamp.pos = pos;
         xa.stamp.stride = L * wcb_handle::kMaxSub; xa.stamp.idx = l * wcb_handle::kMaxSub + chain;
       }
-      h->timed("dec_xattn", 4.0 * M * H * (double)S * 64, (double)nb / c.nb * H * S * 128.0 * e, st_,
-               [&] { attention_decode(h->dt, xa, st_); });
+      // 16-bit, several rows per clip (beams, prefill positions), row group aligned to clips: the
+      // MFMA flash kernel over (clip, head) blocks — each clip's K/V streamed once for all of its rows
+      // (the per-row kernels re-read it once per beam). Chosen from the dtype and the decode shape,
+      // never from the batch size.
+      const int G = c.nb * rps;
+      const bool grouped = h->dt != kF32 && G > 1 && r0 % G == 0 && M % G == 0;
+      if (grouped) {
+        xa.k = xkv + (size_t)(r0 / G) * xa.k_sb * e;
+        xa.v = (const char*)xa.v + (size_t)(r0 / G) * xa.k_sb * e;
+        xa.q_Sb = G; xa.Sq = G; xa.o_Sb = G; xa.B = M / G; xa.row0 = 0; xa.b_div = 1;
+        xa.nsplit = h->flash_split; xa.ticket = nullptr;
+        xa.part = D.xpart.as<float>() + (size_t)r0 * H * kXSplit * 66;
+      }
+      h->timed("dec_xattn", 4.0 * M * H * (double)S * 64, (double)nb / c.nb * H * S * 128.0 * e, st_, [&] {
+        if (!grouped || !attention_flash(h->dt, xa, st_)) attention_decode(h->dt, xa, st_);
+      });
     }
     GemmArgs xo = drow(datt, d, w.xo_w, M, d, d, x, d);
     xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st_pub; xo.st_nb = nbk; xo.out16 = x16;
@@ -1716,9 +1740,15 @@ int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, voi
     a.q = q; a.ldq = ld; a.q_Sb = Sq; a.Sq = Sq;
     a.k = k; a.v = v; a.k_sb = (long)Sk * ld; a.k_sh = 64; a.k_sk = ld;
     a.o = o; a.ldo = ld; a.o_Sb = Sq; a.B = B; a.H = H; a.nkeys = Sk;
-    if (flash == 1) {
+    if (flash == 1 || flash < 0) {   // -n: n key ranges + merge (the few-query form, Sq <= 16)
       REQUIRE(dtype != WCB_F32, "flash attention needs a 16-bit dtype");
-      REQUIRE(Sq == Sk, "flash path is the encoder self-attention (Sq == Sk)");
+      static DevBuf fpart;
+      if (flash < 0) {
+        REQUIRE(-flash <= 8 && Sq <= 16, "flash key split: 1..8 ranges, Sq <= 16");
+        a.nsplit = -flash;
+        fpart.ensure((size_t)B * H * Sq * a.nsplit * 66 * 4);
+        a.part = fpart.as<float>();
+      }
       attention_flash(DType(dtype), a, (hipStream_t)stream);
     } else {
       static DevBuf part, ticket;   // split-KV workspace of this test entry point (zeroed on growth)
