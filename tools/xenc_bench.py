@@ -26,7 +26,7 @@ def run(rows, nsplit, reps=5):
     def step():
         for _ in range(L):
             rc = lib.wcb_op_cross_attention_enc(0, q.data_ptr(), enc.data_ptr(), wkt.data_ptr(), wv.data_ptr(),
-                                                bv.data_ptr(), o.data_ptr(), rows, H, S, nsplit, s.cuda_stream)
+                                                bv.data_ptr(), o.data_ptr(), rows, H, S, nsplit, 1, s.cuda_stream)
             assert rc == 0
     with torch.cuda.stream(s):
         step()

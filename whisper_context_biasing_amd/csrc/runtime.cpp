@@ -153,8 +153,9 @@ struct wcb_handle {
   // 1076 -> 1110 audio-s/s), the two-pass kernel (0) otherwise (medium, C3: 2435 vs 2048 with 1)
   int xvariant = 0;
   // beam-search cross-attention on the flash kernel (16-bit, the rows of a clip grouped): key ranges
-  // per (clip, head), merged by flash_merge_kernel. Fixed per handle (never from the batch).
-  int flash_split = 1;
+  // per (clip, head), merged by flash_merge_kernel. Fixed per handle (never from the batch). Measured
+  // (audio-s/s, splits 1 / 2 / 4): C3 4491 / 4531 / 4452, C5 1405 / 1484 / 1485.
+  int flash_split = 2;
   // Cross-attention formulation: 1 = encoder space (k_xenc.hip: the step streams the encoder output,
   // no cross-K/V precompute; 16-bit dtypes, d <= 1024), 0 = precomputed per-layer K/V (f32 "exact"
   // mode, large-v3). Fixed at create (WCB_XMODE overrides where supported).
