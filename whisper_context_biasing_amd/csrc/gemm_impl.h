@@ -270,7 +270,11 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(GemmArgs g) {
 // barrier), the raw s_barrier makes every wave's tile-k bytes visible and tells the issuers that the
 // stage of tile k-1 is free, then tile k+NS-1 is issued into it. No plain global loads inside the
 // loop (hipcc would drain the DMA ring at their use); __syncthreads only after it.
-template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI>
+// LNF (decode rows > 64): the consumer's pre-block LayerNorm folded in (GemmArgs::ln_u): A = the
+// 16-bit residual rows; each A fragment is scaled by γ (staged in LDS) after its LDS read while the
+// row's Σx, Σx² accumulate from the same values; the epilogue applies r·(acc − μ·u[n]) + c[n].
+constexpr int kLnfMaxK = 1280;
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BK = 64, CE = 8;
@@ -317,6 +321,17 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  float* lng = reinterpret_cast<float*>(smem + NS * STAGE);   // LNF: γ [K], then (μ, r) per tile row
+  float* lnst = lng + kLnfMaxK;
+  float s1[FM], s2[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) { s1[i] = 0.f; s2[i] = 0.f; }
+  if constexpr (LNF) {
+    for (int k = tid * 4; k < g.K; k += NT * 4)
+      *reinterpret_cast<f32x4*>(lng + k) = *reinterpret_cast<const f32x4*>(g.ln_w + k);
+    __syncthreads();
+  }
+
   const int nk = g.K / BK;
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
@@ -360,12 +375,43 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
         const int r = wn * TN + j * 16 + (lane & 15);
         b[j] = *reinterpret_cast<const Frag*>(base + BM * 128 + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
       }
+      if constexpr (LNF) {   // elements k = kt·64 + 8c + e of this lane's rows: row sums, then x·γ
+        const f32x4 g0 = *reinterpret_cast<const f32x4*>(lng + kt * BK + c * 8);
+        const f32x4 g1 = *reinterpret_cast<const f32x4*>(lng + kt * BK + c * 8 + 4);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float x;
+            if constexpr (__is_same(T, bf16_t)) x = bf16_to_f((bf16_t)a[i][e]);
+            else x = float(a[i][e]);
+            s1[i] += x;
+            s2[i] = fmaf(x, x, s2[i]);
+            const float y = x * (e < 4 ? g0[e] : g1[e - 4]);
+            if constexpr (__is_same(T, bf16_t)) a[i][e] = (short)f_to_bf16(y);
+            else a[i][e] = f16_t(y);
+          }
+      }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mma16(a[i], b[j], acc[i][j]);
     }
     st = st + 1 == NS ? 0 : st + 1;
+  }
+  if constexpr (LNF) {   // row statistics: the 4 lane groups hold disjoint k; one wave column publishes
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      float a1 = s1[i], a2 = s2[i];
+      a1 += __shfl_xor(a1, 16, 64); a2 += __shfl_xor(a2, 16, 64);
+      a1 += __shfl_xor(a1, 32, 64); a2 += __shfl_xor(a2, 32, 64);
+      if (wn == 0 && lane < 16) {
+        const int row = wm * TM + i * 16 + lane;
+        const float mean = a1 / g.K;
+        lnst[2 * row] = mean;
+        lnst[2 * row + 1] = rsqrtf(fmaxf(a2 / g.K - mean * mean, 0.f) + 1e-5f);
+      }
+    }
   }
   __syncthreads();   // every wave is done with the ring: the epilogue reuses its LDS
 
@@ -388,7 +434,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
           for (int e = 0; e < 4; ++e) {
             const int row = wm * TM + i * 16 + (lane >> 4) * 4 + e;
             const int m = min(m0 + row, g.M - 1);
-            ct[(row - ps * PR) * LDC + col] = epi_pointwise<T, EPI>(g, m, n, acc[i][j][e]);
+            float v = acc[i][j][e];
+            if constexpr (LNF) v = lnst[2 * row + 1] * (v - lnst[2 * row] * g.ln_u[n]);
+            ct[(row - ps * PR) * LDC + col] = epi_pointwise<T, EPI>(g, m, n, v);
           }
       }
     }
@@ -411,21 +459,21 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
   }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI>
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false>
 static void launch_ring_e(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
-  constexpr int stage_bytes = NS * (BM + BN) * 128;
+  constexpr int stage_bytes = NS * (BM + BN) * 128 + (LNF ? (kLnfMaxK + 2 * BM) * 4 : 0);
   constexpr int epi_full = BM * (BN + 4) * 4;
   constexpr int epi_bytes = epi_full <= 160 * 1024 ? epi_full : epi_full / WM;
   constexpr int lds = stage_bytes > epi_bytes ? stage_bytes : epi_bytes;
   static_assert(lds <= 160 * 1024, "LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI>,
+    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
-  WCB_LAUNCH((gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
+  WCB_LAUNCH((gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
 }
 
 template <typename T, int BM, int BN, int WM, int WN, int NS>
@@ -1032,11 +1080,20 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
       // tile 2 (192+ rows, the d-wide and wide projections): 64-row tiles over a deep LDS-DMA ring, so
       // that even N = d_model spreads over 80-320 workgroups (C3: 320 rows = 5 row tiles); 64 columns
       // where that still fills the chip, else 32. Run-time epilogue (KV append, 16-bit residual copy).
-      if (g.tile == 2 && g.K % 64 == 0 && !g.st_out && g.mode != 1 && !g.addrow) {
+      if (g.tile == 2 && g.K % 64 == 0 && !g.st_out && g.mode != 1 && !g.addrow &&
+          (!g.ln_u || g.K <= kLnfMaxK)) {
         const int mt = (g.M + 63) / 64;
-        if (g.N % 64 == 0 && mt * (g.N / 64) >= 240) launch_ring_e<T, 64, 64, 2, 2, 4, E_RUNTIME>(g, s);
-        else if (mt * ((g.N + 31) / 32) >= 240) launch_ring_e<T, 64, 32, 2, 2, 6, E_RUNTIME>(g, s);
-        else launch_ring_e<T, 32, 32, 2, 2, 6, E_RUNTIME>(g, s);
+        const bool lnf = g.ln_u != nullptr;
+        if (g.N % 64 == 0 && mt * (g.N / 64) >= 240) {
+          if (lnf) launch_ring_e<T, 64, 64, 2, 2, 4, E_RUNTIME, true>(g, s);
+          else launch_ring_e<T, 64, 64, 2, 2, 4, E_RUNTIME>(g, s);
+        } else if (mt * ((g.N + 31) / 32) >= 240) {
+          if (lnf) launch_ring_e<T, 64, 32, 2, 2, 6, E_RUNTIME, true>(g, s);
+          else launch_ring_e<T, 64, 32, 2, 2, 6, E_RUNTIME>(g, s);
+        } else {
+          if (lnf) launch_ring_e<T, 32, 32, 2, 2, 6, E_RUNTIME, true>(g, s);
+          else launch_ring_e<T, 32, 32, 2, 2, 6, E_RUNTIME>(g, s);
+        }
         return;
       }
     }

@@ -70,4 +70,32 @@ void count_diff(const float* a, const float* b, long n, int* count, hipStream_t 
   WCB_LAUNCH(count_diff_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, a, b, n, count);
 }
 
+// LayerNorm folded into the projection that consumes it (decode rows > 64, gemm_impl.h LNF):
+// u[n] = Σ_k γ_k W[n][k] and c[n] = Σ_k β_k W[n][k] + bias[n] (f32, fixed-order wave sums), so that
+// LN(x)·Wᵀ + bias = r·(Σ_k x_k γ_k W[n][k] − μ·u[n]) + c[n] for a row with mean μ, 1/σ = r.
+template <typename T>
+__global__ __launch_bounds__(64) void ln_fold_kernel(const T* W, int K, const float* gam, const float* bet,
+                                                     const float* bias, float* u, float* c) {
+  const int n = blockIdx.x, lane = threadIdx.x;
+  const T* w = W + (long)n * K;
+  float su = 0.f, sc = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float x = DT<T>::tof(w[k]);
+    su = fmaf(gam[k], x, su);
+    sc = fmaf(bet[k], x, sc);
+  }
+  su = wave_sum(su);
+  sc = wave_sum(sc);
+  if (lane == 0) { u[n] = su; c[n] = sc + (bias ? bias[n] : 0.f); }
+}
+
+void ln_fold(DType t, const void* W, int N, int K, const float* gam, const float* bet, const float* bias, float* u,
+             float* c, hipStream_t s) {
+  switch (t) {
+    case kBF16: WCB_LAUNCH(ln_fold_kernel<bf16_t>, dim3(N), dim3(64), 0, s, (const bf16_t*)W, K, gam, bet, bias, u, c); break;
+    case kF16: WCB_LAUNCH(ln_fold_kernel<f16_t>, dim3(N), dim3(64), 0, s, (const f16_t*)W, K, gam, bet, bias, u, c); break;
+    case kF32: WCB_LAUNCH(ln_fold_kernel<float>, dim3(N), dim3(64), 0, s, (const float*)W, K, gam, bet, bias, u, c); break;
+  }
+}
+
 }  // namespace wcb

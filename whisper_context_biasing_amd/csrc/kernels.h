@@ -75,6 +75,10 @@ struct GemmArgs {
   // LN-fused A read from such a copy instead of the f32 rows (lda elements per row)
   void* out16 = nullptr;
   const void* ln_a16 = nullptr;
+  // folded LayerNorm (ring tiles, decode rows > 64): A = the 16-bit residual rows x, ln_w = γ, ln_u =
+  // Σ_k γ_k W[n][k]; bias holds Σ_k β_k W[n][k] + bias. out = r·(Σ_k bf16(x_k γ_k) W[n][k] − μ·ln_u[n]) + bias
+  const float* ln_u = nullptr;
+  const float* ln_c = nullptr;     // Σ_k β_k W[n][k] + bias[n] (becomes `bias` when the fold is taken)
   // f16 encoder layers: the layer output is clamped to ±(finfo(f16).max − 1000)
   // ([tf] modeling_whisper.py:409-411); 0 = off
   float clamp = 0.f;
@@ -227,6 +231,9 @@ struct RepackArgs { void* dst = nullptr; const float* src = nullptr; int n[3] = 
                     long t[3] = {0, 0, 0}; float scale = 1.f; };
 void repack(DType t, const RepackArgs& a, hipStream_t s);
 void count_diff(const float* a, const float* b, long n, int* count, hipStream_t s);   // b null: nonzeros
+// u[n] = Σ_k γ_k W[n][k], c[n] = Σ_k β_k W[n][k] + bias[n] (the LayerNorm fold of gemm_impl.h LNF)
+void ln_fold(DType t, const void* W, int N, int K, const float* gam, const float* bet, const float* bias, float* u,
+             float* c, hipStream_t s);
 
 void fill_i32(int* p, int v, long n, hipStream_t s);
 // dst[0..n) = host values, passed by value in the kernel arguments (stream-ordered, no host buffer

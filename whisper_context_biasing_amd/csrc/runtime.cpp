@@ -85,6 +85,9 @@ struct LayerW {
   void* fc1_w = nullptr; float* fc1_b = nullptr;
   void* fc2_w = nullptr; float* fc2_b = nullptr;
   float *ln2_w = nullptr, *ln2_b = nullptr;
+  // decoder, 16-bit: the pre-block LayerNorms folded into their consumers for rows > 64 (ring LNF):
+  // u = Σ_k γ_k W[n][k], c = Σ_k β_k W[n][k] + bias, for QKV (ln1), cross-q (lnx), fc1 (ln2)
+  float *ln1_u = nullptr, *ln1_c = nullptr, *lnx_u = nullptr, *lnx_c = nullptr, *ln2_u = nullptr, *ln2_c = nullptr;
   // encoder-space cross-attention (k_xenc.hip): W_k,hᵀ repacked [H][d][64], W_v [d][d], b_v
   void* xkt_w = nullptr; void* xv_w = nullptr; float* xv_b = nullptr;
 };
@@ -156,6 +159,9 @@ struct wcb_handle {
   // per (clip, head), merged by flash_merge_kernel. Fixed per handle (never from the batch). Measured
   // (audio-s/s, splits 1 / 2 / 4): C3 4491 / 4531 / 4452, C5 1405 / 1484 / 1485.
   int flash_split = 2;
+  // decode rows > 64 (16-bit): pre-block LayerNorms folded into the ring-tile projections (no
+  // LayerNorm launch); 0 = a LayerNorm launch before each (the A/B switch "ln_fold")
+  int ln_fold = 1;
   // Cross-attention formulation: 1 = encoder space (k_xenc.hip: the step streams the encoder output,
   // no cross-K/V precompute; 16-bit dtypes, d <= 1024), 0 = precomputed per-layer K/V (f32 "exact"
   // mode, large-v3). Fixed at create (WCB_XMODE overrides where supported).
@@ -504,6 +510,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "xenc_variant") {
       REQUIRE(value >= 0 && value <= 3, "option xenc_variant: 0..3");
       h->xenc_variant = value;
+    } else if (n == "ln_fold") {
+      h->ln_fold = value != 0;
     } else if (n == "flash_split") {
       REQUIRE(value >= 1 && value <= kXSplit, "option flash_split: 1..8");
       h->flash_split = value;
@@ -661,6 +669,19 @@ int wcb_finalize_weights(wcb_handle* h) {
         rp(false, (char*)h->xkv_w + (size_t)(2 * i) * dd * e, wk, {1, 1, (int)dd}, {0, 0, 1}, {0, 0, 1});
         rp(false, (char*)h->xkv_w + (size_t)(2 * i + 1) * dd * e, wv, {1, 1, (int)dd}, {0, 0, 1}, {0, 0, 1});
         rp(true, h->xkv_b + (size_t)(2 * i + 1) * d, bv, {1, 1, d}, {0, 0, 1}, {0, 0, 1});
+      }
+    }
+    if (h->dt != kF32) {
+      for (int i = 0; i < L; ++i) {
+        LayerW& lw = h->dec[i];
+        auto fold = [&](const void* W, int N, const float* gam, const float* bet, const float* bias, float*& u, float*& c) {
+          u = reinterpret_cast<float*>(h->own((size_t)N * 4));
+          c = reinterpret_cast<float*>(h->own((size_t)N * 4));
+          ln_fold(h->dt, W, N, d, gam, bet, bias, u, c, st);
+        };
+        fold(lw.qkv_w, 3 * d, lw.ln1_w, lw.ln1_b, lw.qkv_b, lw.ln1_u, lw.ln1_c);
+        fold(lw.xq_w, d, lw.lnx_w, lw.lnx_b, lw.xq_b, lw.lnx_u, lw.lnx_c);
+        fold(lw.fc1_w, F, lw.ln2_w, lw.ln2_b, lw.fc1_b, lw.ln2_u, lw.ln2_c);
       }
     }
     h->enc_ln_w = F_("model.encoder.layer_norm.weight", d);
@@ -933,7 +954,11 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     // and re-reads the weights per 32 rows)
     const bool ring = h->dt != kF32 && !lm && !g.st_out;
     if (tiled && !g.a_grp_n && (lm || ring || (M >= 192 && g.N >= 2048))) {
-      if (g.ln_w) {
+      if (g.ln_w && ring && g.ln_u && h->ln_fold && lna) {   // LayerNorm folded into the ring tiles
+        g.A = lna; g.lda = d;
+        g.bias = g.ln_c; g.ln_b = nullptr; g.st_in = nullptr; g.ln_a16 = nullptr;
+      } else if (g.ln_w) {
+        g.ln_u = nullptr;
         const float* xa = static_cast<const float*>(g.A);
         h->timed("dec_ln", 0, (double)M * d * (4.0 + e), st_,
                  [&] { layernorm(h->dt, xa, g.ln_w, g.ln_b, dh, M, d, st_); });
@@ -953,7 +978,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     GemmArgs q = drow(x, d, w.qkv_w, M, 3 * d, d, dq, d);    // LayerNorm fused (f32 A rows)
     q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nbk; q.ln_a16 = lna;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
-    q.kv_rps = rps;
+    q.kv_rps = rps; q.ln_u = w.ln1_u; q.ln_c = w.ln1_c;
     proj("dec_qkv", q);
     AttnArgs a;
     a.q = dq; a.ldq = d; a.q_Sb = rps; a.Sq = rps; a.causal = rps > 1;
@@ -977,7 +1002,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       char* dqp = (char*)D.dqp.p + (size_t)r0 * H * d * e;
       GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
       xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
-      xq.bias = w.xq_b;
+      xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c;
       proj("dec_xq", xq);
       GemmArgs kq = drow(dq, d, w.xkt_w, M, H * d, 64, dqp, (long)H * d);
       kq.a_grp_n = d; kq.a_grp_off = 64;
@@ -1007,7 +1032,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       // cross attention over the precomputed encoder K/V
       GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
       xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
-      xq.bias = w.xq_b;
+      xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c;
       proj("dec_xq", xq);
       AttnArgs xa;
       const char* xkv = (const char*)h->xkv2[c.buf].p + l * xkv_l * e;
@@ -1047,7 +1072,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     // MLP
     GemmArgs f1 = drow(x, d, w.fc1_w, M, h->d.ffn, d, dffn, h->d.ffn);
     f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nbk; f1.ln_a16 = lna;
-    f1.bias = w.fc1_b; f1.act = 1;
+    f1.bias = w.fc1_b; f1.act = 1; f1.ln_u = w.ln2_u; f1.ln_c = w.ln2_c;
     proj("dec_fc1", f1);
     GemmArgs f2 = drow(dffn, h->d.ffn, w.fc2_w, M, d, h->d.ffn, x, d);
     f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st_pub; f2.st_nb = nbk; f2.out16 = x16;
