@@ -62,7 +62,9 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "beam_xmode" 0/1   the same for beam search (before finalize)
  *   "group_rows" n     decoder rows per layer chain (16..512)
  *   "xenc_variant" v   encoder-space kernel variant, "xvariant" v  K/V cross-attention kernel variant
- *   "flash_split" n    key ranges per (clip, head) of the beam-search cross-attention (flash kernel), 1..8 */
+ *   "flash_split" n    key ranges per (clip, head) of the beam-search cross-attention (flash kernel), 1..8
+ *   "ln_fold" 0/1      decode rows > 64 (16-bit): LayerNorm folded into the projection, or its own launch
+ *   "enc_flash_qw" q   encoder flash attention: 16-row query fragments per wave, 2 or 4 */
 int wcb_set_option(wcb_handle* h, const char* name, int value);
 
 /* replaces from_pretrained / load_state_dict: one HF state-dict tensor (host f32, C order), staged
@@ -163,8 +165,10 @@ int wcb_op_gemm_ln(int dtype, const float* X, const float* ln_w, const float* ln
 int wcb_op_layernorm(int dtype, const float* x, const float* w, const float* b, void* y, int M, int d,
                      void* stream);
 /* o[B][Sq][H*64] = softmax(q kᵀ) v per head (q pre-scaled), k/v [B][Sk][H*64];
- * flash=1 selects the MFMA kernel (16-bit dtypes); 0 the decode kernel; n >= 2 the decode kernel with
- * n split-KV key chunks combined by the last-arriving chunk. */
+ * flash=1 selects the MFMA kernel (16-bit dtypes; Sq <= 16: the few-query form of beam search), 100 the
+ * MFMA kernel with 64 queries per wave, -n (Sq <= 16) the MFMA kernel over n key ranges merged in
+ * fixed order; 0 the decode kernel; n >= 2 the decode kernel with n split-KV key chunks combined by the
+ * last-arriving chunk. */
 int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H, int Sq,
                      int Sk, int flash, void* stream);
 /* decode attention in the runtime's layout: q/o [B][H*64], K/V head-major [B][H][Sk][64]; one query

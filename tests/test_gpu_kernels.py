@@ -120,6 +120,8 @@ def test_flash_attention(dt, S):
     # P is rounded to the 16-bit type before P·V: |err| ≲ 2^-8 relative for bf16
     tol = 1e-2 if dt == "bf16" else 2e-3
     assert (o.double() - ref).abs().max().item() < tol
+    o4 = _attn(dt, q, k, v, 100)   # 64 queries per wave (encoder option enc_flash_qw = 4)
+    assert (o4.double() - ref).abs().max().item() < tol
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])

@@ -614,9 +614,14 @@ static void launch_flash(const AttnArgs& a, hipStream_t s) {
     const dim3 grid((a.Sq + 63) / 64 * ns, a.B * a.H);
     WCB_LAUNCH((attn_flash_kernel<T, 1, 2>), grid, dim3(256), 0, s, b);
     if (ns > 1) WCB_LAUNCH(flash_merge_kernel<T>, dim3(a.B * a.H * a.Sq), dim3(64), 0, s, b);
-  } else {
-    const dim3 grid((a.Sq + 127) / 128, a.B * a.H);
-    WCB_LAUNCH((attn_flash_kernel<T, 2, 2>), grid, dim3(256), 0, s, a);
+  } else {   // one key range (the key split is the few-query form only)
+    AttnArgs b = a;
+    b.nsplit = 1;
+    if (a.variant == 4) {   // 64 queries per wave: half the K/V LDS reads per MFMA
+      WCB_LAUNCH((attn_flash_kernel<T, 4, 2>), dim3((a.Sq + 255) / 256, a.B * a.H), dim3(256), 0, s, b);
+    } else {
+      WCB_LAUNCH((attn_flash_kernel<T, 2, 2>), dim3((a.Sq + 127) / 128, a.B * a.H), dim3(256), 0, s, b);
+    }
   }
 }
 

@@ -162,6 +162,7 @@ struct wcb_handle {
   // decode rows > 64 (16-bit): pre-block LayerNorms folded into the ring-tile projections (no
   // LayerNorm launch); 0 = a LayerNorm launch before each (the A/B switch "ln_fold")
   int ln_fold = 1;
+  int enc_flash_qw = 2;   // encoder flash attention: query fragments (16 rows) per wave, 2 or 4
   // Cross-attention formulation: 1 = encoder space (k_xenc.hip: the step streams the encoder output,
   // no cross-K/V precompute; 16-bit dtypes, d <= 1024), 0 = precomputed per-layer K/V (f32 "exact"
   // mode, large-v3). Fixed at create (WCB_XMODE overrides where supported).
@@ -510,6 +511,9 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "xenc_variant") {
       REQUIRE(value >= 0 && value <= 3, "option xenc_variant: 0..3");
       h->xenc_variant = value;
+    } else if (n == "enc_flash_qw") {
+      REQUIRE(value == 2 || value == 4, "option enc_flash_qw: 2 or 4");
+      h->enc_flash_qw = value;
     } else if (n == "ln_fold") {
       h->ln_fold = value != 0;
     } else if (n == "flash_split") {
@@ -815,7 +819,7 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
     a.q = h->qkv.p; a.ldq = 3 * d; a.q_Sb = S; a.Sq = S;
     a.k = (char*)h->qkv.p + d * e; a.v = (char*)h->qkv.p + 2 * d * e;
     a.k_sb = (long)S * 3 * d; a.k_sh = 64; a.k_sk = 3 * d;
-    a.o = h->att.p; a.ldo = d; a.o_Sb = S; a.B = B; a.H = H; a.nkeys = S;
+    a.o = h->att.p; a.ldo = d; a.o_Sb = S; a.B = B; a.H = H; a.nkeys = S; a.variant = h->enc_flash_qw;
     h->timed("enc_attn", 4.0 * B * H * (double)S * S * 64, 0, h->he, [&] {
       if (!attention_flash(h->dt, a, h->he)) attention_decode(h->dt, a, h->he);
     });
@@ -1766,7 +1770,8 @@ int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, voi
     a.q = q; a.ldq = ld; a.q_Sb = Sq; a.Sq = Sq;
     a.k = k; a.v = v; a.k_sb = (long)Sk * ld; a.k_sh = 64; a.k_sk = ld;
     a.o = o; a.ldo = ld; a.o_Sb = Sq; a.B = B; a.H = H; a.nkeys = Sk;
-    if (flash == 1 || flash < 0) {   // -n: n key ranges + merge (the few-query form, Sq <= 16)
+    if (flash == 1 || flash == 100 || flash < 0) {   // 100: 64 queries per wave; -n: n key ranges + merge (Sq <= 16)
+      a.variant = flash == 100 ? 4 : 1;
       REQUIRE(dtype != WCB_F32, "flash attention needs a 16-bit dtype");
       static DevBuf fpart;
       if (flash < 0) {
