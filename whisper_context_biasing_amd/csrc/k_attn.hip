@@ -318,7 +318,8 @@ __global__ __launch_bounds__(NW * 64) void attn_decode2p_kernel(AttnArgs a) {
 // per load, 8 loads of K and of V per lane in flight.
 // PHYS (beam search): key j of row b lives in cache row phys[(row0 + b)·phys_ld + j]; lane j of the
 // wave loads the map entry of key j0 + j once per 64-key chunk and the K/V row offsets are shuffled
-// from it (one dependent round trip per chunk, not one per key group).
+// from it (one dependent round trip per chunk, not one per key group). Loading only the key groups
+// below the device-side count instead (a branch on it) measured slower: C3 22.8 -> 38.3 µs.
 template <typename T, bool PHYS>
 __global__ __launch_bounds__(64) void attn_self_kernel(AttnArgs a) {
   const int b = blockIdx.y / a.H, h = blockIdx.y % a.H, lane = threadIdx.x;

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
   // a plain strided loop keeps one load per lane in flight and pays the cache latency per element
   const f32x4* row4 = reinterpret_cast<const f32x4*>(row);
   const int V4 = a.V >> 2;
-  constexpr int UB = 4;
+  constexpr int UB = 8;
   auto load4 = [&](int i) -> f32x4 {   // float4 i of the row, -inf past the vocabulary
     if (i < V4) return row4[i];
     f32x4 x;
@@ -98,25 +98,28 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
     return x;
   };
   const int n4 = (a.V + 3) >> 2;
-  float m = -INFINITY;
-  for (int i0 = tid; i0 < n4; i0 += 256 * UB) {
-    f32x4 x[UB];
+  // one pass for max and Σexp (per lane: a running max, the sum rescaled when a batch raises it);
+  // UB2 float4 loads in flight per lane: one workgroup per row, so the row's read is latency-bound
+  // on the loads each lane keeps in flight (C5: 80 rows = 80 workgroups)
+  constexpr int UB2 = 8;
+  float m = -INFINITY, s = 0.f;
+  for (int i0 = tid; i0 < n4; i0 += 256 * UB2) {
+    f32x4 x[UB2];
 #pragma unroll
-    for (int u = 0; u < UB; ++u) x[u] = i0 + u * 256 < n4 ? load4(i0 + u * 256) : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int u = 0; u < UB2; ++u) x[u] = i0 + u * 256 < n4 ? load4(i0 + u * 256) : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    float bm = m;
 #pragma unroll
-    for (int u = 0; u < UB; ++u) m = fmaxf(m, fmaxf(fmaxf(x[u][0], x[u][1]), fmaxf(x[u][2], x[u][3])));
-  }
-  m = block_max4(m, red);
-  float s = 0.f;
-  for (int i0 = tid; i0 < n4; i0 += 256 * UB) {
-    f32x4 x[UB];
+    for (int u = 0; u < UB2; ++u) bm = fmaxf(bm, fmaxf(fmaxf(x[u][0], x[u][1]), fmaxf(x[u][2], x[u][3])));
+    if (bm > m) { s = m == -INFINITY ? 0.f : s * expf(m - bm); m = bm; }
+    if (m == -INFINITY) continue;
 #pragma unroll
-    for (int u = 0; u < UB; ++u) x[u] = i0 + u * 256 < n4 ? load4(i0 + u * 256) : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-    for (int u = 0; u < UB; ++u)
+    for (int u = 0; u < UB2; ++u)
 #pragma unroll
       for (int e = 0; e < 4; ++e) s += expf(x[u][e] - m);
   }
+  const float mrow = block_max4(m, red);
+  s = m == -INFINITY ? 0.f : s * expf(m - mrow);   // lane sums onto the row max
+  m = mrow;
   const float lsum = logf(block_sum4(s, red));
   const bool boost = a.lam != 0.f;
   const int st = a.state[r];

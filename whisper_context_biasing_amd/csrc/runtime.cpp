@@ -160,8 +160,10 @@ struct wcb_handle {
   // (audio-s/s, splits 1 / 2 / 4): C3 4491 / 4531 / 4452, C5 1405 / 1484 / 1485.
   int flash_split = 2;
   // decode rows > 64 (16-bit): pre-block LayerNorms folded into the ring-tile projections (no
-  // LayerNorm launch); 0 = a LayerNorm launch before each (the A/B switch "ln_fold")
-  int ln_fold = 1;
+  // LayerNorm launch, option "ln_fold" = 1) or a LayerNorm launch before each (0, default). Measured
+  // (audio-s/s, fold / launch): C3 4425 / 4572, C5 1399 / 1490 — the per-element γ scaling and row
+  // sums inside the latency-bound ring loop cost more than the 4.6 µs launch they remove.
+  int ln_fold = 0;
   int enc_flash_qw = 2;   // encoder flash attention: query fragments (16 rows) per wave, 2 or 4
   // Cross-attention formulation: 1 = encoder space (k_xenc.hip: the step streams the encoder output,
   // no cross-K/V precompute; 16-bit dtypes, d <= 1024), 0 = precomputed per-layer K/V (f32 "exact"
