@@ -145,6 +145,20 @@ def test_flash_attention_query_groups(dt, B, H, Sq, Sk, split):
     assert torch.equal(_attn(dt, q, k, v, code), o)   # deterministic
 
 
+@pytest.mark.parametrize("code", [1, 100])
+def test_flash_attention_xcd_grouped(code):
+    """B·H % 8 == 0 (the C2 / C3 / C5 encoder batches): the query blocks of one
+    (clip, head) are mapped to one XCD (1-D grid). Same results as the fp64 reference, deterministic."""
+    g = torch.Generator(device="cpu").manual_seed(11 + code)
+    B, H, S = 4, 6, 1500
+    q = (torch.randn(B, S, H * 64, generator=g) * 0.3).bfloat16().cuda()
+    k = torch.randn(B, S, H * 64, generator=g).bfloat16().cuda()
+    v = torch.randn(B, S, H * 64, generator=g).bfloat16().cuda()
+    o = _attn("bf16", q, k, v, code)
+    assert (o.double() - _attn_ref(q, k, v)).abs().max().item() < 1e-2
+    assert torch.equal(_attn("bf16", q, k, v, code), o)
+
+
 def test_flash_attention_spike():
     """Force the online-softmax rescale: one key dominates late in the sequence."""
     B, H, S = 1, 1, 1500

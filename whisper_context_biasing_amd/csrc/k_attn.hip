@@ -435,12 +435,21 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[NS][2][64 * 128];   // [stage][K|V][64 keys x 128 B]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int S = a.nkeys;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  // XCD grouping (a.xcd_nqb > 0, 1-D grid): workgroup w runs on XCD w % 8 (round-robin dispatch), so
+  // (set, head) = (w / 8 / nqb)·8 + w % 8 puts every query block of one (set, head) on one XCD and its
+  // K/V is fetched into one L2 instead of eight (bijective for B·H % 8 == 0)
+  int bxx = blockIdx.x, bh = blockIdx.y;
+  if (a.xcd_nqb > 0) {
+    const int w = blockIdx.x, slot = w >> 3;
+    bh = (slot / a.xcd_nqb) * 8 + (w & 7);
+    bxx = slot % a.xcd_nqb;
+  }
+  const int b = bh / a.H, h = bh % a.H;
   // key split (a.nsplit > 1, few-query launches): workgroup (query block, split) takes a contiguous
   // range of 64-key tiles and publishes unnormalised partials; flash_merge_kernel combines them
   const int nsplit = a.nsplit > 1 ? a.nsplit : 1;
-  const int split = blockIdx.x % nsplit;
-  const int q0 = (blockIdx.x / nsplit) * QB + wave * QW * 16;
+  const int split = bxx % nsplit;
+  const int q0 = (bxx / nsplit) * QB + wave * QW * 16;
   const int nt_all = (S + 63) / 64, per_t = (nt_all + nsplit - 1) / nsplit;
   const int t_lo = min(split * per_t, nt_all), nt = min(nt_all, t_lo + per_t) - t_lo;
   const T* Q = reinterpret_cast<const T*>(a.q);
@@ -615,13 +624,17 @@ static void launch_flash(const AttnArgs& a, hipStream_t s) {
     const dim3 grid((a.Sq + 63) / 64 * ns, a.B * a.H);
     WCB_LAUNCH((attn_flash_kernel<T, 1, 2>), grid, dim3(256), 0, s, b);
     if (ns > 1) WCB_LAUNCH(flash_merge_kernel<T>, dim3(a.B * a.H * a.Sq), dim3(64), 0, s, b);
-  } else {   // one key range (the key split is the few-query form only)
+  } else {   // one key range (the key split is the few-query form only); XCD-grouped query blocks
     AttnArgs b = a;
     b.nsplit = 1;
+    const int qb = a.variant == 4 ? 256 : 128, nqb = (a.Sq + qb - 1) / qb, BH = a.B * a.H;
+    const bool xg = nqb > 1 && BH % 8 == 0;
+    b.xcd_nqb = xg ? nqb : 0;
+    const dim3 grid = xg ? dim3(nqb * BH) : dim3(nqb, BH);
     if (a.variant == 4) {   // 64 queries per wave: half the K/V LDS reads per MFMA
-      WCB_LAUNCH((attn_flash_kernel<T, 4, 2>), dim3((a.Sq + 255) / 256, a.B * a.H), dim3(256), 0, s, b);
+      WCB_LAUNCH((attn_flash_kernel<T, 4, 2>), grid, dim3(256), 0, s, b);
     } else {
-      WCB_LAUNCH((attn_flash_kernel<T, 2, 2>), dim3((a.Sq + 127) / 128, a.B * a.H), dim3(256), 0, s, b);
+      WCB_LAUNCH((attn_flash_kernel<T, 2, 2>), grid, dim3(256), 0, s, b);
     }
   }
 }

@@ -127,6 +127,8 @@ struct AttnArgs {
   int row0 = 0, b_div = 1;
   const int* phys = nullptr; long phys_ld = 0;
   int causal = 0;    // decode kernels, Sq > 1 (prefill): query i sees the first nkeys(+dev) + i keys
+  int xcd_nqb = 0;   // flash, > 0: 1-D grid, the xcd_nqb query blocks of one (set, head) on one XCD
+                     // (they share its K/V through that XCD's L2); requires B·H % 8 == 0
   int kv_rows = 0;   // > 0: K/V rows allocated per (row, head) — the one-token self-attention kernel
                      // loads the first keys before the device key count arrives, clamped to this
 };
