@@ -145,7 +145,7 @@ def test_flash_attention_query_groups(dt, B, H, Sq, Sk, split):
     assert torch.equal(_attn(dt, q, k, v, code), o)   # deterministic
 
 
-@pytest.mark.parametrize("code", [1, 100])
+@pytest.mark.parametrize("code", [1, 100, 123, 124])
 def test_flash_attention_xcd_grouped(code):
     """B·H % 8 == 0 (the C2 / C3 / C5 encoder batches): the query blocks of one
     (clip, head) are mapped to one XCD (1-D grid). Same results as the fp64 reference, deterministic."""

@@ -85,7 +85,7 @@ def attn_case(B, H, Sq, Sk, flash):
 
     def fn():
         lib.wcb_op_attention(0, q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), B, H, Sq, Sk, flash, stream())
-    us = per_launch_us(fn, reps=10 if flash == 1 else 50)
+    us = per_launch_us(fn, reps=10 if flash == 1 or flash >= 100 else 50)
     byts = 2 * B * Sk * H * 64 * 2
     fl = 4.0 * B * H * Sq * Sk * 64
     print(f"attn B={B} H={H} Sq={Sq} Sk={Sk} flash={flash}: {us:9.2f} us  {byts / us / 1e3:8.1f} GB/s (KV)  "
@@ -108,4 +108,6 @@ if __name__ == "__main__":
     attn_case(16, 12, 1, 1500, 0)
     attn_case(16, 12, 1, 1500, 4)
     attn_case(32, 12, 1, 64, 0)
-    attn_case(32, 12, 1500, 1500, 1)
+    for code in (1, 100, 123, 124):   # encoder tilings (option enc_flash)
+        attn_case(32, 12, 1500, 1500, code)
+        attn_case(64, 16, 1500, 1500, code)

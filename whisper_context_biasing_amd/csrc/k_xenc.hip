@@ -184,14 +184,14 @@ __global__ __launch_bounds__(512) void attn_xenc_kernel(XencArgs a) {
     cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
     cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
     const float mnew = fmaxf(m_run, cm);            // finite: every chunk holds >= 1 key of the range
-    const float alpha = exp2f((m_run - mnew) * L2E);
+    const float alpha = __builtin_amdgcn_exp2f((m_run - mnew) * L2E);
     m_run = mnew;
     const float mb = mnew * L2E;
     float ls = 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      s0[e] = exp2f(fmaf(s0[e], L2E, -mb));
-      s1[e] = exp2f(fmaf(s1[e], L2E, -mb));
+      s0[e] = __builtin_amdgcn_exp2f(fmaf(s0[e], L2E, -mb));
+      s1[e] = __builtin_amdgcn_exp2f(fmaf(s1[e], L2E, -mb));
       ls += s0[e] + s1[e];
     }
     l_run = l_run * alpha + ls;
@@ -329,23 +329,27 @@ __global__ __launch_bounds__((XregCfg<D, WNW>::NW * 64), ((NR == 2 && WNW == 4) 
     cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
     cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
     const float mnew = fmaxf(m_run, cm);
-    const float alpha = exp2f((m_run - mnew) * L2E);
+    const float alpha = __builtin_amdgcn_exp2f((m_run - mnew) * L2E);
     m_run = mnew;
     const float mb = mnew * L2E;
     float ls = 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      s0[e] = exp2f(fmaf(s0[e], L2E, -mb));
-      s1[e] = exp2f(fmaf(s1[e], L2E, -mb));
+      s0[e] = __builtin_amdgcn_exp2f(fmaf(s0[e], L2E, -mb));
+      s1[e] = __builtin_amdgcn_exp2f(fmaf(s1[e], L2E, -mb));
       ls += s0[e] + s1[e];
     }
     l_run = l_run * alpha + ls;
     const Frag pf = pack_p<T>(s0, s1);
+    if (__any(alpha != 1.f)) {   // rescale only when some head's max moved (exact: alpha is 1 otherwise)
+#pragma unroll
+      for (int t = 0; t < CTW; ++t) acc[t] *= alpha;
+    }
 #pragma unroll
     for (int t = 0; t < CTW; ++t) {
       const int c0 = t * 16;
       const Frag ef = tr_frag<T>(tile + (c0 >> 6) * PANEL, 0, ((c0 & 63) >> 4) * 2, lane);
-      acc[t] = mma16(ef, pf, acc[t] * alpha);
+      acc[t] = mma16(ef, pf, acc[t]);
     }
   };
 

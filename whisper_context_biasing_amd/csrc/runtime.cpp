@@ -164,7 +164,9 @@ struct wcb_handle {
   // (audio-s/s, fold / launch): C3 4425 / 4572, C5 1399 / 1490 — the per-element γ scaling and row
   // sums inside the latency-bound ring loop cost more than the 4.6 µs launch they remove.
   int ln_fold = 0;
-  int enc_flash_qw = 2;   // encoder flash attention: query fragments (16 rows) per wave, 2 or 4
+  // encoder flash attention tiling (option "enc_flash"): 2 = 32 queries per wave, 2 LDS stages;
+  // 4 = 64 queries per wave; 23 / 24 = 32 queries, 3 / 4 stages
+  int enc_flash_qw = 2;
   // Cross-attention formulation: 1 = encoder space (k_xenc.hip: the step streams the encoder output,
   // no cross-K/V precompute; 16-bit dtypes, d <= 1024), 0 = precomputed per-layer K/V (f32 "exact"
   // mode, large-v3). Fixed at create (WCB_XMODE overrides where supported).
@@ -513,8 +515,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "xenc_variant") {
       REQUIRE(value >= 0 && value <= 3, "option xenc_variant: 0..3");
       h->xenc_variant = value;
-    } else if (n == "enc_flash_qw") {
-      REQUIRE(value == 2 || value == 4, "option enc_flash_qw: 2 or 4");
+    } else if (n == "enc_flash") {
+      REQUIRE(value == 2 || value == 4 || value == 23 || value == 24, "option enc_flash: 2, 4, 23 or 24");
       h->enc_flash_qw = value;
     } else if (n == "ln_fold") {
       h->ln_fold = value != 0;
@@ -1772,8 +1774,9 @@ int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, voi
     a.q = q; a.ldq = ld; a.q_Sb = Sq; a.Sq = Sq;
     a.k = k; a.v = v; a.k_sb = (long)Sk * ld; a.k_sh = 64; a.k_sk = ld;
     a.o = o; a.ldo = ld; a.o_Sb = Sq; a.B = B; a.H = H; a.nkeys = Sk;
-    if (flash == 1 || flash == 100 || flash < 0) {   // 100: 64 queries per wave; -n: n key ranges + merge (Sq <= 16)
-      a.variant = flash == 100 ? 4 : 1;
+    if (flash == 1 || flash == 100 || flash == 123 || flash == 124 || flash < 0) {
+      // 100: 64 queries per wave; 123 / 124: 3 / 4 LDS stages; -n: n key ranges + merge (Sq <= 16)
+      a.variant = flash == 100 ? 4 : flash == 123 ? 23 : flash == 124 ? 24 : 1;
       REQUIRE(dtype != WCB_F32, "flash attention needs a 16-bit dtype");
       static DevBuf fpart;
       if (flash < 0) {
