@@ -426,13 +426,16 @@ void attention_decode(DType t, const AttnArgs& a, hipStream_t s) {
 }
 
 // --------------------------------------------------------------------------------- flash (MFMA)
+// Registers: scores and softmax of every query fragment first, then P·V with one 16-row block of Vᵀ
+// fragments live at a time; 32 queries per wave fit 3 waves per SIMD (152 VGPRs), 64 queries per wave
+// 2 (the encoder default: half the K/Vᵀ LDS reads per MFMA; 3 spills).
 // Softmax exponentials are bare v_exp_f32 (__builtin_amdgcn_exp2f): libm's exp2f wraps each one in a
 // denormal range fix-up (compare, two selects, ldexp) — 4 extra VALU per score on a VALU-bound loop;
 // the arguments are ≤ 0 here and results below 2^-126 contribute nothing.
 // NS LDS stages (NS - 1 K/V tiles in flight behind the one being multiplied). 2 everywhere: a
 // third stage measured 3.6 % slower on the beam cross-attention (C3: 90.9 vs 87.7 µs per launch).
 template <typename T, int QW, int NS>
-__global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnArgs a) {
   using Frag = typename DT<T>::frag;
   constexpr int QB = 4 * QW * 16;     // query rows per workgroup
   __shared__ __attribute__((aligned(16))) char lds[NS][2][64 * 128];   // [stage][K|V][64 keys x 128 B]
@@ -516,14 +519,12 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
         const int r = mf * 16 + (lane & 15);
         kf[mf][ks] = *reinterpret_cast<const Frag*>(kt_l + swz(r, ks * 4 + (lane >> 4)));
       }
-    // Vᵀ fragments (A operand of Oᵀ): rows = dd 16mf' + (lane&15), k = keys (permuted)
-    Frag vf[4][2];
-#pragma unroll
-    for (int mf = 0; mf < 4; ++mf)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) vf[mf][ks] = tr_frag<T>(vt_l, ks * 32, mf * 2, lane);
     const int kabs = (t_lo + kt) * 64;   // first key of this tile
     const bool tail = kabs + 64 > S;
+    // scores and softmax of every query fragment first, then P·V with the Vᵀ fragments of one
+    // 16-row dd block live at a time (read once, used by every query fragment): 8 VGPRs of Vᵀ instead
+    // of 32 keeps the kernel at 3 waves per SIMD
+    Frag pf[QW][2];
 #pragma unroll
     for (int qi = 0; qi < QW; ++qi) {
       f32x4 s[4];
@@ -561,11 +562,17 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(AttnArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[qi][j] *= alpha;
       }
-      const Frag p0 = pack_p<T>(s[0], s[1]), p1 = pack_p<T>(s[2], s[3]);
+      pf[qi][0] = pack_p<T>(s[0], s[1]);
+      pf[qi][1] = pack_p<T>(s[2], s[3]);
+    }
+    // Vᵀ fragments (A operand of Oᵀ): rows = dd 16mf + (lane&15), k = keys (permuted)
 #pragma unroll
-      for (int mf = 0; mf < 4; ++mf) {
-        o[qi][mf] = mma16(vf[mf][0], p0, o[qi][mf]);
-        o[qi][mf] = mma16(vf[mf][1], p1, o[qi][mf]);
+    for (int mf = 0; mf < 4; ++mf) {
+      const Frag v0 = tr_frag<T>(vt_l, 0, mf * 2, lane), v1 = tr_frag<T>(vt_l, 32, mf * 2, lane);
+#pragma unroll
+      for (int qi = 0; qi < QW; ++qi) {
+        o[qi][mf] = mma16(v0, pf[qi][0], o[qi][mf]);
+        o[qi][mf] = mma16(v1, pf[qi][1], o[qi][mf]);
       }
     }
   }

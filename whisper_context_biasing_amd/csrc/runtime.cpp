@@ -165,8 +165,9 @@ struct wcb_handle {
   // sums inside the latency-bound ring loop cost more than the 4.6 µs launch they remove.
   int ln_fold = 0;
   // encoder flash attention tiling (option "enc_flash"): 2 = 32 queries per wave, 2 LDS stages;
-  // 4 = 64 queries per wave; 23 / 24 = 32 queries, 3 / 4 stages
-  int enc_flash_qw = 2;
+  // 4 = 64 queries per wave; 23 / 24 = 32 queries, 3 / 4 stages. Measured (tools/microbench.py,
+  // small / medium encoder shapes, µs): 2: 358 / 878, 4: 313 / 808, 23: 328 / 887, 24: 399 / 1041
+  int enc_flash_qw = 4;
   // Cross-attention formulation: 1 = encoder space (k_xenc.hip: the step streams the encoder output,
   // no cross-K/V precompute; 16-bit dtypes, d <= 1024), 0 = precomputed per-layer K/V (f32 "exact"
   // mode, large-v3). Fixed at create (WCB_XMODE overrides where supported).
