@@ -64,6 +64,7 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "xenc_variant" v   encoder-space kernel variant, "xvariant" v  K/V cross-attention kernel variant
  *   "flash_split" n    key ranges per (clip, head) of the beam-search cross-attention (flash kernel), 1..8
  *   "ln_fold" 0/1      decode rows > 64 (16-bit): LayerNorm folded into the projection, or its own launch
+ *   "merge_v" 0/1      greedy encoder-space cross-attention: range merge and W_v fused (1) or two launches
  *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave, 2 LDS stages), 4 (64 queries),
  *                      23 / 24 (32 queries, 3 / 4 LDS stages) */
 int wcb_set_option(wcb_handle* h, const char* name, int value);
@@ -181,7 +182,8 @@ int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void*
 /* decoder cross-attention in encoder space (k_xenc.hip), the xmode-1 decode path:
  * o[B][d] = Σ_h-blocks W_v,h softmax_j(q'_h · enc_j) enc_j + b_v with q'_h = W_k,hᵀ q_h;
  * q [B][H*64] (pre-scaled by 1/8), enc [B][S][d], wkt = W_k repacked [H][d][64] (element (h,c,i) =
- * W_k[h*64+i][c]), wv [d][d] (HF layout), bv f32 [d]; nsplit key ranges per row (1..16). 16-bit dtypes. */
+ * W_k[h*64+i][c]), wv [d][d] (HF layout), bv f32 [d]; nsplit key ranges per row (1..16). 16-bit dtypes.
+ * variant: attn_xenc kernel variant; + 100 = merge kernel + grouped W_v GEMM instead of the fused merge. */
 int wcb_op_cross_attention_enc(int dtype, const void* q, const void* enc, const void* wkt, const void* wv,
                                const float* bv, void* o, int B, int H, int S, int nsplit, int variant, void* stream);
 

@@ -433,6 +433,87 @@ __global__ __launch_bounds__(256) void xenc_merge_kernel(XencArgs a, T* u, long 
   }
 }
 
+// xenc_merge_v_kernel: the range merge and the value projection in one launch (replaces
+// xenc_merge_kernel + the grouped W_v decode GEMM: one dependent launch fewer per layer).
+// Workgroup = (head h, row): u = Σ_s w_s·part_s / L as in xenc_merge_kernel (rounded to T, as the
+// unfused path stores it), kept in LDS; then o[h·64 + j] = Σ_c W_v[h·64 + j][c]·u[c] + b_v[h·64 + j],
+// 16 lanes per output (each 16-byte weight load of a lane group covers 256 contiguous bytes of a
+// W_v row), 64 outputs in 4 passes of the 4 waves. Every weight load is issued before the partials
+// arrive (they do not depend on them).
+template <typename T, int D>
+__global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* wv, const float* bv, T* out, long ldo) {
+  using Frag = typename DT<T>::frag;
+  constexpr int CPL = D / 128;          // 16-byte chunks per lane per output row (D/8 chunks over 16 lanes)
+  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ns = a.nsplit;
+  __shared__ float2 sv[kXencMaxSplit];
+  __shared__ __attribute__((aligned(16))) float us[D];
+  // weights first: pass p, output j = 16p + 4·wave + (lane >> 4), chunks (k·16 + (lane & 15))
+  Frag wf[4][CPL];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int j = 16 * p + 4 * wave + (lane >> 4);
+    const T* wr = wv + (long)(h * 64 + j) * D + (lane & 15) * 8;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) wf[p][k] = load_frag<T>(wr + k * 128);
+  }
+  if (tid < kXencMaxSplit)
+    sv[tid] = tid < ns ? *reinterpret_cast<const float2*>(a.ml + (((long)b * ns + tid) * a.H + h) * 2) : float2{0.f, 0.f};
+  __syncthreads();
+  float2 v[kXencMaxSplit];
+#pragma unroll
+  for (int s = 0; s < kXencMaxSplit; ++s) v[s] = sv[s];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < kXencMaxSplit; ++s)
+    if (s < ns && v[s].y > 0.f) mx = fmaxf(mx, v[s].x);
+  float w[kXencMaxSplit];
+  float L = 0.f;
+#pragma unroll
+  for (int s = 0; s < kXencMaxSplit; ++s) {
+    w[s] = (s < ns && v[s].y > 0.f) ? __expf(v[s].x - mx) : 0.f;   // empty ranges publish Σp = 0
+    L += w[s] * v[s].y;
+  }
+  const float inv = 1.f / L;
+  const float* pp = a.part + ((long)b * ns * a.H + h) * D;
+  for (int c = tid * 4; c < D; c += 1024) {
+    f32x4 pv[kXencMaxSplit];
+#pragma unroll
+    for (int s = 0; s < kXencMaxSplit; ++s) pv[s] = *reinterpret_cast<const f32x4*>(pp + (long)min(s, ns - 1) * a.H * D + c);
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < kXencMaxSplit; ++s) acc += w[s] * pv[s];
+    acc *= inv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] = DT<T>::tof(DT<T>::fromf(acc[e]));   // u in T, as stored unfused
+    *reinterpret_cast<f32x4*>(us + c) = acc;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    float dsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int c = (k * 16 + (lane & 15)) * 8;
+      const f32x4 u0 = *reinterpret_cast<const f32x4*>(us + c);
+      const f32x4 u1 = *reinterpret_cast<const f32x4*>(us + c + 4);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float wv_e;
+        if constexpr (__is_same(T, bf16_t)) wv_e = bf16_to_f((bf16_t)wf[p][k][e]);
+        else wv_e = float(wf[p][k][e]);
+        dsum = fmaf(wv_e, e < 4 ? u0[e] : u1[e - 4], dsum);
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) dsum += __shfl_xor(dsum, o, 64);
+    if ((lane & 15) == 0) {
+      const int n = h * 64 + 16 * p + 4 * wave + (lane >> 4);
+      out[(long)b * ldo + n] = DT<T>::fromf(dsum + bv[n]);
+    }
+  }
+}
+
 bool xenc_supported(DType t, int D) {
   return (t == kBF16 || t == kF16) && (D == 384 || D == 768 || D == 1024 || D == 64 || D == 128 || D == 256 || D == 512);
 }
@@ -502,6 +583,19 @@ static void launch_merge_t(const XencArgs& a, void* u, long ldu, hipStream_t s) 
 void xenc_merge(DType t, const XencArgs& a, void* u, long ldu, hipStream_t s) {
   if (t == kBF16) launch_merge_t<bf16_t>(a, u, ldu, s);
   else if (t == kF16) launch_merge_t<f16_t>(a, u, ldu, s);
+}
+
+template <typename T>
+static void launch_merge_v_t(const XencArgs& a, const void* wv, const float* bv, void* o, long ldo, hipStream_t s) {
+  const dim3 grid(a.H, a.rows);
+#define WCB_XC(DD) case DD: WCB_LAUNCH((xenc_merge_v_kernel<T, DD>), grid, dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo); break;
+  switch (a.D) { WCB_XC(128) WCB_XC(256) WCB_XC(384) WCB_XC(512) WCB_XC(768) WCB_XC(1024) default: break; }
+#undef WCB_XC
+}
+
+void xenc_merge_v(DType t, const XencArgs& a, const void* wv, const float* bv, void* o, long ldo, hipStream_t s) {
+  if (t == kBF16) launch_merge_v_t<bf16_t>(a, wv, bv, o, ldo, s);
+  else if (t == kF16) launch_merge_v_t<f16_t>(a, wv, bv, o, ldo, s);
 }
 
 }  // namespace wcb

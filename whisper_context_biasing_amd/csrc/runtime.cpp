@@ -164,6 +164,8 @@ struct wcb_handle {
   // (audio-s/s, fold / launch): C3 4425 / 4572, C5 1399 / 1490 — the per-element γ scaling and row
   // sums inside the latency-bound ring loop cost more than the 4.6 µs launch they remove.
   int ln_fold = 0;
+  // greedy cross-attention (encoder space): range merge and W_v in one launch (option "merge_v")
+  int merge_v = 1;
   // encoder flash attention tiling (option "enc_flash"): 2 = 32 queries per wave, 2 LDS stages;
   // 4 = 64 queries per wave; 23 / 24 = 32 queries, 3 / 4 stages. Measured (tools/microbench.py,
   // small / medium encoder shapes, µs): 2: 358 / 878, 4: 313 / 808, 23: 328 / 887, 24: 399 / 1041
@@ -519,6 +521,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "enc_flash") {
       REQUIRE(value == 2 || value == 4 || value == 23 || value == 24, "option enc_flash: 2, 4, 23 or 24");
       h->enc_flash_qw = value;
+    } else if (n == "merge_v") {
+      h->merge_v = value != 0;
     } else if (n == "ln_fold") {
       h->ln_fold = value != 0;
     } else if (n == "flash_split") {
@@ -1031,12 +1035,17 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       // algorithmic bytes: every distinct clip's encoder output once (beams of a clip share it)
       h->timed("dec_xattn", 4.0 * M * H * (double)S * d, (double)nb / c.nb * S * d * e, st_,
                [&] { xenc_attention(h->dt, xa, st_); });
-      char* du = (char*)D.du.p + (size_t)r0 * H * d * e;
-      h->timed("dec_xmerge", 0, (double)M * H * d * (h->xenc_split * 4.0 + e), st_,
-               [&] { xenc_merge(h->dt, xa, du, (long)H * d, st_); });
-      GemmArgs vg = drow(du, (long)H * d, w.xv_w, M, d, d, datt, d);    // o_h = W_v,h u_h + b_v,h
-      vg.a_grp_n = 64; vg.a_grp_off = d; vg.bias = w.xv_b;
-      proj("dec_vg", vg);
+      if (h->merge_v && d % 128 == 0) {   // range merge + o_h = W_v,h u_h + b_v,h in one launch
+        h->timed("dec_xmerge", 0, (double)M * H * d * h->xenc_split * 4.0 + (double)d * d * e, st_,
+                 [&] { xenc_merge_v(h->dt, xa, w.xv_w, w.xv_b, datt, d, st_); });
+      } else {
+        char* du = (char*)D.du.p + (size_t)r0 * H * d * e;
+        h->timed("dec_xmerge", 0, (double)M * H * d * (h->xenc_split * 4.0 + e), st_,
+                 [&] { xenc_merge(h->dt, xa, du, (long)H * d, st_); });
+        GemmArgs vg = drow(du, (long)H * d, w.xv_w, M, d, d, datt, d);    // o_h = W_v,h u_h + b_v,h
+        vg.a_grp_n = 64; vg.a_grp_off = d; vg.bias = w.xv_b;
+        proj("dec_vg", vg);
+      }
     } else {
       // cross attention over the precomputed encoder K/V
       GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
@@ -1740,12 +1749,16 @@ int wcb_op_cross_attention_enc(int dtype, const void* q, const void* enc, const 
     XencArgs xa;
     xa.enc = enc; xa.enc_sb = (long)S * d; xa.qp = qp.p; xa.rows = B; xa.H = H; xa.D = d; xa.S = S;
     xa.nsplit = nsplit; xa.part = part.as<float>(); xa.ml = ml.as<float>();
-    xa.variant = variant;
+    xa.variant = variant % 100;
     xenc_attention(DType(dtype), xa, (hipStream_t)stream);
-    xenc_merge(DType(dtype), xa, u.p, (long)H * d, (hipStream_t)stream);
-    GemmArgs vg = rowgemm(u.p, (long)H * d, wv, B, d, d, o, d);
-    vg.a_grp_n = 64; vg.a_grp_off = d; vg.bias = bv;
-    gemm(DType(dtype), vg, (hipStream_t)stream);
+    if (d % 128 == 0 && variant < 100) {   // the runtime's default: merge + W_v fused
+      xenc_merge_v(DType(dtype), xa, wv, bv, o, d, (hipStream_t)stream);
+    } else {   // variant + 100: merge kernel + grouped W_v GEMM (option merge_v = 0, and d = 64)
+      xenc_merge(DType(dtype), xa, u.p, (long)H * d, (hipStream_t)stream);
+      GemmArgs vg = rowgemm(u.p, (long)H * d, wv, B, d, d, o, d);
+      vg.a_grp_n = 64; vg.a_grp_off = d; vg.bias = bv;
+      gemm(DType(dtype), vg, (hipStream_t)stream);
+    }
     HIPCHK(hipGetLastError());
   });
 }
