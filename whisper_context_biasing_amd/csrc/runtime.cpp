@@ -164,8 +164,9 @@ struct wcb_handle {
   // (audio-s/s, fold / launch): C3 4425 / 4572, C5 1399 / 1490 — the per-element γ scaling and row
   // sums inside the latency-bound ring loop cost more than the 4.6 µs launch they remove.
   int ln_fold = 0;
-  // greedy cross-attention (encoder space): range merge and W_v in one launch (option "merge_v")
-  int merge_v = 0;
+  // greedy cross-attention (encoder space): range merge and W_v in one launch (option "merge_v";
+  // C2 16,570 vs 16,259 audio-s/s for the two launches)
+  int merge_v = 1;
   // encoder flash attention tiling (option "enc_flash"): 2 = 32 queries per wave, 2 LDS stages;
   // 4 = 64 queries per wave; 23 / 24 = 32 queries, 3 / 4 stages. Measured (tools/microbench.py,
   // small / medium encoder shapes, µs): 2: 358 / 878, 4: 313 / 808, 23: 328 / 887, 24: 399 / 1041
