@@ -318,8 +318,9 @@ __global__ __launch_bounds__(NW * 64) void attn_decode2p_kernel(AttnArgs a) {
 // per load, 8 loads of K and of V per lane in flight.
 // PHYS (beam search): key j of row b lives in cache row phys[(row0 + b)·phys_ld + j]; lane j of the
 // wave loads the map entry of key j0 + j once per 64-key chunk and the K/V row offsets are shuffled
-// from it (one dependent round trip per chunk, not one per key group). Loading only the key groups
-// below the device-side count instead (a branch on it) measured slower: C3 22.8 -> 38.3 µs.
+// from it (one dependent round trip per chunk, not one per key group). Skipping the key groups past
+// the device-side count by a branch measured slower (C3 22.8 -> 38.3 µs); clamping their index to the
+// last key (no branch) keeps the loads but collapses them onto one cache line.
 template <typename T, bool PHYS>
 __global__ __launch_bounds__(64) void attn_self_kernel(AttnArgs a) {
   const int b = blockIdx.y / a.H, h = blockIdx.y % a.H, lane = threadIdx.x;
@@ -336,11 +337,27 @@ __global__ __launch_bounds__(64) void attn_self_kernel(AttnArgs a) {
   };
   float qv[8], kv[8][8], vv[8][8];
   load8f<T>(q + seg * 8, qv);
-#pragma unroll
-  for (int u = 0; u < 8; ++u) load8f<T>(kb + koff(min(u * 8 + kg, cap), u), kv[u]);
-#pragma unroll
-  for (int u = 0; u < 8; ++u) load8f<T>(vb + koff(min(u * 8 + kg, cap), u), vv[u]);
   const int nk = a.nkeys_dev ? (*a.nkeys_dev + a.nkeys_add) : a.nkeys;
+  if constexpr (PHYS) {
+    // the key count arrives with the map (the same round trip): keys past it re-read key nk − 1
+    // (one cache line for all of them) instead of fetching rows that are masked anyway
+    const int kl = min(nk, a.kv_rows) - 1;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int kk = min(u * 8 + kg, kl);
+      load8f<T>(kb + (long)kk * a.k_sk + (long)__shfl(pj, kk, 64) * a.k_sb, kv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int kk = min(u * 8 + kg, kl);
+      load8f<T>(vb + (long)kk * a.k_sk + (long)__shfl(pj, kk, 64) * a.k_sb, vv[u]);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) load8f<T>(kb + koff(min(u * 8 + kg, cap), u), kv[u]);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) load8f<T>(vb + koff(min(u * 8 + kg, cap), u), vv[u]);
+  }
   float m = -INFINITY, l = 0.f;
   float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int j0 = 0; j0 < nk; j0 += 64) {
