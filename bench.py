@@ -97,7 +97,13 @@ def _pmc_traffic(kernel: str):
     PMC passes (profiles/*pmc*.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2 (gfx950
     correction) + WRITE_SIZE), or None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+    # profiles/ stays on the build host (.gpurunignore); the latest PMC summary also ships as
+    # tools/pmc_traffic_latest.json (a copy of the newest profiles/*pmc_traffic.json)
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True)
+    paths.append(os.path.join(ROOT, "tools", "pmc_traffic_latest.json"))
+    for path in paths:
+        if not os.path.exists(path):
+            continue
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
