@@ -274,13 +274,17 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(GemmArgs g) {
 // 16-bit residual rows; each A fragment is scaled by γ (staged in LDS) after its LDS read while the
 // row's Σx, Σx² accumulate from the same values; the epilogue applies r·(acc − μ·u[n]) + c[n].
 constexpr int kLnfMaxK = 1280;
-template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false>
+// KT: 64-deep sub-tiles per ring stage (2 for the small decode-row tiles: half the K-loop
+// iterations, and with them half the barriers, of a loop that is latency-bound at 2-8 MFMAs per wave
+// per sub-tile).
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
+  static_assert(!LNF || KT == 1, "the folded LayerNorm indexes gamma by 64-deep K tiles");
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BK = 64, CE = 8;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
-  constexpr int STAGE = (BM + BN) * 128;
-  constexpr int IA = BM / 8 / NW, IB = BN / 8 / NW, GL = IA + IB;   // glds per wave per K tile
+  constexpr int SUB = (BM + BN) * 128, STAGE = SUB * KT;
+  constexpr int IA = BM / 8 / NW, IB = BN / 8 / NW, GL = (IA + IB) * KT;   // glds per wave per stage
   static_assert(IA * NW * 8 == BM && IB * NW * 8 == BN, "tile rows must split over waves");
   using Frag = typename DT<T>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -308,11 +312,14 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
     b_src[i] = W + n * g.ldw + ((lane & 7) ^ ((r >> 1) & 7)) * CE;
   }
   auto stage = [&](int st, int k0) {
-    char* base = smem + st * STAGE;
 #pragma unroll
-    for (int i = 0; i < IA; ++i) glds16(a_src[i] + k0, base + (wave + i * NW) * 1024);
+    for (int t = 0; t < KT; ++t) {
+      char* base = smem + st * STAGE + t * SUB;
 #pragma unroll
-    for (int i = 0; i < IB; ++i) glds16(b_src[i] + k0, base + BM * 128 + (wave + i * NW) * 1024);
+      for (int i = 0; i < IA; ++i) glds16(a_src[i] + k0 + t * BK, base + (wave + i * NW) * 1024);
+#pragma unroll
+      for (int i = 0; i < IB; ++i) glds16(b_src[i] + k0 + t * BK, base + BM * 128 + (wave + i * NW) * 1024);
+    }
   };
 
   f32x4 acc[FM][FN];
@@ -332,10 +339,10 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
     __syncthreads();
   }
 
-  const int nk = g.K / BK;
+  const int nk = g.K / (BK * KT);
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
-    if (p < nk) stage(p, p * BK);
+    if (p < nk) stage(p, p * BK * KT);
   int st = 0;
   for (int kt = 0; kt < nk; ++kt) {
     // tiles issued so far: kt .. min(nk, kt + NS - 1) - 1; keep the ones after kt in flight
@@ -358,11 +365,12 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
       const int nxt = kt + NS - 1;
       int sn = st + NS - 1;
       if (sn >= NS) sn -= NS;
-      if (nxt < nk) stage(sn, nxt * BK);
+      if (nxt < nk) stage(sn, nxt * BK * KT);
     }
-    const char* base = smem + st * STAGE;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int kq = 0; kq < 2 * KT; ++kq) {
+      const char* base = smem + st * STAGE + (kq >> 1) * SUB;
+      const int ks = kq & 1;
       Frag a[FM], b[FN];
       const int c = ks * 4 + (lane >> 4);
 #pragma unroll
@@ -459,21 +467,21 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
   }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false>
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1>
 static void launch_ring_e(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
-  constexpr int stage_bytes = NS * (BM + BN) * 128 + (LNF ? (kLnfMaxK + 2 * BM) * 4 : 0);
+  constexpr int stage_bytes = NS * (BM + BN) * 128 * KT + (LNF ? (kLnfMaxK + 2 * BM) * 4 : 0);
   constexpr int epi_full = BM * (BN + 4) * 4;
   constexpr int epi_bytes = epi_full <= 160 * 1024 ? epi_full : epi_full / WM;
   constexpr int lds = stage_bytes > epi_bytes ? stage_bytes : epi_bytes;
   static_assert(lds <= 160 * 1024, "LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF>,
+    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
-  WCB_LAUNCH((gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
+  WCB_LAUNCH((gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
 }
 
 template <typename T, int BM, int BN, int WM, int WN, int NS>
@@ -1084,14 +1092,18 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
           (!g.ln_u || g.K <= kLnfMaxK)) {
         const int mt = (g.M + 63) / 64;
         const bool lnf = g.ln_u != nullptr;
+        const bool kt2 = g.ring_kt == 2 && g.K % 128 == 0 && !lnf;   // 128-deep stages
         if (g.N % 64 == 0 && mt * (g.N / 64) >= 240) {
           if (lnf) launch_ring_e<T, 64, 64, 2, 2, 4, E_RUNTIME, true>(g, s);
+          else if (kt2) launch_ring_e<T, 64, 64, 2, 2, 3, E_RUNTIME, false, 2>(g, s);
           else launch_ring_e<T, 64, 64, 2, 2, 4, E_RUNTIME>(g, s);
         } else if (mt * ((g.N + 31) / 32) >= 240) {
           if (lnf) launch_ring_e<T, 64, 32, 2, 2, 6, E_RUNTIME, true>(g, s);
+          else if (kt2) launch_ring_e<T, 64, 32, 2, 2, 4, E_RUNTIME, false, 2>(g, s);
           else launch_ring_e<T, 64, 32, 2, 2, 6, E_RUNTIME>(g, s);
         } else {
           if (lnf) launch_ring_e<T, 32, 32, 2, 2, 6, E_RUNTIME, true>(g, s);
+          else if (kt2) launch_ring_e<T, 32, 32, 2, 2, 4, E_RUNTIME, false, 2>(g, s);
           else launch_ring_e<T, 32, 32, 2, 2, 6, E_RUNTIME>(g, s);
         }
         return;

@@ -70,6 +70,7 @@ struct GemmArgs {
   // (n0 / a_grp_n) · a_grp_off elements further (q'_h = W_k,hᵀ q_h: K = 64 columns of head h)
   int a_grp_n = 0; long a_grp_off = 0;
   int skinny = 0;                  // decode projection: the skinny kernel whatever M (row blocks over grid.y)
+  int ring_kt = 1;                 // tile 2: 64-deep K sub-tiles per LDS-ring stage (1 or 2)
   // decode GEMM (gemm_dec_kernel): a T-typed copy of the f32 rows the epilogue writes (the
   // residual stream x → x16, read back as the LN-fused A operand of the next projection), and the
   // LN-fused A read from such a copy instead of the f32 rows (lda elements per row)

@@ -167,6 +167,7 @@ struct wcb_handle {
   // greedy cross-attention (encoder space): range merge and W_v in one launch (option "merge_v";
   // C2 16,570 vs 16,259 audio-s/s for the two launches)
   int merge_v = 1;
+  int ring_kt = 1;   // decode rows > 64: 64-deep K sub-tiles per ring stage (option "ring_kt", 1 or 2)
   // encoder flash attention tiling (option "enc_flash"): 2 = 32 queries per wave, 2 LDS stages;
   // 4 = 64 queries per wave; 23 / 24 = 32 queries, 3 / 4 stages. Measured (tools/microbench.py,
   // small / medium encoder shapes, µs): 2: 358 / 878, 4: 313 / 808, 23: 328 / 887, 24: 399 / 1041
@@ -522,6 +523,9 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "enc_flash") {
       REQUIRE(value == 2 || value == 4 || value == 23 || value == 24, "option enc_flash: 2, 4, 23 or 24");
       h->enc_flash_qw = value;
+    } else if (n == "ring_kt") {
+      REQUIRE(value == 1 || value == 2, "option ring_kt: 1 or 2");
+      h->ring_kt = value;
     } else if (n == "merge_v") {
       h->merge_v = value != 0;
     } else if (n == "ln_fold") {
@@ -979,7 +983,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
         g.A = dh; g.lda = d;
         g.ln_w = g.ln_b = nullptr; g.st_in = nullptr; g.ln_a16 = nullptr;
       }
-      g.tile = ring ? 2 : 1; g.skinny = 0;
+      g.tile = ring ? 2 : 1; g.skinny = 0; g.ring_kt = h->ring_kt;
     }
     dgemm(h, cls, g, st_);
   };
