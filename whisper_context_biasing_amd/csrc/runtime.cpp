@@ -167,7 +167,9 @@ struct wcb_handle {
   // greedy cross-attention (encoder space): range merge and W_v in one launch (option "merge_v";
   // C2 16,570 vs 16,259 audio-s/s for the two launches)
   int merge_v = 1;
-  int ring_kt = 1;   // decode rows > 64: 64-deep K sub-tiles per ring stage (option "ring_kt", 1 or 2)
+  // decode rows > 64: 64-deep K sub-tiles per ring stage of the 64x32 / 32x32 tiles (option "ring_kt",
+  // 1 or 2; C5 1,594 -> 1,644 audio-s/s)
+  int ring_kt = 2;
   // encoder flash attention tiling (option "enc_flash"): 2 = 32 queries per wave, 2 LDS stages;
   // 4 = 64 queries per wave; 23 / 24 = 32 queries, 3 / 4 stages. Measured (tools/microbench.py,
   // small / medium encoder shapes, µs): 2: 358 / 878, 4: 313 / 808, 23: 328 / 887, 24: 399 / 1041
