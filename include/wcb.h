@@ -66,6 +66,7 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "ln_fold" 0/1      decode rows > 64 (16-bit): LayerNorm folded into the projection, or its own launch
  *   "merge_v" 0/1      greedy encoder-space cross-attention: range merge and W_v fused (1) or two launches
  *   "ring_kt" 1/2      decode rows > 64: 64-deep K sub-tiles per LDS-ring stage of the projection tiles
+ *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)
  *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave, 2 LDS stages), 4 (64 queries),
  *                      23 / 24 (32 queries, 3 / 4 LDS stages) */
 int wcb_set_option(wcb_handle* h, const char* name, int value);

@@ -525,6 +525,10 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "enc_flash") {
       REQUIRE(value == 2 || value == 4 || value == 23 || value == 24, "option enc_flash: 2, 4, 23 or 24");
       h->enc_flash_qw = value;
+    } else if (n == "xenc_split") {
+      REQUIRE(!h->ready, "option xenc_split: set before the weights are finalized");
+      REQUIRE(value >= 1 && value <= kXencMaxSplit, "option xenc_split: 1..16");
+      h->xenc_split = value;
     } else if (n == "ring_kt") {
       REQUIRE(value == 1 || value == 2, "option ring_kt: 1 or 2");
       h->ring_kt = value;
