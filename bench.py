@@ -13,9 +13,14 @@ broadcast once over RCCL/xGMI (`dist.broadcast`), no collective in the timed reg
 barriers; time = max over ranks.
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus `roofline` (dominant kernel:
-the encoder MFMA GEMMs, timed with HIP events on the library's stream inside the timed region)
-and `cpu_baseline` (the fp32 PyTorch-CPU restatement, both reference decode modes, timed on this
-host, rank 0 / N=1 only).
+the kernel symbol with the most device time per step, grouped as rocprofv3 --stats groups them; its
+per-launch time from begin/end timestamps of every launch in a serialised profiling pass) and
+`cpu_baseline` (the fp32 PyTorch-CPU restatement, both reference decode modes, timed on this host,
+rank 0 / N=1 only).
+
+`--reference-mode`: the reference's own decode contract instead of the benchmark mode —
+natural EOS, max_length=225, no boost (scripts/evaluation.py:173-179), same clips; its line goes to
+profiles/ beside the benchmark line (not the driver's headline).
 """
 from __future__ import annotations
 
@@ -52,44 +57,78 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(size: str, n_tokens: int, n_phr: int, boost: float, seed: int = 0, clips: int = 1):
+def _cpu_share():
+    """CPUs this process may actually use: the affinity mask and the cgroup v2/v1 CPU quota (the GPU
+    box gives each job a share of a large host: os.cpu_count() counts the whole host)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = q / per if q > 0 else None
+        except (OSError, ValueError):
+            pass
+    share = aff if quota is None else max(1, min(aff, int(quota)))
+    return share, aff, quota
+
+
+def cpu_baseline(size: str, n_tokens: int, n_phr: int, boost: float, seed: int = 0, clips: int = 1, reps: int = 5,
+                 warmups: int = 3):
     """the fp32 PyTorch-CPU restatement of the reference path (oracle/whisper_torch.py,
-    test infrastructure) on the host cores, on a bounded sample of the same workload (log-mel + encoder
-    + n_tokens greedy tokens with the same bias list and boost), in the reference's two decode modes:
-    (i) use_cache=False exactly as scripts/evaluation.py:178 configures generate(), (ii) KV-cached.
-    `value` is the faster mode (ii). One untimed warm-up clip, then `clips` timed clips per mode."""
+    test infrastructure) on this host's CPU share (affinity mask / cgroup quota; os.cpu_count() counts
+    the whole host), on a bounded sample of the same workload — `clips` clip(s) per run: log-mel +
+    encoder + n_tokens greedy tokens with the same bias list and boost — in the reference's two decode
+    modes: (i) use_cache=False exactly as scripts/evaluation.py:178 configures generate(), (ii)
+    KV-cached. `warmups` untimed runs, then the median of `reps` timed runs per mode (the runs of the
+    two modes interleaved). `value` = mode (ii), the faster one. Nothing is extrapolated: the sample
+    is `clips` clip(s) per run, not the 32-clip batch."""
     import torch
     from oracle import whisper_torch as WT
     from whisper_context_biasing_amd.config import get_dims
     from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list, synth_word_start
     from whisper_context_biasing_amd.weights import make_weights
+    share, aff, quota = _cpu_share()
+    torch.set_num_threads(share)
     dims = get_dims(size)
     m = WT.TorchWhisper(dims, make_weights(dims, seed=seed))
     pcm = torch.from_numpy(synth_batch(clips))
     phrases = synth_bias_list(n_phr, eot=dims.eos_token_id)
-    kw = dict(max_length=n_tokens, min_new_tokens=n_tokens, bias=phrases, bias_boost=boost,
+    kw = dict(min_new_tokens=n_tokens, bias=phrases, bias_boost=boost,
               word_start=synth_word_start(dims.eos_token_id, dims.vocab))
 
-    def run(use_cache, n):
+    def run(use_cache, tokens=n_tokens):
         t0 = time.perf_counter()
-        mel = WT.log_mel(pcm[:n], dims.n_mel)
-        m.generate(mel, use_cache=use_cache, **kw)
+        mel = WT.log_mel(pcm, dims.n_mel)
+        m.generate(mel, use_cache=use_cache, max_length=tokens, **dict(kw, min_new_tokens=tokens))
         return time.perf_counter() - t0
 
     with torch.no_grad():
-        run(True, 1)                                  # warm-up (thread pool, allocator)
-        t_cached = run(True, clips)
-        t_nocache = run(False, clips)
+        for i in range(warmups):                      # thread pool, allocator, page-in (short runs)
+            run(i % 2 == 0, tokens=4)
+        t_c, t_n = [], []
+        for _ in range(reps):
+            t_c.append(run(True))
+            t_n.append(run(False))
+    t_cached, t_nocache = float(np.median(t_c)), float(np.median(t_n))
     return {"value": round(clips * 30.0 / t_cached, 3), "unit": "audio-seconds/sec",
             "cores": torch.get_num_threads(), "kind": "port",
-            "host_cpu_count": os.cpu_count(), "cpu_model": _cpu_model(),
+            "cpu_share": {"affinity_cpus": aff, "cgroup_quota_cpus": quota, "threads_used": torch.get_num_threads(),
+                          "host_cpu_count": os.cpu_count(), "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")},
+            "cpu_model": _cpu_model(),
             "modes": {"kv_cached": round(clips * 30.0 / t_cached, 3),
                       "use_cache_false_reference_config": round(clips * 30.0 / t_nocache, 3)},
-            "sample": f"{clips} clip(s) x 30 s, whisper-{size} fp32 PyTorch-CPU restatement of the reference path "
-                      f"(oracle/whisper_torch.py): log-mel + encoder + {n_tokens} greedy tokens with the "
-                      f"{n_phr}-phrase boost; kv-cached {t_cached:.2f} s, use_cache=False "
-                      f"(scripts/evaluation.py:178) {t_nocache:.2f} s wall; torch threads = the box's CPU share "
-                      f"(OMP_NUM_THREADS), host has {os.cpu_count()} logical CPUs"}
+            "runs_s": {"kv_cached": [round(t, 3) for t in t_c], "use_cache_false": [round(t, 3) for t in t_n]},
+            "sample": f"{clips} clip(s) x 30 s per run, whisper-{size} fp32 PyTorch-CPU restatement of the reference "
+                      f"path (oracle/whisper_torch.py): log-mel + encoder + {n_tokens} greedy tokens with the "
+                      f"{n_phr}-phrase boost; {warmups} warm-ups, median of {reps} runs per mode: kv-cached "
+                      f"{t_cached:.2f} s, use_cache=False (scripts/evaluation.py:178) {t_nocache:.2f} s wall; "
+                      f"{torch.get_num_threads()} threads = this job's CPU share (affinity {aff}, cgroup quota "
+                      f"{quota}); not extrapolated to the 32-clip batch"}
 
 
 def _pmc_traffic(kernel: str):
@@ -140,9 +179,15 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=2, help="steps of the serialised roofline pass")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="wcb_set_option on the handle (alternative formulations, for sweeps)")
+    ap.add_argument("--reference-mode", action="store_true",
+                    help="the reference's decode contract: natural EOS, max_length=225, no boost "
+                         "(scripts/evaluation.py:173-179); batches serialised (the host polls EOS)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="serialise batches (default: batch i+1's front end + encoder overlap batch i's decode)")
     args = ap.parse_args()
+    if args.reference_mode:
+        args.new_tokens, args.boost, args.no_overlap, args.no_cpu_baseline = 225, 0.0, True, True
+    min_new = 0 if args.reference_mode else args.new_tokens   # benchmark mode: EOS masked, fixed length
 
     import torch
     import torch.distributed as dist
@@ -195,7 +240,7 @@ def main():
 
     def step():
         mel = model.log_mel(pcm)
-        ids = model.generate(mel, max_length=args.new_tokens, min_new_tokens=args.new_tokens,
+        ids = model.generate(mel, max_length=args.new_tokens, min_new_tokens=min_new,
                              bias_list=phrases, bias_boost=args.boost, use_graph=use_graph, block=not overlap,
                              num_beams=args.num_beams)
         keep.append((mel, ids))
@@ -206,14 +251,17 @@ def main():
         model.synchronize()
         torch.cuda.synchronize()
         log(f"warmup {i} done, ids {tuple(ids.shape)}")
-    assert ids.shape[0] == B and (args.num_beams > 1 or ids.shape == (B, args.new_tokens))
+    assert ids.shape[0] == B and (args.num_beams > 1 or min_new == 0 or ids.shape == (B, args.new_tokens))
     keep.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    gen_tokens = 0
     for i in range(args.steps):
-        step()
+        ids = step()
+        if not overlap:
+            gen_tokens += int((ids != dims.pad_token_id).sum()) + int(ids.shape[0])   # + the final EOS of each row
     model.synchronize()
     torch.cuda.synchronize()
     if world > 1:
@@ -233,7 +281,7 @@ def main():
         model.profile_enable(True, events=True, stamps=False)
         for i in range(prof_steps):
             mel = model.log_mel(pcm)
-            model.generate(mel, max_length=args.new_tokens, min_new_tokens=args.new_tokens, bias_list=phrases,
+            model.generate(mel, max_length=args.new_tokens, min_new_tokens=min_new, bias_list=phrases,
                            bias_boost=args.boost, use_graph=False, block=True, num_beams=args.num_beams)
         model.synchronize()
         torch.cuda.synchronize()
@@ -311,7 +359,7 @@ def main():
         from whisper_context_biasing_amd import _lib
         from whisper_context_biasing_amd.metrics import _cstrs
         mel = model.log_mel(pcm)
-        kw = dict(max_length=args.new_tokens, min_new_tokens=args.new_tokens, use_graph=use_graph,
+        kw = dict(max_length=args.new_tokens, min_new_tokens=min_new, use_graph=use_graph,
                   num_beams=args.num_beams)
         boosted = model.generate(mel, bias_list=phrases, bias_boost=args.boost, **kw).cpu().tolist()
         plain = model.generate(mel, **kw).cpu().tolist()
@@ -357,10 +405,14 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (seeded 30 s/16 kHz clips, random-init weights of the named architecture)",
-            "config": {"workload": f"{_config_tag(args, world)}: whisper-{args.model}, {B} clips/GPU x 30 s, log-mel + "
-                                   f"encoder + {args.new_tokens}-token "
-                                   f"{'greedy' if args.num_beams == 1 else f'beam-{args.num_beams}'} decode, "
-                                   f"{args.bias_phrases}-phrase bias boost lambda={args.boost}",
+            "config": {"workload": (f"{_config_tag(args, world)}: whisper-{args.model}, {B} clips/GPU x 30 s, log-mel + "
+                                    f"encoder + {args.new_tokens}-token "
+                                    f"{'greedy' if args.num_beams == 1 else f'beam-{args.num_beams}'} decode, "
+                                    f"{args.bias_phrases}-phrase bias boost lambda={args.boost}")
+                                   if not args.reference_mode else
+                                   (f"reference mode: whisper-{args.model}, {B} clips/GPU x 30 s, log-mel + encoder + "
+                                    f"greedy decode to natural EOS, max_length=225, no boost "
+                                    f"(scripts/evaluation.py:173-179); batches serialised"),
                        "num_beams": args.num_beams, "global_batch": world * B, "parallelism": f"utterance-dp{world}",
                        "hipgraph_decode": use_graph, "batches_in_flight": 3 if overlap else 1},
             "rtf": round(1.0 / (value / world), 6),
@@ -372,6 +424,9 @@ def main():
         }
         if cpu:
             out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        if args.reference_mode:
+            out["reference_mode"] = {"generated_tokens_per_clip": round(gen_tokens / (args.steps * B), 2),
+                                     "ms_per_generated_token": round(ms_per_step / max(gen_tokens / args.steps / B, 1e-9), 4)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

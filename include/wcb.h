@@ -67,8 +67,7 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "merge_v" 0/1      greedy encoder-space cross-attention: range merge and W_v fused (1) or two launches
  *   "ring_kt" 1/2      decode rows > 64: 64-deep K sub-tiles per LDS-ring stage of the projection tiles
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)
- *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave, 2 LDS stages), 4 (64 queries),
- *                      23 / 24 (32 queries, 3 / 4 LDS stages) */
+ *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave), 4 (64 queries, default) */
 int wcb_set_option(wcb_handle* h, const char* name, int value);
 
 /* replaces from_pretrained / load_state_dict: one HF state-dict tensor (host f32, C order), staged
@@ -170,7 +169,7 @@ int wcb_op_layernorm(int dtype, const float* x, const float* w, const float* b, 
                      void* stream);
 /* o[B][Sq][H*64] = softmax(q kᵀ) v per head (q pre-scaled), k/v [B][Sk][H*64];
  * flash=1 selects the MFMA kernel (16-bit dtypes; Sq <= 16: the few-query form of beam search), 100 the
- * MFMA kernel with 64 queries per wave, 123 / 124 with 3 / 4 LDS stages, -n (Sq <= 16) the MFMA kernel over n key ranges merged in
+ * MFMA kernel with 64 queries per wave, -n (Sq <= 16) the MFMA kernel over n key ranges merged in
  * fixed order; 0 the decode kernel; n >= 2 the decode kernel with n split-KV key chunks combined by the
  * last-arriving chunk. */
 int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H, int Sq,

@@ -1,7 +1,9 @@
 """GPU, world_size 2: utterance sharding end to end on the device. Two processes
 (gloo group; both ranks drive cuda:0 here — the one-GPU box) get the weights by one broadcast of the
 packed bf16 blob, decode their shard of the batch through libwcb with the bias boost, and gather the
-ids; the concatenation in rank order equals the single-process decode of the whole batch."""
+ids; the concatenation in rank order equals the single-process decode of the whole batch. Cases:
+tiny.en (6 clips, plumbing) and C4's model, whisper-small bf16, 2 ranks x 16 clips with the
+1000-phrase boost (scripts/evaluation.py:173-206 decode contract on each shard)."""
 import os
 import socket
 
@@ -13,7 +15,7 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-N_CLIPS, TOKENS, MODEL = 6, 16, "tiny.en"
+CASES = {"tiny.en": (6, 16, 200), "small": (32, 16, 1000)}   # model: clips, tokens, bias phrases
 
 
 def _free_port():
@@ -22,16 +24,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _decode(model, lo, hi, dims):
+def _decode(model, lo, hi, dims, tokens, n_phr):
     from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list
     pcm = torch.from_numpy(synth_batch(hi - lo, start=lo)).cuda()
     mel = model.log_mel(pcm)
-    phrases = synth_bias_list(200, eot=dims.eos_token_id)
-    ids = model.generate(mel, max_length=TOKENS, min_new_tokens=TOKENS, bias_list=phrases, bias_boost=2.0)
+    phrases = synth_bias_list(n_phr, eot=dims.eos_token_id)
+    ids = model.generate(mel, max_length=tokens, min_new_tokens=tokens, bias_list=phrases, bias_boost=2.0)
     return ids.cpu()
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, name):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -39,26 +41,29 @@ def _worker(rank, world, port, outdir):
     from whisper_context_biasing_amd.model import WhisperCB
     from whisper_context_biasing_amd.shard import broadcast_weights, gather_shards, shard_bounds
     torch.cuda.set_device(0)
-    dims = get_dims(MODEL)
+    n_clips, tokens, n_phr = CASES[name]
+    dims = get_dims(name)
     sd = broadcast_weights(dims, torch.device("cpu"), seed=0)
     model = WhisperCB.from_state_dict(dims, sd, dtype="bf16")
-    lo, hi = shard_bounds(N_CLIPS, rank, world)
-    ids = _decode(model, lo, hi, dims)
-    rows = torch.cat(gather_shards(ids, torch.device("cpu")))
+    lo, hi = shard_bounds(n_clips, rank, world)
+    ids = _decode(model, lo, hi, dims, tokens, n_phr)
+    rows = torch.cat(gather_shards(ids, torch.device("cpu"), pad_value=dims.pad_token_id))
     if rank == 0:
         np.save(os.path.join(outdir, "sharded.npy"), rows.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_shards_equal_single_process(tmp_path):
+@pytest.mark.parametrize("name", ["tiny.en", "small"])
+def test_two_rank_shards_equal_single_process(tmp_path, name):
     from whisper_context_biasing_amd.config import get_dims
     from whisper_context_biasing_amd.model import WhisperCB
     from whisper_context_biasing_amd.shard import broadcast_weights
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), name), nprocs=2, join=True)
     sharded = np.load(tmp_path / "sharded.npy")
-    dims = get_dims(MODEL)
+    n_clips, tokens, n_phr = CASES[name]
+    dims = get_dims(name)
     model = WhisperCB.from_state_dict(dims, broadcast_weights(dims, torch.device("cpu"), seed=0), dtype="bf16")
-    full = _decode(model, 0, N_CLIPS, dims).numpy()
-    assert sharded.shape == full.shape == (N_CLIPS, TOKENS)
+    full = _decode(model, 0, n_clips, dims, tokens, n_phr).numpy()
+    assert sharded.shape == full.shape == (n_clips, tokens)
     np.testing.assert_array_equal(sharded, full)

@@ -34,11 +34,12 @@ def _worker(rank, world, port, outdir):
     pcm = synth_batch(hi - lo, start=lo, n_samples=1600)
     t = max_over_ranks(0.25 * (rank + 1), dev)
     ids = torch.arange(lo, hi, dtype=torch.int64)[:, None] * 10 + torch.arange(4)
-    rows = torch.cat(gather_shards(ids, dev))
+    rows = torch.cat(gather_shards(ids, dev, pad_value=50257))
+    flat = torch.cat(gather_shards(ids[:, 0], dev, pad_value=50257))   # 1-D locals stay 1-D
     # natural-EOS decoding trims each shard to its own longest row: unequal widths (and row counts)
     wide = torch.arange(lo, hi, dtype=torch.int64)[:, None] * 10 + torch.arange(3 + 2 * rank)
     ragged = torch.cat(gather_shards(wide if rank == 0 else wide[:2], dev, pad_value=50257))
-    np.savez(os.path.join(outdir, f"r{rank}.npz"), pcm=pcm, t=t, rows=rows.numpy(), lo=lo, hi=hi, ragged=ragged.numpy(),
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), pcm=pcm, t=t, rows=rows.numpy(), flat=flat.numpy(), lo=lo, hi=hi, ragged=ragged.numpy(),
              **{f"w_{k.replace('.', '_')}": v for k, v in sd.items() if "layers.0" in k or "embed" in k})
     dist.barrier()
     dist.destroy_process_group()
@@ -77,6 +78,8 @@ def test_two_rank_gloo(tmp_path):
     # every rank gathered all rows in rank order
     for x in r:
         np.testing.assert_array_equal(x["rows"][:, 0], np.arange(6) * 10)
+        assert x["flat"].shape == (6,)
+        np.testing.assert_array_equal(x["flat"], np.arange(6) * 10)
         # ragged shards: rank 0 sent 3 rows x 3 columns, rank 1 2 rows x 5 columns; every rank holds
         # 5 rows at width 5, rank 0's rows right-padded with the pad id
         rg = x["ragged"]

@@ -387,10 +387,13 @@ __global__ __launch_bounds__(64) void attn_self_kernel(AttnArgs a) {
     for (int e = 0; e < 8; ++e) o[e] *= r;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const float p = (j0 + u * 8 + kg < nk) ? __expf(sc[u] - mn) : 0.f;
+      // keys past the count were loaded speculatively (rows left by an earlier call, possibly
+      // non-finite): they contribute nothing, not even 0·v
+      const bool live = j0 + u * 8 + kg < nk;
+      const float p = live ? __expf(sc[u] - mn) : 0.f;
       if (seg == 0) l += p;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = fmaf(p, vv[u][e], o[e]);
+      for (int e = 0; e < 8; ++e) o[e] = live ? fmaf(p, vv[u][e], o[e]) : o[e];
     }
     m = mn;
   }
@@ -661,12 +664,9 @@ static void launch_flash(const AttnArgs& a, hipStream_t s) {
     const bool xg = nqb > 1 && BH % 8 == 0;
     b.xcd_nqb = xg ? nqb : 0;
     const dim3 grid = xg ? dim3(nqb * BH) : dim3(nqb, BH);
-    switch (a.variant) {   // encoder tilings (option enc_flash): query fragments per wave, LDS stages
-      case 4: WCB_LAUNCH((attn_flash_kernel<T, 4, 2>), grid, dim3(256), 0, s, b); break;   // 64 queries / wave
-      case 23: WCB_LAUNCH((attn_flash_kernel<T, 2, 3>), grid, dim3(256), 0, s, b); break;  // 2 tiles in flight
-      case 24: WCB_LAUNCH((attn_flash_kernel<T, 2, 4>), grid, dim3(256), 0, s, b); break;  // 3 tiles in flight
-      default: WCB_LAUNCH((attn_flash_kernel<T, 2, 2>), grid, dim3(256), 0, s, b); break;
-    }
+    // encoder tilings (option enc_flash): 64 queries per wave (4, default) or 32 (2)
+    if (a.variant == 4) WCB_LAUNCH((attn_flash_kernel<T, 4, 2>), grid, dim3(256), 0, s, b);
+    else WCB_LAUNCH((attn_flash_kernel<T, 2, 2>), grid, dim3(256), 0, s, b);
   }
 }
 

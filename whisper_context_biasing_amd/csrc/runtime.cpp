@@ -23,6 +23,7 @@
 #include <vector>
 #include <cstdlib>
 #include <deque>
+#include <atomic>
 
 #include "../../include/wcb.h"
 #include "kernels.h"
@@ -170,9 +171,9 @@ struct wcb_handle {
   // decode rows > 64: 64-deep K sub-tiles per ring stage of the 64x32 / 32x32 tiles (option "ring_kt",
   // 1 or 2; C5 1,594 -> 1,644 audio-s/s)
   int ring_kt = 2;
-  // encoder flash attention tiling (option "enc_flash"): 2 = 32 queries per wave, 2 LDS stages;
-  // 4 = 64 queries per wave; 23 / 24 = 32 queries, 3 / 4 stages. Measured (tools/microbench.py,
-  // small / medium encoder shapes, µs): 2: 358 / 878, 4: 313 / 808, 23: 328 / 887, 24: 399 / 1041
+  // encoder flash attention tiling (option "enc_flash"): 2 = 32 queries per wave, 4 = 64 queries per
+  // wave. Measured (tools/microbench.py, small / medium encoder shapes, µs): 2: 358 / 878, 4: 313 / 808
+  // (3 / 4 LDS stages at 32 queries measured 328 / 887 and 399 / 1041: removed)
   int enc_flash_qw = 4;
   // Cross-attention formulation: 1 = encoder space (k_xenc.hip: the step streams the encoder output,
   // no cross-K/V precompute; 16-bit dtypes, d <= 1024), 0 = precomputed per-layer K/V (f32 "exact"
@@ -220,7 +221,6 @@ struct wcb_handle {
   // default (empty) bias automaton
   std::unique_ptr<wcb_bias> empty_bias;
   std::vector<wcb_bias*> biases;     // live automatons created on this handle (lifetime, wcb.h)
-  uint64_t next_bias_id = 1;
   // profiling
   bool prof = false, prof_stamps = false;
   std::vector<ProfEntry> prof_e;
@@ -325,6 +325,7 @@ struct wcb_handle {
 namespace {
 
 thread_local std::string g_err;
+std::atomic<uint64_t> g_next_bias_id{1};
 
 template <typename F>
 int guarded(wcb_handle* h, F&& f) {
@@ -523,7 +524,7 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       REQUIRE(value >= 0 && value <= 3, "option xenc_variant: 0..3");
       h->xenc_variant = value;
     } else if (n == "enc_flash") {
-      REQUIRE(value == 2 || value == 4 || value == 23 || value == 24, "option enc_flash: 2, 4, 23 or 24");
+      REQUIRE(value == 2 || value == 4, "option enc_flash: 2 or 4");
       h->enc_flash_qw = value;
     } else if (n == "xenc_split") {
       REQUIRE(!h->ready, "option xenc_split: set before the weights are finalized");
@@ -1257,6 +1258,8 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     const int T = P + cfg->max_new_tokens;
     REQUIRE(T <= h->d.n_text_ctx + 1, "prefix + max_new_tokens exceeds max_target_positions");
     const wcb_bias* bs = bias ? bias : h->empty_bias.get();
+    REQUIRE(bs == h->empty_bias.get() || bs->owner == h,
+            "bias automaton was created on another handle (wcb_bias_create binds it to its handle)");
     REQUIRE(bs->vocab == h->d.vocab, "bias automaton built for another vocabulary");
     const bool fixed_len = cfg->min_new_tokens >= cfg->max_new_tokens;   // EOS masked: no host polling
     const int out_ld = cfg->max_new_tokens;
@@ -1348,8 +1351,9 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     if (use_graph && (!D.gexec || D.gkey != key)) {
       if (D.gexec) { (void)hipGraphExecDestroy(D.gexec); D.gexec = nullptr; }
       if (D.gexec_k) { (void)hipGraphExecDestroy(D.gexec_k); D.gexec_k = nullptr; }
-      for (int k : {1, chunk}) {
-        if (k == 1 ? false : chunk == 1) break;
+      const int ks[2] = {1, chunk};
+      for (int ki = 0; ki < (chunk > 1 ? 2 : 1); ++ki) {   // the k-step graph only when it differs
+        const int k = ks[ki];
         hipGraph_t graph;
         HIPCHK(hipStreamBeginCapture(D.hs, hipStreamCaptureModeThreadLocal));
         for (int i = 0; i < k; ++i) decode_step(h, sc);
@@ -1546,7 +1550,7 @@ int wcb_bias_create(wcb_handle* h, const int32_t* tokens, const int32_t* offsets
     auto b = std::make_unique<wcb_bias>();
     b->n_states = ns;
     b->vocab = V;
-    b->id = h->next_bias_id++;
+    b->id = g_next_bias_id.fetch_add(1);   // process-wide: a graph key never names another handle's bias
     b->owner = h;
     HIPCHK(hipSetDevice(h->device));
     b->root_bits.ensure(bits.size() * 4);
@@ -1799,9 +1803,9 @@ int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, voi
     a.q = q; a.ldq = ld; a.q_Sb = Sq; a.Sq = Sq;
     a.k = k; a.v = v; a.k_sb = (long)Sk * ld; a.k_sh = 64; a.k_sk = ld;
     a.o = o; a.ldo = ld; a.o_Sb = Sq; a.B = B; a.H = H; a.nkeys = Sk;
-    if (flash == 1 || flash == 100 || flash == 123 || flash == 124 || flash < 0) {
-      // 100: 64 queries per wave; 123 / 124: 3 / 4 LDS stages; -n: n key ranges + merge (Sq <= 16)
-      a.variant = flash == 100 ? 4 : flash == 123 ? 23 : flash == 124 ? 24 : 1;
+    if (flash == 1 || flash == 100 || flash < 0) {
+      // 100: 64 queries per wave; -n: n key ranges + merge (Sq <= 16)
+      a.variant = flash == 100 ? 4 : 1;
       REQUIRE(dtype != WCB_F32, "flash attention needs a 16-bit dtype");
       static DevBuf fpart;
       if (flash < 0) {

@@ -117,6 +117,11 @@ class WhisperCB:
         # accumulate one V-sized automaton per distinct batch)
         self._bias_cache: "OrderedDict[tuple, BiasList]" = OrderedDict()
         self.bias_cache_size = 8
+        # automatons evicted from the LRU: destroying one waits for this handle's queued work
+        # (wcb_bias_destroy drops the decode graphs that captured it), so they are kept until the next
+        # synchronize() — where the streams are idle and the wait is free — instead of stalling an
+        # asynchronous (block=False) generate call. Past kRetiredMax they are released anyway (one stall).
+        self._bias_retired: List[BiasList] = []
         self._word_start: Optional[np.ndarray] = None
         self._loaded = False
 
@@ -243,7 +248,9 @@ class WhisperCB:
             b = BiasList(self, phrases)
             self._bias_cache[key] = b
             while len(self._bias_cache) > self.bias_cache_size:
-                self._bias_cache.popitem(last=False)   # wcb_bias_destroy drops graphs that captured it
+                self._bias_retired.append(self._bias_cache.popitem(last=False)[1])
+            if len(self._bias_retired) > self.kRetiredMax:
+                self.synchronize()
         else:
             self._bias_cache.move_to_end(key)
         return b
@@ -370,9 +377,13 @@ class WhisperCB:
                 out[i, n:] = pad
         return out
 
+    kRetiredMax = 32
+
     def synchronize(self):
-        """Wait for every queued front-end / encoder / decode operation of this model."""
+        """Wait for every queued front-end / encoder / decode operation of this model (and release the
+        bias automatons evicted since the last call, now that no queued work reads them)."""
         _lib.check(self._lib.wcb_synchronize(self._h), self._h, "wcb_synchronize")
+        self._bias_retired.clear()
 
     # ------------------------------------------------------------------------------- forward
     def forward(self, input_features=None, decoder_input_ids=None, labels=None, bias_spans=None,

@@ -84,17 +84,19 @@ def max_over_ranks(value: float, device: torch.device) -> float:
     return float(t.item())
 
 
-def gather_shards(local: torch.Tensor, device: torch.device, pad_value: int = 0) -> List[torch.Tensor]:
+def gather_shards(local: torch.Tensor, device: torch.device, pad_value: int) -> List[torch.Tensor]:
     """Collect every rank's result rows (evaluation-time convenience; not on the timed path).
 
     Ranks may return different numbers of rows and — with natural-EOS decoding, where generate()
     trims each shard to its own longest row — different widths: both are all-gathered first, every
-    shard is padded (rows with zeros, columns with `pad_value`, the tokenizer's pad id) to the global
-    maximum for the collective, and each rank's rows come back at the common width."""
+    shard is padded (rows with zeros, columns with `pad_value` — the caller passes the model's pad
+    id, WhisperDims.pad_token_id) to the global maximum for the collective, and each rank's rows come
+    back at the common width. 1-D locals (one value per row) come back 1-D."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return [local]
     world = dist.get_world_size()
-    local = local.reshape(local.shape[0], -1) if local.dim() == 1 else local
+    one_d = local.dim() == 1
+    local = local.reshape(local.shape[0], -1) if one_d else local
     shp = torch.tensor([local.shape[0], local.shape[1] if local.dim() > 1 else 1], dtype=torch.int64, device=device)
     shps = [torch.zeros_like(shp) for _ in range(world)]
     dist.all_gather(shps, shp)
@@ -105,4 +107,5 @@ def gather_shards(local: torch.Tensor, device: torch.device, pad_value: int = 0)
     buf[:local.shape[0], :local.shape[1]] = local.to(device)
     bufs = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(bufs, buf)
-    return [b[:int(k[0].item())] for b, k in zip(bufs, shps)]
+    out = [b[:int(k[0].item())] for b, k in zip(bufs, shps)]
+    return [o[:, 0] for o in out] if one_d else out

@@ -84,10 +84,13 @@ def synth_bias_list(n: int, eot: int, seed: int = 7) -> List[List[int]]:
     return [phrase_token_ids(p, eot) for p in sample_bias_phrases(n, seed)]
 
 
-def runner_up_phrases(model, mel, n_tokens: int, lam: float, word_start=None):
+def runner_up_phrases(model, mel, n_tokens: int, lam: float, word_start=None, band=(0.25, 0.75)):
     """Bias phrases the boost can actually place (the bench's biased-WER workload): for every clip, the
-    step of the lam = 0 greedy decode whose top-1/top-2 logit gap is smallest among those below `lam`
-    (first step excluded) whose runner-up token r may start a match (`word_start`), and the phrase
+    EARLIEST step (first step excluded) of the lam = 0 greedy decode whose top-1/top-2 logit gap lies
+    in the band [band[0]·lam, band[1]·lam) — below lam, so one boost unit lifts the runner-up r over
+    the top-1; well above the 16-bit noise between the prefill and decode paths, so r is not the decode
+    path's own choice at lam = 0 — whose runner-up may start a match (`word_start`), and where the
+    teacher-forced top-1 is the decode's own token (the two paths agree on the step). The phrase is
     [r, n] with n the greedy token after r (the decode teacher-forced through r). Returns
     (plain_ids [B, n_tokens] int64, phrases, targets) with targets[i] = (clip, step) of phrase i.
     Runs on the GPU through the model's own generate / forward; untimed setup."""
@@ -101,12 +104,13 @@ def runner_up_phrases(model, mel, n_tokens: int, lam: float, word_start=None):
     top2, idx2 = logits.topk(2, dim=-1)                                   # [B, T, 2]
     gap = (top2[..., 0] - top2[..., 1]).float()
     ru = idx2[..., 1]
-    ok = (gap < lam) & (ru != dims.eos_token_id)
+    ok = (gap >= band[0] * lam) & (gap < band[1] * lam) & (ru != dims.eos_token_id) & (idx2[..., 0] == plain)
     ok[:, 0] = False
     if word_start is not None:
         ok &= torch.as_tensor(np.asarray(word_start, dtype=bool), device=ru.device)[ru]
-    gap = torch.where(ok, gap, torch.full_like(gap, float("inf")))
-    t = gap.argmin(dim=1)
+    T = gap.shape[1]
+    steps = torch.arange(T, device=gap.device)[None, :].expand(B, T)
+    t = torch.where(ok, steps, torch.full_like(steps, T)).min(dim=1).values.clamp(max=T - 1)   # earliest
     keep = ok.gather(1, t[:, None])[:, 0]
     r = ru.gather(1, t[:, None])[:, 0]
     forced = torch.cat([sot, plain], 1).clone()                          # [SOT, ids[:t], r, ...]
