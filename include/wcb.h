@@ -65,6 +65,9 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "flash_split" n    key ranges per (clip, head) of the beam-search cross-attention (flash kernel), 1..8
  *   "ln_fold" 0/1      decode rows > 64 (16-bit): LayerNorm folded into the projection, or its own launch
  *   "merge_v" 0/1      greedy encoder-space cross-attention: range merge and W_v fused (1) or two launches
+ *   "xqk" 0/1          greedy encoder-space cross-attention query: LN + q_proj + W_k,hᵀ in one launch (1) or
+ *                      two decode GEMMs (0); bit-identical
+ *   "decode_contexts" n  decode contexts in flight (1..4): calls decode on n streams from n buffers
  *   "ring_kt" 1/2      decode rows > 64: 64-deep K sub-tiles per LDS-ring stage of the projection tiles
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)
  *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave), 4 (64 queries, default) */

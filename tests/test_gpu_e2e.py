@@ -241,3 +241,63 @@ def test_broadcast_blob_views_load_without_host_copy():
     x = torch.from_numpy(W.log_mel(synth_batch(2), dims.n_mel))
     assert np.array_equal(m1.generate(x, max_length=10, min_new_tokens=10).cpu().numpy(),
                           m2.generate(x, max_length=10, min_new_tokens=10).cpu().numpy())
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_fused_cross_query_is_bit_identical(dtype):
+    """Option xqk (default 1): LN + q_proj + W_k,hᵀ as one launch (k_xenc.hip xq_kq_kernel) against the
+    two decode GEMMs it replaces (xqk 0): identical arithmetic, so identical ids even on the diverse
+    recipe, whose near-ties (gaps ~1e-3) flip on any rounding difference. 32 rows (one 32-row block)
+    and 13 rows (16-row blocks), 1000-phrase boost."""
+    dims = get_dims("small")
+    sd = make_weights(dims, seed=0, recipe="diverse")
+    fused = WhisperCB.from_state_dict(dims, sd, dtype=dtype)
+    plain = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options={"xqk": 0})
+    phrases = synth_bias_list(1000, eot=dims.eos_token_id)
+    for B in (32, 13):
+        x = torch.from_numpy(W.log_mel(synth_batch(B, start=3), dims.n_mel))
+        kw = dict(max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0)
+        a = fused.generate(x, **kw).cpu().numpy()
+        b = plain.generate(x, **kw).cpu().numpy()
+        np.testing.assert_array_equal(a, b)
+
+
+def test_bias_from_another_handle_is_rejected():
+    """A bias automaton belongs to the handle that built it (its decode graphs are keyed on it): passing
+    it to another handle is an argument error, not a silently wrong boost."""
+    from whisper_context_biasing_amd import _lib
+    dims = get_dims("micro")
+    sd = make_weights(dims, seed=0, recipe="margin")
+    m1 = WhisperCB.from_state_dict(dims, sd, dtype="f32")
+    m2 = WhisperCB.from_state_dict(dims, sd, dtype="f32")
+    phrases = synth_bias_list(20, eot=dims.eos_token_id)
+    b1 = m1.bias_list(phrases)
+    x = torch.from_numpy(W.log_mel(synth_batch(2), dims.n_mel))
+    m1.generate(x, max_length=4, bias_list=phrases, bias_boost=2.0)
+    with pytest.raises(_lib.WcbError, match="another handle"):
+        m2.generate(x, max_length=4, bias_list=b1, bias_boost=2.0)
+    # its own handle takes the prebuilt automaton
+    assert m1.generate(x, max_length=4, bias_list=b1, bias_boost=2.0).shape[0] == 2
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_folded_layernorm_beam_rows_match_layernorm_launch(dtype):
+    """Decode rows > 64 (beam search: 16 clips x 5 beams = 80 rows): the ring-tile projections with the
+    pre-block LayerNorm folded in (option ln_fold 1, default: W·diag(γ) weights, row statistics from the
+    residual writers' 32-column partials, r·(acc − μ·u) + c in the epilogue) against a LayerNorm launch
+    before each projection (ln_fold 0): the same beams on the high-margin recipe, and both equal to the
+    numpy oracle's beam search on the first clip."""
+    from oracle.beam_np import generate_beam
+    dims = get_dims("small")
+    sd = make_weights(dims, seed=1, recipe="margin")
+    fold = WhisperCB.from_state_dict(dims, sd, dtype=dtype)
+    launch = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options={"ln_fold": 0})
+    phrases = synth_bias_list(1000, eot=dims.eos_token_id)
+    x = torch.from_numpy(W.log_mel(synth_batch(16), dims.n_mel))
+    kw = dict(max_length=10, num_beams=5, bias_list=phrases, bias_boost=2.0)
+    a = fold.generate(x, **kw).cpu().numpy()
+    b = launch.generate(x, **kw).cpu().numpy()
+    np.testing.assert_array_equal(a, b)
+    om = W.OracleModel.from_dims(dims, sd)
+    ref = generate_beam(om, mel=x[:1].numpy(), num_beams=5, max_length=10, bias=phrases, bias_boost=2.0)
+    np.testing.assert_array_equal(a[:1, :ref.shape[1]], ref)

@@ -270,16 +270,17 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(GemmArgs g) {
 // barrier), the raw s_barrier makes every wave's tile-k bytes visible and tells the issuers that the
 // stage of tile k-1 is free, then tile k+NS-1 is issued into it. No plain global loads inside the
 // loop (hipcc would drain the DMA ring at their use); __syncthreads only after it.
-// LNF (decode rows > 64): the consumer's pre-block LayerNorm folded in (GemmArgs::ln_u): A = the
-// 16-bit residual rows; each A fragment is scaled by γ (staged in LDS) after its LDS read while the
-// row's Σx, Σx² accumulate from the same values; the epilogue applies r·(acc − μ·u[n]) + c[n].
-constexpr int kLnfMaxK = 1280;
+// LNF (decode rows > 64, 16-bit): the consumer's pre-block LayerNorm folded into the weights and the
+// epilogue, no per-element work in the K loop. LN(x)·Wᵀ + b = r·(Σ_k x_k W'[n][k] − μ·u[n]) + c[n] with
+// W' = W·diag(γ) (rounded to T at finalize, GemmArgs::W), u[n] = Σ_k W'[n][k], c[n] = Σ_k β_k W[n][k] +
+// b[n] (GemmArgs::bias); A = the 16-bit copy of the residual rows. The row statistics (μ, r) come from
+// the per-32-column partial sums (Σx, Σx²) the residual writer published (GemmArgs::rst_in, fixed-order
+// sums: deterministic); they are fetched into LDS by the same LDS-DMA as the first ring stage.
 // KT: 64-deep sub-tiles per ring stage (2 for the small decode-row tiles: half the K-loop
 // iterations, and with them half the barriers, of a loop that is latency-bound at 2-8 MFMAs per wave
 // per sub-tile).
 template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
-  static_assert(!LNF || KT == 1, "the folded LayerNorm indexes gamma by 64-deep K tiles");
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BK = 64, CE = 8;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
@@ -328,15 +329,19 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  float* lng = reinterpret_cast<float*>(smem + NS * STAGE);   // LNF: γ [K], then (μ, r) per tile row
-  float* lnst = lng + kLnfMaxK;
-  float s1[FM], s2[FM];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) { s1[i] = 0.f; s2[i] = 0.f; }
+  // LNF: the tile rows' statistics partials [BM][rst_nb] float2 (LDS-DMA, older than ring stage 0:
+  // the first stage wait retires them), then (μ, r) per tile row
+  constexpr int LNF_OFF = NS * STAGE > BM * (BN + 4) * 4 ? NS * STAGE : BM * (BN + 4) * 4;
+  float* lnraw = reinterpret_cast<float*>(smem + LNF_OFF);
+  float* lnst = lnraw + BM * (kLnfMaxK / 32) * 2;
   if constexpr (LNF) {
-    for (int k = tid * 4; k < g.K; k += NT * 4)
-      *reinterpret_cast<f32x4*>(lng + k) = *reinterpret_cast<const f32x4*>(g.ln_w + k);
-    __syncthreads();
+    const int per_row = g.rst_nb * 8 / 16;                  // 16-byte chunks per row (rst_nb float2)
+    const int chunks = BM * per_row;
+    for (int q0 = wave * 64; q0 < chunks; q0 += NT) {
+      const int q = min(q0 + lane, chunks - 1), r = q / per_row, j = q % per_row;
+      const int m = min(m0 + r, g.M - 1);
+      glds16(g.rst_in + ((long)m * g.rst_nb) * 2 + j * 4, reinterpret_cast<char*>(lnraw) + (long)q0 * 16);
+    }
   }
 
   const int nk = g.K / (BK * KT);
@@ -383,23 +388,6 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
         const int r = wn * TN + j * 16 + (lane & 15);
         b[j] = *reinterpret_cast<const Frag*>(base + BM * 128 + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
       }
-      if constexpr (LNF) {   // elements k = kt·64 + 8c + e of this lane's rows: row sums, then x·γ
-        const f32x4 g0 = *reinterpret_cast<const f32x4*>(lng + kt * BK + c * 8);
-        const f32x4 g1 = *reinterpret_cast<const f32x4*>(lng + kt * BK + c * 8 + 4);
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            float x;
-            if constexpr (__is_same(T, bf16_t)) x = bf16_to_f((bf16_t)a[i][e]);
-            else x = float(a[i][e]);
-            s1[i] += x;
-            s2[i] = fmaf(x, x, s2[i]);
-            const float y = x * (e < 4 ? g0[e] : g1[e - 4]);
-            if constexpr (__is_same(T, bf16_t)) a[i][e] = (short)f_to_bf16(y);
-            else a[i][e] = f16_t(y);
-          }
-      }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -407,18 +395,17 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
     }
     st = st + 1 == NS ? 0 : st + 1;
   }
-  if constexpr (LNF) {   // row statistics: the 4 lane groups hold disjoint k; one wave column publishes
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      float a1 = s1[i], a2 = s2[i];
-      a1 += __shfl_xor(a1, 16, 64); a2 += __shfl_xor(a2, 16, 64);
-      a1 += __shfl_xor(a1, 32, 64); a2 += __shfl_xor(a2, 32, 64);
-      if (wn == 0 && lane < 16) {
-        const int row = wm * TM + i * 16 + lane;
-        const float mean = a1 / g.K;
-        lnst[2 * row] = mean;
-        lnst[2 * row + 1] = rsqrtf(fmaxf(a2 / g.K - mean * mean, 0.f) + 1e-5f);
+  if constexpr (LNF) {   // (μ, r) per tile row from the producer's partials, summed in column order
+    for (int r = tid; r < BM; r += NT) {
+      float a1 = 0.f, a2 = 0.f;
+      for (int j = 0; j < g.rst_nb; ++j) {
+        const float2 t = *reinterpret_cast<const float2*>(lnraw + ((long)r * g.rst_nb + j) * 2);
+        a1 += t.x;
+        a2 += t.y;
       }
+      const float mean = a1 / g.K;
+      lnst[2 * r] = mean;
+      lnst[2 * r + 1] = rsqrtf(fmaxf(a2 / g.K - mean * mean, 0.f) + 1e-5f);
     }
   }
   __syncthreads();   // every wave is done with the ring: the epilogue reuses its LDS
@@ -455,13 +442,21 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
       const int row = idx / C8, c8 = idx % C8;
       const int m = m0 + ps * PR + row;
       const int n = n0 + c8 * 8;
-      if (m >= g.M || n >= g.N) continue;
+      const bool ok = m < g.M && n < g.N;
       float v[8];
       const f32x4 lo = *reinterpret_cast<const f32x4*>(ct + row * LDC + c8 * 8);
       const f32x4 hi = *reinterpret_cast<const f32x4*>(ct + row * LDC + c8 * 8 + 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) { v[e] = lo[e]; v[e + 4] = hi[e]; }
-      epi_store8<T, EPI>(g, m, n, v);
+      if (ok) epi_store8<T, EPI>(g, m, n, v);
+      if (EPI == E_RUNTIME && g.rst_out) {   // residual writer: (Σx, Σx²) of the new row per 32 columns
+        float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { a1 += v[e]; a2 = fmaf(v[e], v[e], a2); }
+        a1 += __shfl_xor(a1, 1, 64); a2 += __shfl_xor(a2, 1, 64);   // the 4 lanes of a 32-column block
+        a1 += __shfl_xor(a1, 2, 64); a2 += __shfl_xor(a2, 2, 64);
+        if (ok && (c8 & 3) == 0) *reinterpret_cast<float2*>(g.rst_out + ((long)m * (g.N / 32) + n / 32) * 2) = float2{a1, a2};
+      }
     }
     if (PASSES > 1) __syncthreads();
   }
@@ -470,10 +465,11 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
 template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1>
 static void launch_ring_e(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
-  constexpr int stage_bytes = NS * (BM + BN) * 128 * KT + (LNF ? (kLnfMaxK + 2 * BM) * 4 : 0);
+  constexpr int ring_bytes = NS * (BM + BN) * 128 * KT;
   constexpr int epi_full = BM * (BN + 4) * 4;
   constexpr int epi_bytes = epi_full <= 160 * 1024 ? epi_full : epi_full / WM;
-  constexpr int lds = stage_bytes > epi_bytes ? stage_bytes : epi_bytes;
+  constexpr int base = ring_bytes > epi_bytes ? ring_bytes : epi_bytes;
+  constexpr int lds = base + (LNF ? BM * (kLnfMaxK / 32) * 2 * 4 + 2 * BM * 4 : 0);
   static_assert(lds <= 160 * 1024, "LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
@@ -1089,7 +1085,7 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
       // that even N = d_model spreads over 80-320 workgroups (C3: 320 rows = 5 row tiles); 64 columns
       // where that still fills the chip, else 32. Run-time epilogue (KV append, 16-bit residual copy).
       if (g.tile == 2 && g.K % 64 == 0 && !g.st_out && g.mode != 1 && !g.addrow &&
-          (!g.ln_u || g.K <= kLnfMaxK)) {
+          (!g.ln_u || (g.K <= kLnfMaxK && g.rst_in && g.rst_nb * 32 == g.K))) {
         const int mt = (g.M + 63) / 64;
         const bool lnf = g.ln_u != nullptr;
         const bool kt2 = g.ring_kt == 2 && g.K % 128 == 0 && !lnf;   // 128-deep stages

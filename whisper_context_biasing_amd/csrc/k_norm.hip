@@ -82,7 +82,7 @@ void layernorm(DType t, const float* x, const float* w, const float* b, void* y,
 template <typename T>
 __global__ __launch_bounds__(256) void embed_kernel(const T* __restrict__ emb, const T* __restrict__ pemb, const int* __restrict__ ids,
                                                     const int* __restrict__ pos, float* __restrict__ x, float* __restrict__ st,
-                                                    int M, int d, T* __restrict__ x16, int V, int rps) {
+                                                    int M, int d, T* __restrict__ x16, int V, int rps, int st_w) {
   const int row = blockIdx.x;
   const int p = *pos + row % rps;
   const int raw = ids[row];
@@ -95,26 +95,34 @@ __global__ __launch_bounds__(256) void embed_kernel(const T* __restrict__ emb, c
       x[(long)row * d + c] = v;
       if (x16) x16[(long)row * d + c] = DT<T>::fromf(v);
     }
-    float s1 = v, s2 = v * v;
+    if (st) {
+      // one partial per group of st_w lanes (= columns), fixed butterfly order
+      float s1 = v, s2 = v * v;
+      if (st_w == 32) {
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
-    if (st && c < d && (c & 15) == 0) {
-      st[((long)row * (d / 16) + c / 16) * 2] = s1;
-      st[((long)row * (d / 16) + c / 16) * 2 + 1] = s2;
+        for (int o = 1; o < 32; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      } else {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      }
+      if (c < d && (c & (st_w - 1)) == 0) {
+        st[((long)row * (d / st_w) + c / st_w) * 2] = s1;
+        st[((long)row * (d / st_w) + c / st_w) * 2 + 1] = s2;
+      }
     }
   }
 }
 
 void embed(DType t, const void* emb, const void* pemb, const int* ids, const int* pos, float* x, float* st, int M,
-           int d, hipStream_t s, void* x16, int V, int rps) {
+           int d, hipStream_t s, void* x16, int V, int rps, int st_w) {
   rps = rps > 1 ? rps : 1;
   switch (t) {
     case kBF16: WCB_LAUNCH(embed_kernel<bf16_t>, dim3(M), dim3(256), 0, s, (const bf16_t*)emb,
-                                   (const bf16_t*)pemb, ids, pos, x, st, M, d, (bf16_t*)x16, V, rps); break;
+                                   (const bf16_t*)pemb, ids, pos, x, st, M, d, (bf16_t*)x16, V, rps, st_w); break;
     case kF16: WCB_LAUNCH(embed_kernel<f16_t>, dim3(M), dim3(256), 0, s, (const f16_t*)emb,
-                                  (const f16_t*)pemb, ids, pos, x, st, M, d, (f16_t*)x16, V, rps); break;
+                                  (const f16_t*)pemb, ids, pos, x, st, M, d, (f16_t*)x16, V, rps, st_w); break;
     case kF32: WCB_LAUNCH(embed_kernel<float>, dim3(M), dim3(256), 0, s, (const float*)emb,
-                                  (const float*)pemb, ids, pos, x, st, M, d, (float*)x16, V, rps); break;
+                                  (const float*)pemb, ids, pos, x, st, M, d, (float*)x16, V, rps, st_w); break;
   }
 }
 

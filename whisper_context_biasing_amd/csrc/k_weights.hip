@@ -6,6 +6,7 @@
 // QKV, conv im2col order, the W_k,hᵀ panels, the cross-K/V stack, ...) with repack_kernel: a 3-D
 // strided gather with a scale, rounded once to the model dtype — the same round-to-nearest-even the
 // host packing used, so weights are bit-identical whichever way they arrived.
+
 #include <algorithm>
 
 #include "common.h"
@@ -81,12 +82,31 @@ __global__ __launch_bounds__(64) void ln_fold_kernel(const T* W, int K, const fl
   float su = 0.f, sc = 0.f;
   for (int k = lane; k < K; k += 64) {
     const float x = DT<T>::tof(w[k]);
-    su = fmaf(gam[k], x, su);
-    sc = fmaf(bet[k], x, sc);
+    su = gam ? fmaf(gam[k], x, su) : su + x;
+    sc = bet ? fmaf(bet[k], x, sc) : sc;
   }
   su = wave_sum(su);
   sc = wave_sum(sc);
-  if (lane == 0) { u[n] = su; c[n] = sc + (bias ? bias[n] : 0.f); }
+  if (lane == 0) {
+    u[n] = su;
+    if (c) c[n] = sc + (bias ? bias[n] : 0.f);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void scale_cols_kernel(const T* W, long n_el, int K, const float* gam, T* Wg) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n_el; i += (long)gridDim.x * 256)
+    Wg[i] = DT<T>::fromf(gam[i % K] * DT<T>::tof(W[i]));
+}
+
+void scale_cols(DType t, const void* W, int N, int K, const float* gam, void* Wg, hipStream_t s) {
+  const long n = (long)N * K;
+  const dim3 grid((unsigned)std::min<long>((n + 255) / 256, 8192));
+  switch (t) {
+    case kBF16: WCB_LAUNCH(scale_cols_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)W, n, K, gam, (bf16_t*)Wg); break;
+    case kF16: WCB_LAUNCH(scale_cols_kernel<f16_t>, grid, dim3(256), 0, s, (const f16_t*)W, n, K, gam, (f16_t*)Wg); break;
+    case kF32: WCB_LAUNCH(scale_cols_kernel<float>, grid, dim3(256), 0, s, (const float*)W, n, K, gam, (float*)Wg); break;
+  }
 }
 
 void ln_fold(DType t, const void* W, int N, int K, const float* gam, const float* bet, const float* bias, float* u,

@@ -26,6 +26,8 @@
 // xenc_merge_kernel: workgroup = (head, row): merges the ranges (fixed order: deterministic) and
 //   normalises: u[row][h] = Σ_j p_j,h e_j in the model dtype. W_v,h and b_v are then one block-diagonal
 //   skinny GEMM (gemm_impl.h, grouped A), whose output feeds the out-projection GEMM.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -512,6 +514,178 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
       out[(long)b * ldo + n] = DT<T>::fromf(dsum + bv[n]);
     }
   }
+}
+
+// xq_kq_kernel: workgroup = (column block cb of CB columns of q'_h, head h, row block of 16·MF rows),
+// 4 waves. Phase 1 is the LN-fused q_proj decode GEMM of gemm_dec_kernel (AM = 2) restricted to the
+// head's 64 columns, with its exact arithmetic: the K range split over the 4 waves (KPW 32-deep steps
+// each, the same split as the decode-GEMM table for K = D), row statistics from the loaded 16-bit
+// residual copy (per-wave partials summed in wave order), γ/β through LDS, wave partials summed in
+// wave order, + b_q, rounded to T. Phase 2 is the grouped W_k,hᵀ product of the decode GEMM with
+// K = 64 (two 32-deep MFMA steps summed after the fact, as its two waves do). Every load of the launch
+// (the head's W_q rows, the W_kt block, the residual rows, LN parameters, b_q) is issued up front.
+// The head's W_q rows are read by the D/CB workgroups of that head (L2 / Infinity Cache after the
+// first): redundant reads bought with one dependent launch fewer per decoder layer.
+template <typename T, int D, int MF>
+__global__ __launch_bounds__(256) void xq_kq_kernel(XqkArgs a) {
+  using Frag = typename DT<T>::frag;
+  constexpr int NW = 4, KPW = D / 128, R = MF * 16, CB = 64;
+  __shared__ __attribute__((aligned(16))) float red[NW][R][65];
+  __shared__ __attribute__((aligned(16))) float lnp[2 * D];
+  __shared__ float2 rst[NW][R];
+  __shared__ __attribute__((aligned(16))) T qh[R][64 + 8];     // q_h rows (T), the phase-2 A operand
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cb = blockIdx.x, h = blockIdx.y, mb = blockIdx.z * R;
+  const int kb = wave * (KPW * 32) + 8 * (lane >> 4);
+  // ---- every load of the launch
+  Frag w[4][KPW];                                   // W_q rows h·64 + 16j + (lane & 15)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const T* W = reinterpret_cast<const T*>(a.wq) + (long)(h * 64 + j * 16 + (lane & 15)) * D + kb;
+#pragma unroll
+    for (int ks = 0; ks < KPW; ++ks) w[j][ks] = __builtin_nontemporal_load(reinterpret_cast<const Frag*>(W + ks * 32));
+  }
+  Frag wk[2];                                       // W_kt[h][cb·CB + 16·wave + (lane & 15)][k]
+  {
+    const T* Wk = reinterpret_cast<const T*>(a.wkt) + ((long)h * D + cb * CB + wave * 16 + (lane & 15)) * 64 + 8 * (lane >> 4);
+    wk[0] = load_frag<T>(Wk);
+    wk[1] = load_frag<T>(Wk + 32);
+  }
+  Frag x[MF][KPW];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    const int m = min(mb + i * 16 + (lane & 15), a.M - 1);
+    const T* xr = reinterpret_cast<const T*>(a.x16) + (long)m * D + kb;
+#pragma unroll
+    for (int ks = 0; ks < KPW; ++ks) x[i][ks] = load_frag<T>(xr + ks * 32);
+  }
+  constexpr int LQ = (2 * D / 4 + 255) / 256;
+  f32x4 lq[LQ];
+#pragma unroll
+  for (int j = 0; j < LQ; ++j) {
+    const int c = (j * 256 + tid) * 4;
+    lq[j] = c < 2 * D ? *reinterpret_cast<const f32x4*>((c < D ? a.ln_w : a.ln_b) + (c < D ? c : c - D))
+                      : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  constexpr int EP = (R * 64 + 255) / 256;          // phase-1 outputs per thread
+  float pf_bias[EP];
+#pragma unroll
+  for (int it = 0; it < EP; ++it) pf_bias[it] = a.bq[h * 64 + ((it * 256 + tid) & 63)];
+  __builtin_amdgcn_sched_barrier(0);
+  // ---- LayerNorm of the rows (gemm_dec_kernel AM = 2 arithmetic)
+  float xv[MF][KPW][8];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KPW; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v;
+        if constexpr (__is_same(T, bf16_t)) v = bf16_to_f((bf16_t)x[i][ks][e]);
+        else v = float(x[i][ks][e]);
+        xv[i][ks][e] = v;
+        s1 += v;
+        s2 = fmaf(v, v, s2);
+      }
+    s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
+    if (lane < 16) rst[wave][i * 16 + lane] = float2{s1, s2};
+  }
+#pragma unroll
+  for (int j = 0; j < LQ; ++j) {
+    const int c = (j * 256 + tid) * 4;
+    if (c < 2 * D) *reinterpret_cast<f32x4*>(lnp + c) = lq[j];
+  }
+  __syncthreads();
+  f32x4 acc[MF][4];
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) { const float2 t = rst[ww][i * 16 + (lane & 15)]; s1 += t.x; s2 += t.y; }
+    const float mean = s1 / D;
+    const float rstd = rsqrtf(fmaxf(s2 / D - mean * mean, 0.f) + 1e-5f);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KPW; ++ks) {
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(lnp + kb + ks * 32);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(lnp + kb + ks * 32 + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(lnp + D + kb + ks * 32);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(lnp + D + kb + ks * 32 + 4);
+      Frag af;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gw = e < 4 ? w0[e] : w1[e - 4], gb = e < 4 ? b0[e] : b1[e - 4];
+        const float v = (xv[i][ks][e] - mean) * rstd * gw + gb;
+        af[e] = __builtin_bit_cast(typename std::remove_reference<decltype(af[0])>::type, DT<T>::fromf(v));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mma16(af, w[j][ks], acc[i][j]);
+    }
+  }
+  // ---- wave partials → LDS, summed in wave order + b_q, rounded to T: q_h
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[wave][i * 16 + (lane >> 4) * 4 + e][j * 16 + (lane & 15)] = acc[i][j][e];
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < EP; ++it) {
+    const int o = it * 256 + tid;
+    if (o < R * 64) {
+      const int r = o >> 6, c = o & 63;
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) v += red[ww][r][c];
+      qh[r][c] = DT<T>::fromf(v + pf_bias[it]);
+    }
+  }
+  __syncthreads();
+  // ---- phase 2: q'_h[m][c] = Σ_i q_h[m][i] W_kt[h][c][i], wave → 16 columns of the block
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    const Frag a0 = *reinterpret_cast<const Frag*>(&qh[i * 16 + (lane & 15)][8 * (lane >> 4)]);
+    const Frag a1 = *reinterpret_cast<const Frag*>(&qh[i * 16 + (lane & 15)][32 + 8 * (lane >> 4)]);
+    const f32x4 p0 = mma16(a0, wk[0], f32x4{0.f, 0.f, 0.f, 0.f});
+    const f32x4 p1 = mma16(a1, wk[1], f32x4{0.f, 0.f, 0.f, 0.f});
+    const int c = cb * CB + wave * 16 + (lane & 15);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = mb + i * 16 + (lane >> 4) * 4 + e;
+      if (m < a.M) reinterpret_cast<T*>(a.qp)[((long)m * a.H + h) * D + c] = DT<T>::fromf(p0[e] + p1[e]);
+    }
+  }
+}
+
+bool xqk_supported(DType t, int D) {
+  return (t == kBF16 || t == kF16) && (D == 384 || D == 512 || D == 768 || D == 1024);
+}
+
+template <typename T, int D>
+static void launch_xqk(const XqkArgs& a, hipStream_t s) {
+  // 16 rows per workgroup up to 16 rows, else 32 (more rows per W_q read; C2's 32 rows: one row block)
+  if (a.M <= 16) WCB_LAUNCH((xq_kq_kernel<T, D, 1>), dim3(D / 64, a.H, 1), dim3(256), 0, s, a);
+  else WCB_LAUNCH((xq_kq_kernel<T, D, 2>), dim3(D / 64, a.H, (a.M + 31) / 32), dim3(256), 0, s, a);
+}
+
+template <typename T>
+static void launch_xqk_t(const XqkArgs& a, hipStream_t s) {
+  switch (a.D) {
+    case 384: launch_xqk<T, 384>(a, s); break;
+    case 512: launch_xqk<T, 512>(a, s); break;
+    case 768: launch_xqk<T, 768>(a, s); break;
+    case 1024: launch_xqk<T, 1024>(a, s); break;
+    default: break;
+  }
+}
+
+void xq_kq(DType t, const XqkArgs& a, hipStream_t s) {
+  if (t == kBF16) launch_xqk_t<bf16_t>(a, s);
+  else if (t == kF16) launch_xqk_t<f16_t>(a, s);
 }
 
 bool xenc_supported(DType t, int D) {

@@ -76,24 +76,31 @@ struct GemmArgs {
   // LN-fused A read from such a copy instead of the f32 rows (lda elements per row)
   void* out16 = nullptr;
   const void* ln_a16 = nullptr;
-  // folded LayerNorm (ring tiles, decode rows > 64): A = the 16-bit residual rows x, ln_w = γ, ln_u =
-  // Σ_k γ_k W[n][k]; bias holds Σ_k β_k W[n][k] + bias. out = r·(Σ_k bf16(x_k γ_k) W[n][k] − μ·ln_u[n]) + bias
+  // folded LayerNorm (ring tiles, decode rows > 64, gemm_impl.h LNF): A = the 16-bit residual rows x,
+  // W = W' = W·diag(γ), ln_u = Σ_k W'[n][k], bias = ln_c = Σ_k β_k W[n][k] + b[n]; out = r·(acc − μ·ln_u[n]) + bias
+  // with (μ, r) from rst_in: per row rst_nb = K / 32 partial sums (Σx, Σx²) of 32 columns each
   const float* ln_u = nullptr;
   const float* ln_c = nullptr;     // Σ_k β_k W[n][k] + bias[n] (becomes `bias` when the fold is taken)
+  const void* ln_wg = nullptr;     // W' = W·diag(γ) in the model dtype (becomes `W` when the fold is taken)
+  const float* rst_in = nullptr; int rst_nb = 0;
+  float* rst_out = nullptr;        // ring-tile residual writers: [M][N / 32] float2 partials of the written f32 rows
   // f16 encoder layers: the layer output is clamped to ±(finfo(f16).max − 1000)
   // ([tf] modeling_whisper.py:409-411); 0 = off
   float clamp = 0.f;
 };
 
 void gemm(DType t, const GemmArgs& g, hipStream_t s);
+constexpr int kLnfMaxK = 1280;   // widest K of the ring tiles' folded LayerNorm (GemmArgs::ln_wg)
 
 // LayerNorm over rows of f32 x[M][d] → T y[M][d] (w, b f32).
 void layernorm(DType t, const float* x, const float* w, const float* b, void* y, int M, int d,
                hipStream_t s);
 
 // x[r][:] = emb[ids[r]][:] + pos_emb[*pos + r_pos][:] (f32 out), r_pos = r % rows_per_seq.
+// stats: per-st_w-column partial sums (Σx, Σx²) of the new rows (16: the older skinny consumers; 32:
+// the ring tiles' folded LayerNorm, GemmArgs::rst_in)
 void embed(DType t, const void* emb, const void* pos_emb, const int* ids, const int* pos, float* x,
-           float* stats, int M, int d, hipStream_t s, void* x16 = nullptr, int V = 1 << 30, int rps = 1);
+           float* stats, int M, int d, hipStream_t s, void* x16 = nullptr, int V = 1 << 30, int rps = 1, int st_w = 16);
 // prefill: ids[r·np + t] = src[r·ld + *pos + t] (ld 0: one prefix row shared by every row)
 void prefill_ids(int* ids, const int* src, int R, int np, int ld, const int* pos, hipStream_t s);
 void add_i32(int* p, int v, hipStream_t s);   // *p += v (one thread)
@@ -157,6 +164,19 @@ void xenc_attention(DType t, const XencArgs& a, hipStream_t s);
 void xenc_merge(DType t, const XencArgs& a, void* u, long ldu, hipStream_t s);
 // merge + value projection fused (D % 128 == 0): o[row][h·64 + j] = W_v,h·u_h + b_v, T
 void xenc_merge_v(DType t, const XencArgs& a, const void* wv, const float* bv, void* o, long ldo, hipStream_t s);
+// The cross-attention query of the encoder-space formulation in ONE launch (replaces the LN-fused
+// q_proj decode GEMM + the grouped W_k,hᵀ GEMM): q_h = LN(x) W_q,hᵀ + b_q,h rounded to T (bit-identical
+// to the two-launch path), then q'_h[c] = Σ_i W_kt[h][c][i] q_h[i] for this workgroup's block of c.
+struct XqkArgs {
+  const void* x16 = nullptr;                    // [M][D] T copy of the residual stream (LayerNorm input)
+  const float* ln_w = nullptr; const float* ln_b = nullptr;
+  const void* wq = nullptr; const float* bq = nullptr;   // [D][D] (pre-scaled q_proj), [D]
+  const void* wkt = nullptr;                    // [H][D][64]
+  void* qp = nullptr;                           // [M][H][D] T
+  int M = 0, H = 0, D = 0;
+};
+bool xqk_supported(DType t, int D);
+void xq_kq(DType t, const XqkArgs& a, hipStream_t s);
 
 // log-mel front end
 void logmel_power_mel(const float* pcm, long pcm_stride, int n_samples, int B, const float* dft,
@@ -236,10 +256,13 @@ struct RepackArgs { void* dst = nullptr; const float* src = nullptr; int n[3] = 
                     long t[3] = {0, 0, 0}; float scale = 1.f; };
 void repack(DType t, const RepackArgs& a, hipStream_t s);
 void count_diff(const float* a, const float* b, long n, int* count, hipStream_t s);   // b null: nonzeros
-// u[n] = Σ_k γ_k W[n][k], c[n] = Σ_k β_k W[n][k] + bias[n] (the LayerNorm fold of gemm_impl.h LNF)
+// u[n] = Σ_k γ_k W[n][k], c[n] = Σ_k β_k W[n][k] + bias[n] (the LayerNorm fold of gemm_impl.h LNF;
+// gam null: γ = 1; bet / c null: no c)
 void ln_fold(DType t, const void* W, int N, int K, const float* gam, const float* bet, const float* bias, float* u,
              float* c, hipStream_t s);
 
+// Wg[n][k] = T(γ_k · W[n][k]) (the folded LayerNorm's weights)
+void scale_cols(DType t, const void* W, int N, int K, const float* gam, void* Wg, hipStream_t s);
 void fill_i32(int* p, int v, long n, hipStream_t s);
 // dst[0..n) = host values, passed by value in the kernel arguments (stream-ordered, no host buffer
 // lifetime or pageable-copy ordering to worry about)

@@ -86,8 +86,10 @@ struct LayerW {
   void* fc1_w = nullptr; float* fc1_b = nullptr;
   void* fc2_w = nullptr; float* fc2_b = nullptr;
   float *ln2_w = nullptr, *ln2_b = nullptr;
-  // decoder, 16-bit: the pre-block LayerNorms folded into their consumers for rows > 64 (ring LNF):
-  // u = Σ_k γ_k W[n][k], c = Σ_k β_k W[n][k] + bias, for QKV (ln1), cross-q (lnx), fc1 (ln2)
+  // decoder, 16-bit: the pre-block LayerNorms folded into their consumers for rows > 64 (ring LNF,
+  // gemm_impl.h): W' = W·diag(γ) (T), u = Σ_k W'[n][k], c = Σ_k β_k W[n][k] + bias, for QKV (ln1),
+  // cross-q (lnx), fc1 (ln2)
+  void *qkv_wg = nullptr, *xq_wg = nullptr, *fc1_wg = nullptr;
   float *ln1_u = nullptr, *ln1_c = nullptr, *lnx_u = nullptr, *lnx_c = nullptr, *ln2_u = nullptr, *ln2_c = nullptr;
   // encoder-space cross-attention (k_xenc.hip): W_k,hᵀ repacked [H][d][64], W_v [d][d], b_v
   void* xkt_w = nullptr; void* xv_w = nullptr; float* xv_b = nullptr;
@@ -121,8 +123,8 @@ struct DecCtx {
   hipStream_t sub[kMaxSub] = {};                // row-group chains (fork/join inside the step graph)
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSub] = {};
   int dec_B = 0, dec_T = 0;
-  DevBuf kvself, dx, dx16, dh, dq, dqp, du, datt, dffn, dstats, xpart, xml, xticket, logits, part_val, part_idx, ints, pids,
-      outbuf, forced, beam;
+  DevBuf kvself, dx, dx16, dh, dq, dqp, du, datt, dffn, dstats, drst, xpart, xml, xticket, logits, part_val, part_idx, ints,
+      pids, outbuf, forced, beam;
   int nchunk = 64;
   hipGraphExec_t gexec = nullptr;               // captured decode step
   hipGraphExec_t gexec_k = nullptr;             // steps_per_graph consecutive decode steps in one graph
@@ -160,14 +162,18 @@ struct wcb_handle {
   // per (clip, head), merged by flash_merge_kernel. Fixed per handle (never from the batch). Measured
   // (audio-s/s, splits 1 / 2 / 4): C3 4491 / 4531 / 4452, C5 1405 / 1484 / 1485.
   int flash_split = 2;
-  // decode rows > 64 (16-bit): pre-block LayerNorms folded into the ring-tile projections (no
-  // LayerNorm launch, option "ln_fold" = 1) or a LayerNorm launch before each (0, default). Measured
-  // (audio-s/s, fold / launch): C3 4425 / 4572, C5 1399 / 1490 — the per-element γ scaling and row
-  // sums inside the latency-bound ring loop cost more than the 4.6 µs launch they remove.
-  int ln_fold = 0;
+  // decode rows > 64 (16-bit): pre-block LayerNorms folded into the ring-tile projections (option
+  // "ln_fold" 1: γ folded into the weights, (μ, r) from the residual writers' per-32-column partial
+  // sums, applied in the epilogue — no per-element work in the K loop, no LayerNorm launch) or a
+  // LayerNorm launch before each projection (0). (Round 2's in-loop form — A scaled by γ and the row
+  // sums accumulated inside the K loop — measured slower than the launch and is gone.)
+  int ln_fold = 1;
   // greedy cross-attention (encoder space): range merge and W_v in one launch (option "merge_v";
   // C2 16,570 vs 16,259 audio-s/s for the two launches)
   int merge_v = 1;
+  // greedy cross-attention query (<= 64 rows, encoder space): LN + q_proj + W_k,hᵀ as one launch
+  // (option "xqk"; 0 = the two decode GEMMs, bit-identical)
+  int xqk = 1;
   // decode rows > 64: 64-deep K sub-tiles per ring stage of the 64x32 / 32x32 tiles (option "ring_kt",
   // 1 or 2; C5 1,594 -> 1,644 audio-s/s)
   int ring_kt = 2;
@@ -391,7 +397,7 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     const int dprio = prio_hi;
     HIPCHK(hipStreamCreateWithPriority(&h->he, hipStreamNonBlocking, 0));
-    for (int ci = 0; ci < h->nctx; ++ci) {
+    for (int ci = 0; ci < wcb_handle::kMaxCtx; ++ci) {   // every context (option decode_contexts picks how many)
       DecCtx& D = h->dc[ci];
       HIPCHK(hipStreamCreateWithPriority(&D.hs, hipStreamNonBlocking, dprio));
       HIPCHK(hipEventCreateWithFlags(&D.ev_fork, hipEventDisableTiming));
@@ -402,7 +408,7 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
         HIPCHK(hipEventCreateWithFlags(&D.ev_join[i], hipEventDisableTiming));
       }
     }
-    for (int i = 0; i < h->nctx; ++i) {
+    for (int i = 0; i < wcb_handle::kMaxCtx; ++i) {
       HIPCHK(hipEventCreateWithFlags(&h->ev_xkv[i], hipEventDisableTiming));
       HIPCHK(hipEventCreateWithFlags(&h->ev_dec[i], hipEventDisableTiming));
     }
@@ -472,7 +478,7 @@ void wcb_destroy(wcb_handle* h) {
   for (DecCtx& D : h->dc) {
     if (D.gexec) (void)hipGraphExecDestroy(D.gexec);
     if (D.gexec_k) (void)hipGraphExecDestroy(D.gexec_k);
-    for (DevBuf* b : {&D.kvself, &D.dx, &D.dx16, &D.dh, &D.dq, &D.dqp, &D.du, &D.datt, &D.dffn, &D.dstats, &D.xpart, &D.xml, &D.xticket,
+    for (DevBuf* b : {&D.kvself, &D.dx, &D.dx16, &D.dh, &D.dq, &D.dqp, &D.du, &D.datt, &D.dffn, &D.dstats, &D.drst, &D.xpart, &D.xml, &D.xticket,
                       &D.logits, &D.part_val, &D.part_idx, &D.ints, &D.outbuf, &D.forced, &D.beam})
       b->release();
     if (D.ev_fork) (void)hipEventDestroy(D.ev_fork);
@@ -517,6 +523,9 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       if (n == "xmode") h->xmode = value && xenc_supported(h->dt, h->d.d_model);
       else h->beam_xmode = value && h->xmode;
       if (!h->xmode) h->beam_xmode = 0;
+    } else if (n == "decode_contexts") {
+      REQUIRE(value >= 1 && value <= wcb_handle::kMaxCtx, "option decode_contexts: 1..4");
+      h->nctx = value;
     } else if (n == "group_rows") {
       REQUIRE(value >= 16 && value <= 512, "option group_rows: 16..512");
       h->group_rows = value;
@@ -533,6 +542,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "ring_kt") {
       REQUIRE(value == 1 || value == 2, "option ring_kt: 1 or 2");
       h->ring_kt = value;
+    } else if (n == "xqk") {
+      h->xqk = value != 0;
     } else if (n == "merge_v") {
       h->merge_v = value != 0;
     } else if (n == "ln_fold") {
@@ -699,14 +710,20 @@ int wcb_finalize_weights(wcb_handle* h) {
     if (h->dt != kF32) {
       for (int i = 0; i < L; ++i) {
         LayerW& lw = h->dec[i];
-        auto fold = [&](const void* W, int N, const float* gam, const float* bet, const float* bias, float*& u, float*& c) {
+        // W' = W·diag(γ) rounded to T, u = Σ_k W'[n][k] (of the rounded W': the epilogue's μ·u then
+        // removes exactly the mean the accumulator carries), c = Σ_k β_k W[n][k] + bias
+        auto fold = [&](const void* W, int N, const float* gam, const float* bet, const float* bias, void*& Wg, float*& u,
+                        float*& c) {
+          Wg = h->own((size_t)N * d * e);
           u = reinterpret_cast<float*>(h->own((size_t)N * 4));
           c = reinterpret_cast<float*>(h->own((size_t)N * 4));
-          ln_fold(h->dt, W, N, d, gam, bet, bias, u, c, st);
+          scale_cols(h->dt, W, N, d, gam, Wg, st);
+          ln_fold(h->dt, W, N, d, gam, bet, bias, u, c, st);          // c (u overwritten below)
+          ln_fold(h->dt, Wg, N, d, nullptr, nullptr, nullptr, u, nullptr, st);
         };
-        fold(lw.qkv_w, 3 * d, lw.ln1_w, lw.ln1_b, lw.qkv_b, lw.ln1_u, lw.ln1_c);
-        fold(lw.xq_w, d, lw.lnx_w, lw.lnx_b, lw.xq_b, lw.lnx_u, lw.lnx_c);
-        fold(lw.fc1_w, F, lw.ln2_w, lw.ln2_b, lw.fc1_b, lw.ln2_u, lw.ln2_c);
+        fold(lw.qkv_w, 3 * d, lw.ln1_w, lw.ln1_b, lw.qkv_b, lw.qkv_wg, lw.ln1_u, lw.ln1_c);
+        fold(lw.xq_w, d, lw.lnx_w, lw.lnx_b, lw.xq_b, lw.xq_wg, lw.lnx_u, lw.lnx_c);
+        fold(lw.fc1_w, F, lw.ln2_w, lw.ln2_b, lw.fc1_b, lw.fc1_wg, lw.ln2_u, lw.ln2_c);
       }
     }
     h->enc_ln_w = F_("model.encoder.layer_norm.weight", d);
@@ -904,6 +921,7 @@ void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode
     D.datt.ensure((size_t)rows * d * e);
     D.dffn.ensure((size_t)rows * h->d.ffn * e);
     D.dstats.ensure((size_t)rows * (d / 16) * 2 * 4);
+    D.drst.ensure((size_t)rows * (d / 32) * 2 * 4);
     D.xpart.ensure(std::max((size_t)rows * h->H() * kXSplit * 66, (size_t)rows * h->xenc_split * h->H() * d) * 4);
     D.xml.ensure((size_t)rows * h->xenc_split * h->H() * 2 * 4);
     D.dqp.ensure((size_t)rows * h->H() * d * e);
@@ -942,6 +960,11 @@ struct StepCfg {
   int rps = 1;                         // positions per decoder row in this pass (> 1: causal prefill)
 };
 
+// the folded LayerNorm of the > 64-row projections is available (16-bit, d a multiple of 32)
+bool lnf_possible(const wcb_handle* h) {
+  return h->ln_fold && h->dt != kF32 && h->d.d_model % 32 == 0 && h->d.d_model <= kLnfMaxK;
+}
+
 // Decoder layers + LM head for rows [b0, b0 + nb) of the batch on stream `st_`: WhisperDecoder.forward
 // with a KV cache ([tf] modeling_whisper.py:690-795). Every position-dependent quantity is read on
 // the device, so the launch sequence replays as a hipGraph. Row-indexed buffers are addressed with
@@ -961,6 +984,10 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
   const int nbk = d / 16;
   float* st = D.dstats.as<float>() + (size_t)r0 * nbk * 2;
   float* st_pub = h->dec_gemm ? nullptr : st;   // LN partial sums only for the older skinny consumers
+  // > 64 rows, 16-bit, decode GEMMs supported: every residual writer is a ring tile that publishes
+  // per-32-column (Σx, Σx²) of its rows (and the embedding does), so the LN consumers fold the
+  // LayerNorm into their tiles (ln_fold) instead of a LayerNorm launch each
+  float* rst = D.drst.as<float>() + (size_t)r0 * (d / 32) * 2;
   char* dq = (char*)D.dq.p + (size_t)r0 * d * e;
   char* datt = (char*)D.datt.p + (size_t)r0 * d * e;
   char* dffn = (char*)D.dffn.p + (size_t)r0 * h->d.ffn * e;
@@ -971,6 +998,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
   // N >= 2048 projections (QKV, fc1) at >= 192 rows (C3: 320 beam rows); the d-wide projections keep
   // the decode kernel (and keep writing the 16-bit residual copy its LayerNorm consumers read).
   const bool tiled = M > 64;
+  const bool lnf_ok = tiled && h->dec_gemm && lnf_possible(h);
   char* dh = (char*)D.dh.p + (size_t)r0 * d * e;
   auto proj = [&](const char* cls, GemmArgs g) {
     const bool lm = g.W == h->tok_emb;
@@ -979,9 +1007,10 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     // and re-reads the weights per 32 rows)
     const bool ring = h->dt != kF32 && !lm && !g.st_out;
     if (tiled && !g.a_grp_n && (lm || ring || (M >= 192 && g.N >= 2048))) {
-      if (g.ln_w && ring && g.ln_u && h->ln_fold && lna) {   // LayerNorm folded into the ring tiles
-        g.A = lna; g.lda = d;
-        g.bias = g.ln_c; g.ln_b = nullptr; g.st_in = nullptr; g.ln_a16 = nullptr;
+      if (g.ln_w && ring && g.ln_u && g.ln_wg && lnf_ok && lna) {   // LayerNorm folded into the ring tiles
+        g.A = lna; g.lda = d; g.W = g.ln_wg; g.ldw = g.K;
+        g.bias = g.ln_c; g.ln_w = g.ln_b = nullptr; g.st_in = nullptr; g.ln_a16 = nullptr;
+        g.rst_in = rst; g.rst_nb = d / 32;
       } else if (g.ln_w) {
         g.ln_u = nullptr;
         const float* xa = static_cast<const float*>(g.A);
@@ -991,6 +1020,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
         g.ln_w = g.ln_b = nullptr; g.st_in = nullptr; g.ln_a16 = nullptr;
       }
       g.tile = ring ? 2 : 1; g.skinny = 0; g.ring_kt = h->ring_kt;
+      if (ring && g.resid && g.out16 && lnf_ok) g.rst_out = rst;   // residual writer: stats for the next LN
     }
     dgemm(h, cls, g, st_);
   };
@@ -1003,7 +1033,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     GemmArgs q = drow(x, d, w.qkv_w, M, 3 * d, d, dq, d);    // LayerNorm fused (f32 A rows)
     q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nbk; q.ln_a16 = lna;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
-    q.kv_rps = rps; q.ln_u = w.ln1_u; q.ln_c = w.ln1_c;
+    q.kv_rps = rps; q.ln_u = w.ln1_u; q.ln_c = w.ln1_c; q.ln_wg = w.qkv_wg;
     proj("dec_qkv", q);
     AttnArgs a;
     a.q = dq; a.ldq = d; a.q_Sb = rps; a.Sq = rps; a.causal = rps > 1;
@@ -1025,13 +1055,22 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       // cross attention in encoder space: q'_h = W_k,hᵀ q_h (block-diagonal GEMM, K = 64), one pass
       // over the encoder output per layer for all heads, range combine + W_v,h + b_v
       char* dqp = (char*)D.dqp.p + (size_t)r0 * H * d * e;
-      GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
-      xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
-      xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c;
-      proj("dec_xq", xq);
-      GemmArgs kq = drow(dq, d, w.xkt_w, M, H * d, 64, dqp, (long)H * d);
-      kq.a_grp_n = d; kq.a_grp_off = 64;
-      proj("dec_kq", kq);
+      if (!tiled && lna && h->xqk && xqk_supported(h->dt, d)) {
+        // LN + q_proj + W_k,hᵀ in one launch (bit-identical to the two decode GEMMs below)
+        XqkArgs qa;
+        qa.x16 = lna; qa.ln_w = w.lnx_w; qa.ln_b = w.lnx_b; qa.wq = w.xq_w; qa.bq = w.xq_b; qa.wkt = w.xkt_w;
+        qa.qp = dqp; qa.M = M; qa.H = H; qa.D = d;
+        h->timed("dec_xqk", 2.0 * M * d * d * 2, (2.0 * d * d * 2 + (double)M * d * (1 + H)) * e, st_,
+                 [&] { xq_kq(h->dt, qa, st_); });
+      } else {
+        GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
+        xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
+        xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg;
+        proj("dec_xq", xq);
+        GemmArgs kq = drow(dq, d, w.xkt_w, M, H * d, 64, dqp, (long)H * d);
+        kq.a_grp_n = d; kq.a_grp_off = 64;
+        proj("dec_kq", kq);
+      }
       XencArgs xa;
       xa.enc = h->xkv2[c.buf].p; xa.enc_sb = (long)S * d;
       xa.row0 = r0; xa.rows_per_enc = c.nb * rps;   // beams (and prefill positions) of a clip share its encoder output
@@ -1062,7 +1101,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       // cross attention over the precomputed encoder K/V
       GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
       xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
-      xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c;
+      xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg;
       proj("dec_xq", xq);
       AttnArgs xa;
       const char* xkv = (const char*)h->xkv2[c.buf].p + l * xkv_l * e;
@@ -1102,7 +1141,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     // MLP
     GemmArgs f1 = drow(x, d, w.fc1_w, M, h->d.ffn, d, dffn, h->d.ffn);
     f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nbk; f1.ln_a16 = lna;
-    f1.bias = w.fc1_b; f1.act = 1; f1.ln_u = w.ln2_u; f1.ln_c = w.ln2_c;
+    f1.bias = w.fc1_b; f1.act = 1; f1.ln_u = w.ln2_u; f1.ln_c = w.ln2_c; f1.ln_wg = w.fc1_wg;
     proj("dec_fc1", f1);
     GemmArgs f2 = drow(dffn, h->d.ffn, w.fc2_w, M, d, h->d.ffn, x, d);
     f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st_pub; f2.st_nb = nbk; f2.out16 = x16;
@@ -1141,9 +1180,11 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
   int* ints = D.ints.as<int>();
   int* pos = ints + I_POS;
   int* next_ids = ints + I_NEXT;
+  const bool r32 = h->dec_gemm && lnf_possible(h);   // 32-column stats for the folded LayerNorm (rows > 64)
   h->timed("dec_embed", 0, (double)B * d * (2.0 * esize(h->d.dtype) + 4), D.hs, [&] {
-    embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, D.dx.as<float>(), h->dec_gemm ? nullptr : D.dstats.as<float>(), B, d,
-        D.hs, D.dx16.p, h->d.vocab);
+    embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, D.dx.as<float>(),
+          !h->dec_gemm ? D.dstats.as<float>() : r32 ? D.drst.as<float>() : nullptr, B, d, D.hs, D.dx16.p, h->d.vocab, 1,
+          r32 ? 32 : 16);
   });
   // rows per chain: the skinny projections split rows over grid.y, so a chain can take any number
   // of rows (WCB_GROUP_ROWS; more chains overlap latency, fewer re-read the weights less often)
@@ -1203,8 +1244,9 @@ void prefill_step(wcb_handle* h, StepCfg c, int np, const int* src, int ld) {
   c.beam = nullptr;
   h->timed("dec_embed", 0, (double)M * d * (2.0 * esize(h->d.dtype) + 4), D.hs, [&] {
     prefill_ids(D.pids.as<int>(), src, R, np, ld, pos, D.hs);
-    embed(h->dt, h->tok_emb, h->dec_pos, D.pids.as<int>(), pos, D.dx.as<float>(), nullptr, M, d, D.hs, D.dx16.p,
-          h->d.vocab, np);
+    const bool r32 = h->dec_gemm && lnf_possible(h);
+    embed(h->dt, h->tok_emb, h->dec_pos, D.pids.as<int>(), pos, D.dx.as<float>(), r32 ? D.drst.as<float>() : nullptr, M,
+          d, D.hs, D.dx16.p, h->d.vocab, np, 32);
   });
   decode_rows(h, c, 0, R, 0, D.hs);
   add_i32(pos, np, D.hs);

@@ -334,7 +334,10 @@ class WhisperCB:
         phrases = bias_list
         if phrases is None and bias_boost > 0 and bias_spans is not None:
             phrases = self._spans_to_phrases(bias_spans)
-        bl = self.bias_list(phrases) if (phrases and bias_boost > 0) else None
+        if isinstance(phrases, BiasList):          # a prebuilt automaton (it must belong to this model)
+            bl = phrases if bias_boost > 0 else None
+        else:
+            bl = self.bias_list(phrases) if (phrases and bias_boost > 0) else None
         cfg = _lib.WcbGenCfg(max_new, int(min_new_tokens), num_beams, float(bias_boost), int(use_graph), int(not block))
         out = torch.empty(B, max_new, dtype=torch.int32, device=self.device)
         steps = C.c_int32(0)
