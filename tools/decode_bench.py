@@ -29,9 +29,11 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--concurrent", type=int, default=0,
                     help="also time this many overlapping async calls of --long tokens (decode contexts in flight)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE", help="wcb_set_option")
     a = ap.parse_args()
     dims = get_dims(a.model)
-    m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=0), dtype=a.dtype)
+    opts = {k: int(v) for k, v in (o.split("=", 1) for o in a.opt)}
+    m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=0), dtype=a.dtype, options=opts or None)
     pcm = torch.from_numpy(synth_batch(a.batch)).cuda()
     mel = m.log_mel(pcm)
     phrases = synth_bias_list(a.phrases, eot=dims.eos_token_id) if a.phrases else None
@@ -50,7 +52,7 @@ def main():
         t0 = time.perf_counter(); run(a.short); ts.append(time.perf_counter() - t0)
         t0 = time.perf_counter(); run(a.long); tl.append(time.perf_counter() - t0)
     per_tok = (min(tl) - min(ts)) / (a.long - a.short) * 1e3
-    print(f"{a.model} B={a.batch} beams={a.beams} {a.dtype}: call {a.short} tok {min(ts)*1e3:.2f} ms, "
+    print(f"{a.model} B={a.batch} beams={a.beams} {a.dtype} {opts or ''}: call {a.short} tok {min(ts)*1e3:.2f} ms, "
           f"{a.long} tok {min(tl)*1e3:.2f} ms -> {per_tok:.3f} ms/token (decode alone), "
           f"encoder+setup ~{(min(ts) * 1e3 - a.short * per_tok):.2f} ms", flush=True)
 
