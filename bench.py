@@ -221,16 +221,23 @@ def main():
     lo, hi = shard_bounds(world * B, rank, world)                      # this rank's utterances
     pcm = torch.from_numpy(synth_batch(hi - lo, start=lo)).to(dev)     # resident in HBM before timing
     # bias list (untimed setup): matches start only at word-start tokens (synthetic half of the
-    # vocabulary, the role of BPE's leading-space tokens); one phrase per clip built from its own
-    # lam = 0 decode's runner-up continuation (so the boost has something to place and the biased-WER
-    # half of the metric is not vacuous), the rest of the list from the reference's bias-word pool
+    # vocabulary, the role of BPE's leading-space tokens); the reference's bias-word pool, plus one phrase
+    # per clip built from its own lam = 0 decode's runner-up continuation at a step where a boost of
+    # lam_plumb places it (so the biased-WER half of the metric measures the boost). lam_plumb is sized
+    # to this random-weight model's logit gaps (2 x the median top-1/top-2 gap): the bench's lam = 2
+    # is 10-30x those gaps and flips the first step of every clip (reported as measured, below).
     ws = synth_word_start(dims.eos_token_id, dims.vocab)
     model.set_word_start(ws)
-    targets, placed = [], []
+    pool_all = synth_bias_list(args.bias_phrases, eot=dims.eos_token_id)
+    targets, placed, lam_plumb, gaps = [], [], None, None
     if args.boost > 0 and args.num_beams == 1:
-        _, placed, targets = runner_up_phrases(model, model.log_mel(pcm), args.new_tokens, args.boost, ws)
+        mel0 = model.log_mel(pcm)
+        _, _, _, gaps = runner_up_phrases(model, mel0, args.new_tokens, args.boost, ws)
+        lam_plumb = round(2.0 * float(np.median(gaps[:, 1:])), 4)
+        pool_cut = pool_all[:max(0, args.bias_phrases - B)]
+        _, placed, targets, _ = runner_up_phrases(model, mel0, args.new_tokens, lam_plumb, ws, pool=pool_cut)
     seen = {tuple(p) for p in placed}
-    pool = [p for p in synth_bias_list(args.bias_phrases, eot=dims.eos_token_id) if tuple(p) not in seen]
+    pool = [p for p in pool_all if tuple(p) not in seen]
     phrases = placed + pool[:max(0, args.bias_phrases - len(placed))]
     bias = model.bias_list(phrases)
     use_graph = not args.no_graph
@@ -354,44 +361,55 @@ def main():
     # placed phrases (each clip's runner-up continuation, absent from its lam = 0 decode); untimed
     bias_plumb = None
     if rank == 0 and args.boost > 0:
-        from whisper_context_biasing_amd.metrics import wer_counts
         import ctypes as C
         from whisper_context_biasing_amd import _lib
-        from whisper_context_biasing_amd.metrics import _cstrs
+        from whisper_context_biasing_amd.metrics import _cstrs, wer_counts
         mel = model.log_mel(pcm)
-        kw = dict(max_length=args.new_tokens, min_new_tokens=min_new, use_graph=use_graph,
-                  num_beams=args.num_beams)
-        boosted = model.generate(mel, bias_list=phrases, bias_boost=args.boost, **kw).cpu().tolist()
+        kw = dict(max_length=args.new_tokens, min_new_tokens=min_new, use_graph=use_graph, num_beams=args.num_beams)
         plain = model.generate(mel, **kw).cpu().tolist()
-        model.synchronize()
         as_text = lambda rows: [" ".join(map(str, r)) for r in rows]
-        err, words = wer_counts(as_text(boosted), as_text(plain))
         ptxt = [" ".join(map(str, p)) for p in phrases]
-        bd = bt = 0
-        for r, h in zip(as_text(boosted), as_text(plain)):   # phrases the boost placed, lost without it
-            d_, t_ = C.c_int64(), C.c_int64()
-            _lib.check(_lib.load().wcb_bias_counts((" " + r + " ").encode(), (" " + h + " ").encode(),
-                                                   _cstrs([" " + t + " " for t in ptxt]), len(ptxt),
-                                                   C.byref(d_), C.byref(t_)), None, "wcb_bias_counts")
-            bd += d_.value
-            bt += t_.value
-        has = lambda row, p: any(row[i:i + len(p)] == p for i in range(len(row) - len(p) + 1))
-        hit_b = sum(has(boosted[b], placed[i]) for i, (b, _) in enumerate(targets))
-        hit_p = sum(has(plain[b], placed[i]) for i, (b, _) in enumerate(targets))
-        at_b = sum(boosted[b][t:t + 2] == placed[i] for i, (b, t) in enumerate(targets))
-        at_p = sum(plain[b][t:t + 2] == placed[i] for i, (b, t) in enumerate(targets))
-        bias_plumb = {"wer_boosted_vs_unboosted": round(100.0 * sum(err) / max(sum(words), 1), 3),
-                      "bias_wer_unboosted_vs_boosted": round(100.0 * bd / bt, 3) if bt else 0.0,
-                      "bias_phrase_tokens_in_boosted": bt,
-                      "placed_phrases": len(placed),
-                      "placed_phrase_recall_boosted": round(hit_b / len(placed), 4) if placed else None,
-                      "placed_phrase_recall_unboosted": round(hit_p / len(placed), 4) if placed else None,
-                      "placed_at_target_step_boosted": round(at_b / len(placed), 4) if placed else None,
-                      "placed_at_target_step_unboosted": round(at_p / len(placed), 4) if placed else None,
-                      "note": "random weights: token ids as words; WER of the boosted decode against the "
-                              "lam=0 decode, bias-WER of the lam=0 decode against the boosted one over the "
-                              "whole bias list, recall of each clip's placed phrase (its lam=0 runner-up "
-                              "continuation) in that clip's decode"}
+
+        def score(lam):
+            boosted = model.generate(mel, bias_list=phrases, bias_boost=lam, **kw).cpu().tolist()
+            model.synchronize()
+            err, words = wer_counts(as_text(boosted), as_text(plain))
+            bd = bt = 0
+            for r, h in zip(as_text(boosted), as_text(plain)):   # the list's phrases: boosted vs lam = 0
+                d_, t_ = C.c_int64(), C.c_int64()
+                _lib.check(_lib.load().wcb_bias_counts((" " + r + " ").encode(), (" " + h + " ").encode(),
+                                                       _cstrs([" " + t + " " for t in ptxt]), len(ptxt),
+                                                       C.byref(d_), C.byref(t_)), None, "wcb_bias_counts")
+                bd += d_.value
+                bt += t_.value
+            has = lambda row, p: any(row[i:i + len(p)] == p for i in range(len(row) - len(p) + 1))
+            n = len(placed)
+            first_div = [next((i for i, (a, b) in enumerate(zip(x, y)) if a != b), len(x)) for x, y in zip(boosted, plain)]
+            return {"lambda": lam,
+                    "wer_boosted_vs_unboosted": round(100.0 * sum(err) / max(sum(words), 1), 3),
+                    "bias_wer_unboosted_vs_boosted": round(100.0 * bd / bt, 3) if bt else 0.0,
+                    "bias_phrase_tokens_in_boosted": bt,
+                    "median_first_divergence_step": float(np.median(first_div)),
+                    "placed_phrase_recall_boosted":
+                        round(sum(has(boosted[b], placed[i]) for i, (b, _) in enumerate(targets)) / n, 4) if n else None,
+                    "placed_phrase_recall_unboosted":
+                        round(sum(has(plain[b], placed[i]) for i, (b, _) in enumerate(targets)) / n, 4) if n else None,
+                    "placed_at_target_step_boosted":
+                        round(sum(boosted[b][t:t + 2] == placed[i] for i, (b, t) in enumerate(targets)) / n, 4) if n else None,
+                    "placed_at_target_step_unboosted":
+                        round(sum(plain[b][t:t + 2] == placed[i] for i, (b, t) in enumerate(targets)) / n, 4) if n else None}
+
+        bias_plumb = {"placed_phrases": len(placed), "bench_lambda": score(args.boost),
+                      "plumb_lambda": score(lam_plumb) if lam_plumb else None,
+                      "model_gap_quantiles_5_50_95": ([round(float(q), 4) for q in np.quantile(gaps[:, 1:], [0.05, 0.5, 0.95])]
+                                                      if gaps is not None else None),
+                      "note": "random weights: token ids as words. WER of the boosted decode against the lam=0 decode; "
+                              "bias-WER of the lam=0 decode against the boosted one over the whole bias list; recall "
+                              "of each clip's placed phrase (its lam=0 runner-up continuation at the earliest step "
+                              "whose gap lies in [0.25, 0.75) x plumb_lambda, before the pool-only boosted decode "
+                              "first diverges). The bench's lambda=2 exceeds this random model's top-1/top-2 gaps "
+                              "(quantiles above), so it flips the first steps of every clip; plumb_lambda = 2 x the "
+                              "median gap is the scale at which targeted placement is measurable."}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -63,10 +63,12 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "group_rows" n     decoder rows per layer chain (16..512)
  *   "xenc_variant" v   encoder-space kernel variant, "xvariant" v  K/V cross-attention kernel variant
  *   "flash_split" n    key ranges per (clip, head) of the beam-search cross-attention (flash kernel), 1..8
+ *   "beam_xattn" v     beam-search cross-attention: keys split over the waves of one (clip, head) workgroup
+ *                      (1: 4 waves x 2 LDS stages, 2: 2 x 4, 3: 2 x 5) or the flash kernel over key ranges (0)
  *   "ln_fold" 0/1      decode rows > 64 (16-bit): LayerNorm folded into the projection, or its own launch
  *   "merge_v" 0/1      greedy encoder-space cross-attention: range merge and W_v fused (1) or two launches
  *   "xqk" 0/1          greedy encoder-space cross-attention query: LN + q_proj + W_k,hᵀ in one launch (1) or
- *                      two decode GEMMs (0); bit-identical
+ *                      two decode GEMMs (0, default: measured faster); bit-identical
  *   "decode_contexts" n  decode contexts in flight (1..4): calls decode on n streams from n buffers
  *   "ring_kt" 1/2      decode rows > 64: 64-deep K sub-tiles per LDS-ring stage of the projection tiles
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)
@@ -172,7 +174,9 @@ int wcb_op_layernorm(int dtype, const float* x, const float* w, const float* b, 
                      void* stream);
 /* o[B][Sq][H*64] = softmax(q kᵀ) v per head (q pre-scaled), k/v [B][Sk][H*64];
  * flash=1 selects the MFMA kernel (16-bit dtypes; Sq <= 16: the few-query form of beam search), 100 the
- * MFMA kernel with 64 queries per wave, -n (Sq <= 16) the MFMA kernel over n key ranges merged in
+ * MFMA kernel with 64 queries per wave, 200 / 201 / 202 (Sq <= 16) the beam kernel (the keys of a (set,
+ * head) split over its waves, merged in the workgroup: 4 waves x 2 LDS stages, 2 x 4, 2 x 5), -n (Sq <= 16)
+ * the MFMA kernel over n key ranges merged in
  * fixed order; 0 the decode kernel; n >= 2 the decode kernel with n split-KV key chunks combined by the
  * last-arriving chunk. */
 int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H, int Sq,

@@ -245,13 +245,13 @@ def test_broadcast_blob_views_load_without_host_copy():
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 def test_fused_cross_query_is_bit_identical(dtype):
-    """Option xqk (default 1): LN + q_proj + W_k,hᵀ as one launch (k_xenc.hip xq_kq_kernel) against the
+    """Option xqk (1; default 0, measured slower): LN + q_proj + W_k,hᵀ as one launch (k_xenc.hip xq_kq_kernel) against the
     two decode GEMMs it replaces (xqk 0): identical arithmetic, so identical ids even on the diverse
     recipe, whose near-ties (gaps ~1e-3) flip on any rounding difference. 32 rows (one 32-row block)
     and 13 rows (16-row blocks), 1000-phrase boost."""
     dims = get_dims("small")
     sd = make_weights(dims, seed=0, recipe="diverse")
-    fused = WhisperCB.from_state_dict(dims, sd, dtype=dtype)
+    fused = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options={"xqk": 1})
     plain = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options={"xqk": 0})
     phrases = synth_bias_list(1000, eot=dims.eos_token_id)
     for B in (32, 13):

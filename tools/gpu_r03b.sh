@@ -11,15 +11,13 @@ db() {   # decode_bench args... (appends to decode.txt)
   tail -1 "$O/decode.txt"
 }
 if [ "${DECODE:-1}" = 1 ]; then
-  db --model small --batch 32 ${DB_EXTRA:-}
-  db --model small --batch 32 --opt xqk=0
-  db --model medium --batch 64 --beams 5 --short 4 --long 20
-  db --model medium --batch 64 --beams 5 --short 4 --long 20 --opt ln_fold=0
-  db --model large-v3 --batch 16 --beams 5 --dtype f16 --phrases 5000 --short 4 --long 20
-  db --model large-v3 --batch 16 --beams 5 --dtype f16 --phrases 5000 --short 4 --long 20 --opt ln_fold=0
+  C3A="--model medium --batch 64 --beams 5 --short 4 --long 20"
+  C5A="--model large-v3 --batch 16 --beams 5 --dtype f16 --phrases 5000 --short 4 --long 20"
+  IFS=';' read -ra DBS <<< "${DB_LIST:---model small --batch 32;--model small --batch 32 --opt xqk=0;$C3A;$C3A --opt beam_xattn=0;$C3A --opt ln_fold=0;$C5A;$C5A --opt beam_xattn=0;$C5A --opt ln_fold=0}"
+  for a in "${DBS[@]}"; do db $a; done
 fi
 if [ "${TESTS:-1}" = 1 ]; then
-  timeout -k 10 ${TT:-900} python -u -m pytest tests -m gpu -v --maxfail=8 --timeout 300 --timeout-method thread --durations=25 ${PYTEST_ARGS:-} > "$O/pytest.log" 2>&1
+  timeout -k 10 ${TT:-900} python -u -m pytest tests -m gpu -v --maxfail=8 --timeout 300 --timeout-method thread --durations=25 ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} > "$O/pytest.log" 2>&1
   rc=$?
   grep -E "FAILED|ERROR|passed|failed" "$O/pytest.log" | tail -30
   [ $rc -le 1 ] || { echo "pytest rc $rc: stopping"; tail -20 "$O/pytest.log"; exit $rc; }

@@ -334,7 +334,12 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
   constexpr int LNF_OFF = NS * STAGE > BM * (BN + 4) * 4 ? NS * STAGE : BM * (BN + 4) * 4;
   float* lnraw = reinterpret_cast<float*>(smem + LNF_OFF);
   float* lnst = lnraw + BM * (kLnfMaxK / 32) * 2;
-  if constexpr (LNF) {
+  const int nk = g.K / (BK * KT);
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) stage(p, p * BK * KT);
+  if constexpr (LNF) {   // after the prologue stages (younger: the first waits over-wait by a few
+                         // pieces of stage 1 at most; the loop's last vmcnt(0) retires them)
     const int per_row = g.rst_nb * 8 / 16;                  // 16-byte chunks per row (rst_nb float2)
     const int chunks = BM * per_row;
     for (int q0 = wave * 64; q0 < chunks; q0 += NT) {
@@ -343,11 +348,6 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
       glds16(g.rst_in + ((long)m * g.rst_nb) * 2 + j * 4, reinterpret_cast<char*>(lnraw) + (long)q0 * 16);
     }
   }
-
-  const int nk = g.K / (BK * KT);
-#pragma unroll
-  for (int p = 0; p < NS - 1; ++p)
-    if (p < nk) stage(p, p * BK * KT);
   int st = 0;
   for (int kt = 0; kt < nk; ++kt) {
     // tiles issued so far: kt .. min(nk, kt + NS - 1) - 1; keep the ones after kt in flight
@@ -395,14 +395,21 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
     }
     st = st + 1 == NS ? 0 : st + 1;
   }
-  if constexpr (LNF) {   // (μ, r) per tile row from the producer's partials, summed in column order
-    for (int r = tid; r < BM; r += NT) {
-      float a1 = 0.f, a2 = 0.f;
-      for (int j = 0; j < g.rst_nb; ++j) {
-        const float2 t = *reinterpret_cast<const float2*>(lnraw + ((long)r * g.rst_nb + j) * 2);
-        a1 += t.x;
-        a2 += t.y;
-      }
+  if constexpr (LNF) {   // (μ, r) per tile row from the producer's partials: LPR lanes per row, each a
+                         // strided subset in column order, then a fixed butterfly (deterministic)
+    __syncthreads();     // every wave's statistics pieces have landed (each waited vmcnt(0) above)
+    constexpr int LPR = NT / BM;
+    static_assert(LPR >= 1 && (LPR & (LPR - 1)) == 0 && LPR <= 64, "lanes per row");
+    const int r = tid / LPR, sub = tid % LPR;
+    float a1 = 0.f, a2 = 0.f;
+    for (int j = sub; j < g.rst_nb; j += LPR) {
+      const float2 t = *reinterpret_cast<const float2*>(lnraw + ((long)r * g.rst_nb + j) * 2);
+      a1 += t.x;
+      a2 += t.y;
+    }
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) { a1 += __shfl_xor(a1, o, 64); a2 += __shfl_xor(a2, o, 64); }
+    if (sub == 0) {
       const float mean = a1 / g.K;
       lnst[2 * r] = mean;
       lnst[2 * r + 1] = rsqrtf(fmaxf(a2 / g.K - mean * mean, 0.f) + 1e-5f);
@@ -1088,17 +1095,19 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
           (!g.ln_u || (g.K <= kLnfMaxK && g.rst_in && g.rst_nb * 32 == g.K))) {
         const int mt = (g.M + 63) / 64;
         const bool lnf = g.ln_u != nullptr;
-        const bool kt2 = g.ring_kt == 2 && g.K % 128 == 0 && !lnf;   // 128-deep stages
+        const bool kt2 = g.ring_kt == 2 && g.K % 128 == 0;           // 128-deep stages
         if (g.N % 64 == 0 && mt * (g.N / 64) >= 240) {
           // (128-deep stages measured slower here: C3 4,871 vs 4,946 audio-s/s with all three tiles)
           if (lnf) launch_ring_e<T, 64, 64, 2, 2, 4, E_RUNTIME, true>(g, s);
           else launch_ring_e<T, 64, 64, 2, 2, 4, E_RUNTIME>(g, s);
         } else if (mt * ((g.N + 31) / 32) >= 240) {
-          if (lnf) launch_ring_e<T, 64, 32, 2, 2, 6, E_RUNTIME, true>(g, s);
+          if (lnf && kt2) launch_ring_e<T, 64, 32, 2, 2, 4, E_RUNTIME, true, 2>(g, s);
+          else if (lnf) launch_ring_e<T, 64, 32, 2, 2, 6, E_RUNTIME, true>(g, s);
           else if (kt2) launch_ring_e<T, 64, 32, 2, 2, 4, E_RUNTIME, false, 2>(g, s);
           else launch_ring_e<T, 64, 32, 2, 2, 6, E_RUNTIME>(g, s);
         } else {
-          if (lnf) launch_ring_e<T, 32, 32, 2, 2, 6, E_RUNTIME, true>(g, s);
+          if (lnf && kt2) launch_ring_e<T, 32, 32, 2, 2, 4, E_RUNTIME, true, 2>(g, s);
+          else if (lnf) launch_ring_e<T, 32, 32, 2, 2, 6, E_RUNTIME, true>(g, s);
           else if (kt2) launch_ring_e<T, 32, 32, 2, 2, 4, E_RUNTIME, false, 2>(g, s);
           else launch_ring_e<T, 32, 32, 2, 2, 6, E_RUNTIME>(g, s);
         }

@@ -648,9 +648,174 @@ __global__ __launch_bounds__(64) void flash_merge_kernel(AttnArgs a) {
   reinterpret_cast<T*>(a.o)[((long)b * a.o_Sb + q) * a.ldo + h * 64 + lane] = DT<T>::fromf(O / L);
 }
 
+// attn_beam_kernel — beam-search cross-attention: the Sq <= 16 beam rows of one clip against its
+// precomputed K/V, one workgroup per (clip, head). The flash kernel above gives each of its 4 waves
+// 16 query rows of the block, so with 5 beams 3 of its 4 waves compute on padding; here the KEYS are
+// split instead: wave w streams its own contiguous 1/NWV of the clip's keys through a private LDS-DMA
+// ring (NSW stages of one 64-key K and V tile; only the issuing wave reads them, so the loop needs no
+// workgroup barrier — its own counted vmcnt orders the reads), with the 16 query slots of the clip
+// (the same swapped products and lane-local online softmax as the flash kernel). The waves' (max,
+// Σp, Σp·v) are merged in wave order through LDS at the end (deterministic); no key-range partials
+// leave the workgroup. [tf] modeling_whisper.py:284-356 (cross-attention), generation/utils.py:3208
+// (beams share the clip's encoder states).
+template <typename T, int NWV, int NSW>
+__global__ __launch_bounds__(NWV * 64) void attn_beam_kernel(AttnArgs a) {
+  using Frag = typename DT<T>::frag;
+  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  char* ring = lds_dyn + wave * NSW * 2 * 64 * 128;              // this wave's stages [NSW][K|V][64 x 128 B]
+  const int S = a.nkeys;
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const int nt_all = (S + 63) / 64, per_w = (nt_all + NWV - 1) / NWV;
+  const int t_lo = min(wave * per_w, nt_all), nt = min(nt_all, t_lo + per_w) - t_lo;
+  const T* Q = reinterpret_cast<const T*>(a.q);
+  const T* K = reinterpret_cast<const T*>(a.k) + (long)b * a.k_sb + (long)h * a.k_sh;
+  const T* V = reinterpret_cast<const T*>(a.v) + (long)b * a.k_sb + (long)h * a.k_sh;
+  Frag qf[2];
+  {
+    const int qr = min(lane & 15, a.Sq - 1);
+    const T* qp = Q + ((long)b * a.q_Sb + qr) * a.ldq + h * 64 + 8 * (lane >> 4);
+    qf[0] = load_frag<T>(qp);
+    qf[1] = load_frag<T>(qp + 32);
+  }
+  // one tile = 64 rows of K and of V, 8 x 1 KiB wave-instructions each (row r = 8i + (lane >> 3))
+  auto stage = [&](int st, int kt) {
+    char* base = ring + st * 2 * 64 * 128;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = i * 8 + (lane >> 3);
+      const int key = min((t_lo + kt) * 64 + r, S - 1);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      glds16a(K + (long)key * a.k_sk + c * 8, base + i * 1024);
+      glds16a(V + (long)key * a.k_sk + c * 8, base + 64 * 128 + i * 1024);
+    }
+  };
+  f32x4 o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float mrow = -INFINITY, lrow = 0.f;
+  const float L2E = 1.4426950408889634f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // Q retired: only LDS-DMA is counted below
+#pragma unroll
+  for (int p = 0; p < NSW - 1; ++p)
+    if (p < nt) stage(p, p);
+  int st = 0;
+  for (int kt = 0; kt < nt; ++kt) {
+    const int ahead = min(nt - 1 - kt, NSW - 2);       // younger tiles of this wave still in flight
+    if (NSW >= 5 && ahead >= 3) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+    else if (NSW >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if (NSW >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the stage read in iteration kt - 1 is free: its fragments were consumed by that iteration's MFMAs
+    if (kt + NSW - 1 < nt) stage((st + NSW - 1) % NSW, kt + NSW - 1);
+    const char* kt_l = ring + st * 2 * 64 * 128;
+    const char* vt_l = kt_l + 64 * 128;
+    st = st + 1 == NSW ? 0 : st + 1;
+    Frag kf[4][2];
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) kf[mf][ks] = *reinterpret_cast<const Frag*>(kt_l + swz(mf * 16 + (lane & 15), ks * 4 + (lane >> 4)));
+    const int kabs = (t_lo + kt) * 64;
+    f32x4 sc[4];
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf) {
+      sc[mf] = mma16(kf[mf][0], qf[0], f32x4{0.f, 0.f, 0.f, 0.f});
+      sc[mf] = mma16(kf[mf][1], qf[1], sc[mf]);
+    }
+    if (kabs + 64 > S) {
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (kabs + mf * 16 + 4 * (lane >> 4) + e >= S) sc[mf][e] = -INFINITY;
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tmax = fmaxf(tmax, sc[mf][e]);
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mnew = fmaxf(mrow, tmax);
+    const float alpha = __builtin_amdgcn_exp2f((mrow - mnew) * L2E);
+    mrow = mnew;
+    const float mb = mnew * L2E;
+    float ls = 0.f;
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { sc[mf][e] = __builtin_amdgcn_exp2f(fmaf(sc[mf][e], L2E, -mb)); ls += sc[mf][e]; }
+    lrow = lrow * alpha + ls;
+    if (__any(alpha != 1.f)) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] *= alpha;
+    }
+    const Frag p0 = pack_p<T>(sc[0], sc[1]), p1 = pack_p<T>(sc[2], sc[3]);
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf) {
+      o[mf] = mma16(tr_frag<T>(vt_l, 0, mf * 2, lane), p0, o[mf]);
+      o[mf] = mma16(tr_frag<T>(vt_l, 32, mf * 2, lane), p1, o[mf]);
+    }
+  }
+  // ---- merge the waves' partials (wave order): lane holds Oᵀ[dd = 16mf + 4(lane>>4) + e][q = lane&15]
+  lrow += __shfl_xor(lrow, 16, 64);
+  lrow += __shfl_xor(lrow, 32, 64);
+  __syncthreads();                                     // every wave is done with its ring: reuse it
+  f32x4* ob = reinterpret_cast<f32x4*>(lds_dyn);       // [NWV][4][64]
+  float2* ml = reinterpret_cast<float2*>(lds_dyn + NWV * 4 * 64 * 16);   // [NWV][16]
+#pragma unroll
+  for (int mf = 0; mf < 4; ++mf) ob[(wave * 4 + mf) * 64 + lane] = o[mf];
+  if (lane < 16) ml[wave * 16 + lane] = float2{nt > 0 ? mrow : -INFINITY, nt > 0 ? lrow : 0.f};
+  __syncthreads();
+  if (wave != 0) return;
+  const int q = lane & 15;
+  float M = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < NWV; ++w) { const float2 t = ml[w * 16 + q]; if (t.y > 0.f) M = fmaxf(M, t.x); }
+  float L = 0.f, wgt[NWV];
+#pragma unroll
+  for (int w = 0; w < NWV; ++w) {
+    const float2 t = ml[w * 16 + q];
+    wgt[w] = t.y > 0.f ? __builtin_amdgcn_exp2f((t.x - M) * L2E) : 0.f;
+    L += wgt[w] * t.y;
+  }
+  const float inv = 1.f / L;
+  if (q >= a.Sq) return;
+  T* op = reinterpret_cast<T*>(a.o) + ((long)b * a.o_Sb + q) * a.ldo + h * 64 + 4 * (lane >> 4);
+#pragma unroll
+  for (int mf = 0; mf < 4; ++mf) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) acc += wgt[w] * ob[(w * 4 + mf) * 64 + lane];
+    typedef short s4 __attribute__((ext_vector_type(4)));
+    s4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = __builtin_bit_cast(short, DT<T>::fromf(acc[e] * inv));
+    *reinterpret_cast<s4*>(op + mf * 16) = v;
+  }
+}
+
+template <typename T, int NWV, int NSW>
+static void launch_beam(const AttnArgs& a, hipStream_t s) {
+  constexpr int lds = NWV * NSW * 2 * 64 * 128;
+  static_assert(lds >= NWV * 4 * 64 * 16 + NWV * 16 * 8 && lds <= 160 * 1024, "LDS budget");
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)attn_beam_kernel<T, NWV, NSW>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr_set = true;
+  }
+  WCB_LAUNCH((attn_beam_kernel<T, NWV, NSW>), dim3(a.B * a.H), dim3(NWV * 64), lds, s, a);
+}
+
 template <typename T>
 static void launch_flash(const AttnArgs& a, hipStream_t s) {
-  if (a.Sq <= 16) {   // a few query rows per K/V set (the beams of one clip): 16 queries per wave
+  if (a.Sq <= 16 && a.variant >= 7 && a.variant <= 9) {   // beam rows of a clip, keys split over the waves
+    // 7: 4 waves x 2 stages, 8: 2 waves x 4 stages, 9: 2 waves x 5 stages (128 / 128 / 160 KiB of LDS)
+    if (a.variant == 7) launch_beam<T, 4, 2>(a, s);
+    else if (a.variant == 8) launch_beam<T, 2, 4>(a, s);
+    else launch_beam<T, 2, 5>(a, s);
+  } else if (a.Sq <= 16) {   // a few query rows per K/V set (the beams of one clip): 16 queries per wave
     const int ns = (a.part && a.nsplit > 1) ? a.nsplit : 1;
     AttnArgs b = a;
     b.nsplit = ns;

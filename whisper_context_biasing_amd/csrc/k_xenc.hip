@@ -517,37 +517,39 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
 }
 
 // xq_kq_kernel: workgroup = (column block cb of CB columns of q'_h, head h, row block of 16·MF rows),
-// 4 waves. Phase 1 is the LN-fused q_proj decode GEMM of gemm_dec_kernel (AM = 2) restricted to the
-// head's 64 columns, with its exact arithmetic: the K range split over the 4 waves (KPW 32-deep steps
-// each, the same split as the decode-GEMM table for K = D), row statistics from the loaded 16-bit
-// residual copy (per-wave partials summed in wave order), γ/β through LDS, wave partials summed in
-// wave order, + b_q, rounded to T. Phase 2 is the grouped W_k,hᵀ product of the decode GEMM with
-// K = 64 (two 32-deep MFMA steps summed after the fact, as its two waves do). Every load of the launch
-// (the head's W_q rows, the W_kt block, the residual rows, LN parameters, b_q) is issued up front.
-// The head's W_q rows are read by the D/CB workgroups of that head (L2 / Infinity Cache after the
-// first): redundant reads bought with one dependent launch fewer per decoder layer.
+// 8 waves = 4 K slices x 2 column pairs. Phase 1 is the LN-fused q_proj decode GEMM of gemm_dec_kernel
+// (AM = 2) restricted to the head's 64 columns, with its exact arithmetic: the K range split into the
+// same 4 slices (KPW 32-deep steps each, the decode-GEMM table for K = D), row statistics from the
+// loaded 16-bit residual copy (per-slice partials summed in slice order), γ/β through LDS, slice
+// partials summed in slice order, + b_q, rounded to T. Phase 2 is the grouped W_k,hᵀ product of the
+// decode GEMM with K = 64 (two 32-deep MFMA steps summed after the fact, as its two waves do). Every
+// load of the launch (the head's W_q rows, the W_kt block, the residual rows, LN parameters, b_q) is
+// issued up front; the head's 98 KB of W_q rows are spread over 8 waves (loads in flight) and read by
+// the D/CB workgroups of that head (L2 / Infinity Cache after the first): redundant reads bought with
+// one dependent launch fewer per decoder layer.
 template <typename T, int D, int MF>
-__global__ __launch_bounds__(256) void xq_kq_kernel(XqkArgs a) {
+__global__ __launch_bounds__(512) void xq_kq_kernel(XqkArgs a) {
   using Frag = typename DT<T>::frag;
-  constexpr int NW = 4, KPW = D / 128, R = MF * 16, CB = 64;
-  __shared__ __attribute__((aligned(16))) float red[NW][R][65];
+  constexpr int NS = 4, KPW = D / 128, R = MF * 16, CB = 64, NT = 512;
+  __shared__ __attribute__((aligned(16))) float red[NS][R][65];
   __shared__ __attribute__((aligned(16))) float lnp[2 * D];
-  __shared__ float2 rst[NW][R];
+  __shared__ float2 rst[NS][R];
   __shared__ __attribute__((aligned(16))) T qh[R][64 + 8];     // q_h rows (T), the phase-2 A operand
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ks_w = wave & 3, jp = wave >> 2;                     // K slice, column pair (frags 2jp, 2jp+1)
   const int cb = blockIdx.x, h = blockIdx.y, mb = blockIdx.z * R;
-  const int kb = wave * (KPW * 32) + 8 * (lane >> 4);
+  const int kb = ks_w * (KPW * 32) + 8 * (lane >> 4);
   // ---- every load of the launch
-  Frag w[4][KPW];                                   // W_q rows h·64 + 16j + (lane & 15)
+  Frag w[2][KPW];                                   // W_q rows h·64 + 16(2jp + j) + (lane & 15)
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const T* W = reinterpret_cast<const T*>(a.wq) + (long)(h * 64 + j * 16 + (lane & 15)) * D + kb;
+  for (int j = 0; j < 2; ++j) {
+    const T* W = reinterpret_cast<const T*>(a.wq) + (long)(h * 64 + (2 * jp + j) * 16 + (lane & 15)) * D + kb;
 #pragma unroll
-    for (int ks = 0; ks < KPW; ++ks) w[j][ks] = __builtin_nontemporal_load(reinterpret_cast<const Frag*>(W + ks * 32));
+    for (int ks = 0; ks < KPW; ++ks) w[j][ks] = load_frag<T>(W + ks * 32);   // default policy: re-read by the head's D/64 workgroups
   }
-  Frag wk[2];                                       // W_kt[h][cb·CB + 16·wave + (lane & 15)][k]
+  Frag wk[2];                                       // waves 0-3: W_kt[h][cb·CB + 16·wave + (lane & 15)][k]
   {
-    const T* Wk = reinterpret_cast<const T*>(a.wkt) + ((long)h * D + cb * CB + wave * 16 + (lane & 15)) * 64 + 8 * (lane >> 4);
+    const T* Wk = reinterpret_cast<const T*>(a.wkt) + ((long)h * D + cb * CB + ks_w * 16 + (lane & 15)) * 64 + 8 * (lane >> 4);
     wk[0] = load_frag<T>(Wk);
     wk[1] = load_frag<T>(Wk + 32);
   }
@@ -559,55 +561,57 @@ __global__ __launch_bounds__(256) void xq_kq_kernel(XqkArgs a) {
 #pragma unroll
     for (int ks = 0; ks < KPW; ++ks) x[i][ks] = load_frag<T>(xr + ks * 32);
   }
-  constexpr int LQ = (2 * D / 4 + 255) / 256;
+  constexpr int LQ = (2 * D / 4 + NT - 1) / NT;
   f32x4 lq[LQ];
 #pragma unroll
   for (int j = 0; j < LQ; ++j) {
-    const int c = (j * 256 + tid) * 4;
+    const int c = (j * NT + tid) * 4;
     lq[j] = c < 2 * D ? *reinterpret_cast<const f32x4*>((c < D ? a.ln_w : a.ln_b) + (c < D ? c : c - D))
                       : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  constexpr int EP = (R * 64 + 255) / 256;          // phase-1 outputs per thread
+  constexpr int EP = (R * 64 + NT - 1) / NT;        // phase-1 outputs per thread
   float pf_bias[EP];
 #pragma unroll
-  for (int it = 0; it < EP; ++it) pf_bias[it] = a.bq[h * 64 + ((it * 256 + tid) & 63)];
+  for (int it = 0; it < EP; ++it) pf_bias[it] = a.bq[h * 64 + ((it * NT + tid) & 63)];
   __builtin_amdgcn_sched_barrier(0);
-  // ---- LayerNorm of the rows (gemm_dec_kernel AM = 2 arithmetic)
-  float xv[MF][KPW][8];
+  // ---- LayerNorm of the rows (gemm_dec_kernel AM = 2 arithmetic; slice partials from the jp = 0 waves)
+  auto xval = [&](int i, int ks, int e) -> float {
+    if constexpr (__is_same(T, bf16_t)) return bf16_to_f((bf16_t)x[i][ks][e]);
+    else return float(x[i][ks][e]);
+  };
+  if (jp == 0) {
 #pragma unroll
-  for (int i = 0; i < MF; ++i) {
-    float s1 = 0.f, s2 = 0.f;
+    for (int i = 0; i < MF; ++i) {
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int ks = 0; ks < KPW; ++ks)
+      for (int ks = 0; ks < KPW; ++ks)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float v;
-        if constexpr (__is_same(T, bf16_t)) v = bf16_to_f((bf16_t)x[i][ks][e]);
-        else v = float(x[i][ks][e]);
-        xv[i][ks][e] = v;
-        s1 += v;
-        s2 = fmaf(v, v, s2);
-      }
-    s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
-    s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
-    if (lane < 16) rst[wave][i * 16 + lane] = float2{s1, s2};
+        for (int e = 0; e < 8; ++e) {
+          const float v = xval(i, ks, e);
+          s1 += v;
+          s2 = fmaf(v, v, s2);
+        }
+      s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
+      if (lane < 16) rst[ks_w][i * 16 + lane] = float2{s1, s2};
+    }
   }
 #pragma unroll
   for (int j = 0; j < LQ; ++j) {
-    const int c = (j * 256 + tid) * 4;
+    const int c = (j * NT + tid) * 4;
     if (c < 2 * D) *reinterpret_cast<f32x4*>(lnp + c) = lq[j];
   }
   __syncthreads();
-  f32x4 acc[MF][4];
+  f32x4 acc[MF][2];
 #pragma unroll
   for (int i = 0; i < MF; ++i) {
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < NW; ++ww) { const float2 t = rst[ww][i * 16 + (lane & 15)]; s1 += t.x; s2 += t.y; }
+    for (int ww = 0; ww < NS; ++ww) { const float2 t = rst[ww][i * 16 + (lane & 15)]; s1 += t.x; s2 += t.y; }
     const float mean = s1 / D;
     const float rstd = rsqrtf(fmaxf(s2 / D - mean * mean, 0.f) + 1e-5f);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KPW; ++ks) {
       const f32x4 w0 = *reinterpret_cast<const f32x4*>(lnp + kb + ks * 32);
@@ -618,33 +622,35 @@ __global__ __launch_bounds__(256) void xq_kq_kernel(XqkArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float gw = e < 4 ? w0[e] : w1[e - 4], gb = e < 4 ? b0[e] : b1[e - 4];
-        const float v = (xv[i][ks][e] - mean) * rstd * gw + gb;
+        const float v = (xval(i, ks, e) - mean) * rstd * gw + gb;
         af[e] = __builtin_bit_cast(typename std::remove_reference<decltype(af[0])>::type, DT<T>::fromf(v));
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mma16(af, w[j][ks], acc[i][j]);
+      acc[i][0] = mma16(af, w[0][ks], acc[i][0]);
+      acc[i][1] = mma16(af, w[1][ks], acc[i][1]);
     }
   }
-  // ---- wave partials → LDS, summed in wave order + b_q, rounded to T: q_h
+  // ---- slice partials → LDS, summed in slice order + b_q, rounded to T: q_h
 #pragma unroll
   for (int i = 0; i < MF; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) red[wave][i * 16 + (lane >> 4) * 4 + e][j * 16 + (lane & 15)] = acc[i][j][e];
+      for (int e = 0; e < 4; ++e)
+        red[ks_w][i * 16 + (lane >> 4) * 4 + e][(2 * jp + j) * 16 + (lane & 15)] = acc[i][j][e];
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < EP; ++it) {
-    const int o = it * 256 + tid;
+    const int o = it * NT + tid;
     if (o < R * 64) {
       const int r = o >> 6, c = o & 63;
       float v = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < NW; ++ww) v += red[ww][r][c];
+      for (int ww = 0; ww < NS; ++ww) v += red[ww][r][c];
       qh[r][c] = DT<T>::fromf(v + pf_bias[it]);
     }
   }
   __syncthreads();
+  if (wave >= 4) return;
   // ---- phase 2: q'_h[m][c] = Σ_i q_h[m][i] W_kt[h][c][i], wave → 16 columns of the block
 #pragma unroll
   for (int i = 0; i < MF; ++i) {
@@ -668,8 +674,8 @@ bool xqk_supported(DType t, int D) {
 template <typename T, int D>
 static void launch_xqk(const XqkArgs& a, hipStream_t s) {
   // 16 rows per workgroup up to 16 rows, else 32 (more rows per W_q read; C2's 32 rows: one row block)
-  if (a.M <= 16) WCB_LAUNCH((xq_kq_kernel<T, D, 1>), dim3(D / 64, a.H, 1), dim3(256), 0, s, a);
-  else WCB_LAUNCH((xq_kq_kernel<T, D, 2>), dim3(D / 64, a.H, (a.M + 31) / 32), dim3(256), 0, s, a);
+  if (a.M <= 16) WCB_LAUNCH((xq_kq_kernel<T, D, 1>), dim3(D / 64, a.H, 1), dim3(512), 0, s, a);
+  else WCB_LAUNCH((xq_kq_kernel<T, D, 2>), dim3(D / 64, a.H, (a.M + 31) / 32), dim3(512), 0, s, a);
 }
 
 template <typename T>

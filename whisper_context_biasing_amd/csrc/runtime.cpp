@@ -162,6 +162,10 @@ struct wcb_handle {
   // per (clip, head), merged by flash_merge_kernel. Fixed per handle (never from the batch). Measured
   // (audio-s/s, splits 1 / 2 / 4): C3 4491 / 4531 / 4452, C5 1405 / 1484 / 1485.
   int flash_split = 2;
+  // the same with the clip's keys split over the 4 waves of one (clip, head) workgroup, merged in the
+  // workgroup (option "beam_xattn" 1, default; 0 = the flash kernel above, whose 4 waves split 16-query
+  // blocks — with 5 beams three of them compute on padding)
+  int beam_xattn = 1;
   // decode rows > 64 (16-bit): pre-block LayerNorms folded into the ring-tile projections (option
   // "ln_fold" 1: γ folded into the weights, (μ, r) from the residual writers' per-32-column partial
   // sums, applied in the epilogue — no per-element work in the K loop, no LayerNorm launch) or a
@@ -173,7 +177,7 @@ struct wcb_handle {
   int merge_v = 1;
   // greedy cross-attention query (<= 64 rows, encoder space): LN + q_proj + W_k,hᵀ as one launch
   // (option "xqk"; 0 = the two decode GEMMs, bit-identical)
-  int xqk = 1;
+  int xqk = 0;   // measured (C2 decode alone): 0.53-0.61 ms/token unfused vs 0.67-0.69 fused
   // decode rows > 64: 64-deep K sub-tiles per ring stage of the 64x32 / 32x32 tiles (option "ring_kt",
   // 1 or 2; C5 1,594 -> 1,644 audio-s/s)
   int ring_kt = 2;
@@ -548,6 +552,9 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       h->merge_v = value != 0;
     } else if (n == "ln_fold") {
       h->ln_fold = value != 0;
+    } else if (n == "beam_xattn") {
+      REQUIRE(value >= 0 && value <= 3, "option beam_xattn: 0..3");
+      h->beam_xattn = value;
     } else if (n == "flash_split") {
       REQUIRE(value >= 1 && value <= kXSplit, "option flash_split: 1..8");
       h->flash_split = value;
@@ -1130,6 +1137,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
         xa.q_Sb = G; xa.Sq = G; xa.o_Sb = G; xa.B = M / G; xa.row0 = 0; xa.b_div = 1;
         xa.nsplit = h->flash_split; xa.ticket = nullptr;
         xa.part = D.xpart.as<float>() + (size_t)r0 * H * kXSplit * 66;
+        if (h->beam_xattn && G <= 16) xa.variant = 6 + h->beam_xattn;   // keys split over the waves (attn_beam_kernel)
       }
       h->timed("dec_xattn", 4.0 * M * H * (double)S * 64, (double)nb / c.nb * H * S * 128.0 * e, st_, [&] {
         if (!grouped || !attention_flash(h->dt, xa, st_)) attention_decode(h->dt, xa, st_);
@@ -1845,9 +1853,12 @@ int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, voi
     a.q = q; a.ldq = ld; a.q_Sb = Sq; a.Sq = Sq;
     a.k = k; a.v = v; a.k_sb = (long)Sk * ld; a.k_sh = 64; a.k_sk = ld;
     a.o = o; a.ldo = ld; a.o_Sb = Sq; a.B = B; a.H = H; a.nkeys = Sk;
-    if (flash == 1 || flash == 100 || flash < 0) {
-      // 100: 64 queries per wave; -n: n key ranges + merge (Sq <= 16)
-      a.variant = flash == 100 ? 4 : 1;
+    const bool beam = flash >= 200 && flash <= 202;
+    if (flash == 1 || flash == 100 || beam || flash < 0) {
+      // 100: 64 queries per wave; 200 / 201 / 202: the beam kernel (keys split over the waves, Sq <= 16;
+      // 4 waves x 2 stages, 2 x 4, 2 x 5); -n: n key ranges + merge (Sq <= 16)
+      a.variant = flash == 100 ? 4 : beam ? 7 + (flash - 200) : 1;
+      REQUIRE(!beam || Sq <= 16, "the beam kernel takes at most 16 query rows per set");
       REQUIRE(dtype != WCB_F32, "flash attention needs a 16-bit dtype");
       static DevBuf fpart;
       if (flash < 0) {

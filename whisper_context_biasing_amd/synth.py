@@ -84,16 +84,19 @@ def synth_bias_list(n: int, eot: int, seed: int = 7) -> List[List[int]]:
     return [phrase_token_ids(p, eot) for p in sample_bias_phrases(n, seed)]
 
 
-def runner_up_phrases(model, mel, n_tokens: int, lam: float, word_start=None, band=(0.25, 0.75)):
+def runner_up_phrases(model, mel, n_tokens: int, lam: float, word_start=None, band=(0.25, 0.75), pool=None):
     """Bias phrases the boost can actually place (the bench's biased-WER workload): for every clip, the
     EARLIEST step (first step excluded) of the lam = 0 greedy decode whose top-1/top-2 logit gap lies
     in the band [band[0]·lam, band[1]·lam) — below lam, so one boost unit lifts the runner-up r over
-    the top-1; well above the 16-bit noise between the prefill and decode paths, so r is not the decode
-    path's own choice at lam = 0 — whose runner-up may start a match (`word_start`), and where the
-    teacher-forced top-1 is the decode's own token (the two paths agree on the step). The phrase is
-    [r, n] with n the greedy token after r (the decode teacher-forced through r). Returns
-    (plain_ids [B, n_tokens] int64, phrases, targets) with targets[i] = (clip, step) of phrase i.
-    Runs on the GPU through the model's own generate / forward; untimed setup."""
+    the top-1; above the 16-bit noise between the prefill and decode paths, so r is not the decode
+    path's own choice at lam = 0 — whose runner-up may start a match (`word_start`), where the
+    teacher-forced top-1 is the decode's own token (the two paths agree on the step), and — given the
+    rest of the bias list `pool` — before the step where the decode boosted with `pool` alone first
+    leaves the lam = 0 decode (a target after that point would be scored on a different prefix). The
+    phrase is [r, n] with n the greedy token after r (the decode teacher-forced through r).
+    Returns (plain_ids [B, n_tokens] int64, phrases, targets, gaps) with targets[i] = (clip, step) of
+    phrase i and gaps the [B, n_tokens] top-1/top-2 gaps (numpy). Untimed setup on the GPU through the
+    model's own generate / forward."""
     import torch
 
     dims = model.dims
@@ -110,6 +113,11 @@ def runner_up_phrases(model, mel, n_tokens: int, lam: float, word_start=None, ba
         ok &= torch.as_tensor(np.asarray(word_start, dtype=bool), device=ru.device)[ru]
     T = gap.shape[1]
     steps = torch.arange(T, device=gap.device)[None, :].expand(B, T)
+    if pool:
+        boosted = model.generate(mel, max_length=n_tokens, min_new_tokens=n_tokens, bias_list=pool, bias_boost=lam)
+        diff = boosted[:, :T] != plain[:, :T]
+        derail = torch.where(diff, steps, torch.full_like(steps, T)).min(dim=1).values
+        ok &= steps < derail[:, None]
     t = torch.where(ok, steps, torch.full_like(steps, T)).min(dim=1).values.clamp(max=T - 1)   # earliest
     keep = ok.gather(1, t[:, None])[:, 0]
     r = ru.gather(1, t[:, None])[:, 0]
@@ -122,4 +130,4 @@ def runner_up_phrases(model, mel, n_tokens: int, lam: float, word_start=None, ba
         if bool(keep[b]):
             phrases.append([int(r[b]), int(n1[b])])
             targets.append((b, int(t[b])))
-    return plain.cpu().numpy().astype(np.int64), phrases, targets
+    return plain.cpu().numpy().astype(np.int64), phrases, targets, gap.cpu().numpy()
