@@ -139,7 +139,7 @@ def test_flash_attention_query_groups(dt, B, H, Sq, Sk, split):
     q = (torch.randn(B, Sq, H * 64, generator=g) * 0.3).to(DT[dt][0]).cuda()
     k = torch.randn(B, Sk, H * 64, generator=g).to(DT[dt][0]).cuda()
     v = torch.randn(B, Sk, H * 64, generator=g).to(DT[dt][0]).cuda()
-    code = {"beam": 200, "beam8": 201, "beam9": 202}.get(split, 1 if split == 1 else -split)
+    code = {"beam": 200, "beam8": 201, "beam9": 202}[split] if isinstance(split, str) else (1 if split == 1 else -split)
     if str(split).startswith("beam") and Sq > 16:
         pytest.skip("the beam kernel takes <= 16 queries")
     o = _attn(dt, q, k, v, code)

@@ -163,9 +163,10 @@ struct wcb_handle {
   // (audio-s/s, splits 1 / 2 / 4): C3 4491 / 4531 / 4452, C5 1405 / 1484 / 1485.
   int flash_split = 2;
   // the same with the clip's keys split over the 4 waves of one (clip, head) workgroup, merged in the
-  // workgroup (option "beam_xattn" 1, default; 0 = the flash kernel above, whose 4 waves split 16-query
-  // blocks — with 5 beams three of them compute on padding)
-  int beam_xattn = 1;
+  // workgroup (option "beam_xattn" 1..3; 0, default = the flash kernel above, whose 4 waves split
+  // 16-query blocks — with 5 beams three of them compute on padding, yet it measured as fast: the
+  // launch streams 393 MB of K/V per layer at C3, ~5.3 TB/s, bandwidth- not compute-bound)
+  int beam_xattn = 0;   // measured: C3 4.37 / 4.41 ms/token (1 / 0), C5 3.60 / 3.49: within noise / worse
   // decode rows > 64 (16-bit): pre-block LayerNorms folded into the ring-tile projections (option
   // "ln_fold" 1: γ folded into the weights, (μ, r) from the residual writers' per-32-column partial
   // sums, applied in the epilogue — no per-element work in the K loop, no LayerNorm launch) or a
