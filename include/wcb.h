@@ -69,6 +69,8 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "merge_v" 0/1      greedy encoder-space cross-attention: range merge and W_v fused (1) or two launches
  *   "xqk" 0/1          greedy encoder-space cross-attention query: LN + q_proj + W_k,hᵀ in one launch (1) or
  *                      two decode GEMMs (0, default: measured faster); bit-identical
+ *   "lean" 0/1         decode projections of <= 64 rows (16-bit) on the lean single-tile kernel (1, default)
+ *                      or the general decode GEMM (0); bit-identical
  *   "decode_contexts" n  decode contexts in flight (1..4): calls decode on n streams from n buffers
  *   "ring_kt" 1/2      decode rows > 64: 64-deep K sub-tiles per LDS-ring stage of the projection tiles
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)
@@ -183,7 +185,8 @@ int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, voi
                      int Sk, int flash, void* stream);
 /* decode attention in the runtime's layout: q/o [B][H*64], K/V head-major [B][H][Sk][64]; one query
  * per (row, head), nsplit key chunks (split-KV), kernel variant (k_attn.hip launch_decode; 6 = the
- * one-token self-attention kernel, nsplit 1). */
+ * one-token self-attention kernel, nsplit 1; 7 = the same with the key count read on the device, as the
+ * decode step runs it: the lean form for 16-bit). */
 int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void* v, void* o, int B, int H,
                             int Sk, int nsplit, int variant, void* stream);
 

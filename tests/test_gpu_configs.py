@@ -286,3 +286,21 @@ def test_forward_teacher_forcing_is_one_prefill_pass_per_chunk():
     h = om.decode_tokens(dec, 0, {}, om.cross_kv(enc))
     ref = om.lm_head(h)
     np.testing.assert_allclose(got, ref, atol=2e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("size,dtype,B", [("small", "bf16", 32), ("medium", "f16", 8), ("large-v3", "f16", 4)])
+def test_lean_decode_projections_bit_identical(size, dtype, B):
+    """dec_lean_kernel (option "lean", default) against gemm_dec_kernel on the same greedy decode with the
+    1000-phrase boost: every decode projection of <= 64 rows (QKV with the KV append, out / xo / fc2
+    residual writers, LN-fused xq / fc1, grouped W_k,hᵀ) has the same K split and sum order, so the ids
+    must be identical (d = 768 / 1024 / 1280 tables)."""
+    dims = get_dims(size)
+    sd = weights(size, 0, "diverse")
+    x = mel_of(dims, B)
+    phrases = synth_bias_list(1000, eot=dims.eos_token_id)
+    out = []
+    for lean in (1, 0):
+        m = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options={"lean": lean})
+        out.append(m.generate(x, max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0).cpu().numpy())
+        del m
+    assert np.array_equal(out[0], out[1]), np.argwhere(out[0] != out[1])[:8]

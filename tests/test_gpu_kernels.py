@@ -281,7 +281,7 @@ def test_gemm_ring_encoder_shapes(dt, M, N, K, act, resid):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f32"])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("Sk,split", [(1500, 1), (1500, 4), (37, 1), (1, 3), (64, 1), (65, 1), (200, 1)])
 def test_decode_attention_variants(dt, variant, Sk, split):
     """Every cross-attention kernel variant in the runtime's head-major K/V layout, with and without
@@ -300,6 +300,12 @@ def test_decode_attention_variants(dt, variant, Sk, split):
     ref = (p @ v.double()).view(B, H * 64)
     tol = 1e-5 if dt == "f32" else 1e-2
     assert (o.double() - ref).abs().max().item() < tol
+    if variant == 7 and split == 1 and dt == "bf16":   # the lean one-token kernel: bit-identical to variant 6
+        o6 = torch.empty_like(q)
+        _lib.check(lib.wcb_op_attention_decode(DT[dt][1], q.data_ptr(), k.data_ptr(), v.data_ptr(), o6.data_ptr(), B, H,
+                                               Sk, split, 6, _s()), None, "attention_decode")
+        torch.cuda.synchronize()
+        assert torch.equal(o, o6)
 
 
 @pytest.mark.parametrize("n_mel", [80, 128])

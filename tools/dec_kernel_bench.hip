@@ -1,0 +1,187 @@
+// Decode-projection launch cost on MI355X: the library's own gemm_dec_kernel instances (gemm_impl.h)
+// at the C2 shapes (whisper-small, 32 rows), each replayed as a hipGraph chain of 100 dependent
+// launches with the weights rotating over 1 GiB (cold, as in the decode step), against a bare
+// stream kernel moving the same bytes. Prints µs per launch (gap included).
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I whisper_context_biasing_amd/csrc tools/dec_kernel_bench.hip -o tools/dec_kernel_bench
+#include "gemm_impl.h"
+
+#include <functional>
+
+#define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+using namespace wcb;
+
+double time_graph(int n, const std::function<void(int, hipStream_t)>& launch) {
+  hipStream_t s;
+  CHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipGraph_t g;
+  hipGraphExec_t ge;
+  CHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  for (int i = 0; i < n; ++i) launch(i, s);
+  CHK(hipStreamEndCapture(s, &g));
+  CHK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  for (int w = 0; w < 3; ++w) CHK(hipGraphLaunch(ge, s));
+  CHK(hipStreamSynchronize(s));
+  hipEvent_t a, b;
+  CHK(hipEventCreate(&a));
+  CHK(hipEventCreate(&b));
+  const int reps = 10;
+  CHK(hipEventRecord(a, s));
+  for (int r = 0; r < reps; ++r) CHK(hipGraphLaunch(ge, s));
+  CHK(hipEventRecord(b, s));
+  CHK(hipEventSynchronize(b));
+  float ms = 0;
+  CHK(hipEventElapsedTime(&ms, a, b));
+  CHK(hipGraphExecDestroy(ge));
+  CHK(hipGraphDestroy(g));
+  CHK(hipStreamDestroy(s));
+  return ms * 1e3 / (reps * n);
+}
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+template <int NT, int WPL, int APL>
+__global__ __launch_bounds__(NT) void k_stream(const f4* __restrict__ w, long w_stride_wg, const f4* __restrict__ act_in,
+                                               long act_elems, f4* __restrict__ act_out) {
+  const int tid = threadIdx.x;
+  const f4* wp = w + blockIdx.x * w_stride_wg + tid;
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  f4 wv[WPL > 0 ? WPL : 1];
+#pragma unroll
+  for (int i = 0; i < WPL; ++i) wv[i] = __builtin_nontemporal_load(wp + i * NT);
+  f4 av[APL > 0 ? APL : 1];
+#pragma unroll
+  for (int i = 0; i < APL; ++i) av[i] = act_in[(blockIdx.x * 64 + tid + i * NT) % act_elems];
+#pragma unroll
+  for (int i = 0; i < WPL; ++i) acc += wv[i];
+#pragma unroll
+  for (int i = 0; i < APL; ++i) acc += av[i];
+  if (tid < 64) act_out[(blockIdx.x * 64 + tid) % act_elems] = acc;
+}
+
+char* g_w;
+const size_t kW = (size_t)1 << 30;
+float *g_x, *g_bias, *g_lnw, *g_lnb;
+bf16_t *g_x16, *g_a, *g_out, *g_kv;
+int* g_pos;
+
+GemmArgs base(int N, int K, long wsz) {
+  GemmArgs g;
+  g.M = 32; g.N = N; g.K = K; g.ldw = K; g.lda = K; g.ldc = N;
+  (void)wsz;
+  return g;
+}
+
+template <int MF, int NW, int KPW, int AM>
+void run(const char* name, GemmArgs g0, int gx) {
+  const long wbytes = (long)g0.N * g0.K * 2;
+  const long nreg = (long)(kW / wbytes);
+  const int gy = (g0.M + MF * 16 - 1) / (MF * 16);
+  double us = time_graph(100, [&](int i, hipStream_t s) {
+    GemmArgs g = g0;
+    g.W = g_w + (i % nreg) * wbytes;
+    hipLaunchKernelGGL((gemm_dec_kernel<bf16_t, MF, NW, KPW, AM, false>), dim3(gx, gy), dim3(NW * 64), 0, s, g);
+  });
+  printf("%-40s MF=%d NW=%2d KPW=%2d AM=%d grid=%4dx%d: %6.2f us/launch\n", name, MF, NW, KPW, AM, gx, gy, us);
+  fflush(stdout);
+}
+
+void run_lean(const char* name, GemmArgs g0) {
+  const long wbytes = (long)g0.N * g0.K * 2;
+  const long nreg = (long)(kW / wbytes);
+  bool ok = true;
+  double us = time_graph(100, [&](int i, hipStream_t s) {
+    GemmArgs g = g0;
+    g.W = g_w + (i % nreg) * wbytes;
+    ok &= launch_lean<bf16_t>(g, s);
+  });
+  printf("%-40s lean%s: %6.2f us/launch\n", name, ok ? "" : " (NOT TAKEN)", us);
+  fflush(stdout);
+}
+
+template <int NT, int WPL, int APL>
+void run_stream(const char* name, int grid) {
+  const long per_wg = (long)NT * WPL, per_launch = per_wg * grid;
+  const long nreg = (long)(kW / 16) / per_launch;
+  const long act_elems = 98304 / 16;
+  double us = time_graph(100, [&](int i, hipStream_t s) {
+    const f4* w = reinterpret_cast<const f4*>(g_w) + (i % nreg) * per_launch;
+    f4* in = reinterpret_cast<f4*>(g_x) + (i & 1) * act_elems;
+    f4* out = reinterpret_cast<f4*>(g_x) + ((i + 1) & 1) * act_elems;
+    hipLaunchKernelGGL((k_stream<NT, WPL, APL>), dim3(grid), dim3(NT), 0, s, w, per_wg, in, act_elems, out);
+  });
+  printf("%-40s NT=%d W/wg=%5.1f KB A/wg=%5.1f KB grid=%4d: %6.2f us/launch\n", name, NT, WPL * NT * 16 / 1024.0,
+         APL * NT * 16 / 1024.0, grid, us);
+  fflush(stdout);
+}
+
+int main() {
+  CHK(hipSetDevice(0));
+  CHK(hipMalloc(&g_w, kW));
+  CHK(hipMemset(g_w, 0, kW));
+  CHK(hipMalloc(&g_x, 4 << 20));
+  CHK(hipMemset(g_x, 0, 4 << 20));
+  CHK(hipMalloc(&g_x16, 4 << 20));
+  CHK(hipMemset(g_x16, 0, 4 << 20));
+  CHK(hipMalloc(&g_a, 4 << 20));
+  CHK(hipMemset(g_a, 0, 4 << 20));
+  CHK(hipMalloc(&g_out, 4 << 20));
+  CHK(hipMalloc(&g_kv, 64 << 20));
+  CHK(hipMalloc(&g_bias, 1 << 16));
+  CHK(hipMemset(g_bias, 0, 1 << 16));
+  CHK(hipMalloc(&g_lnw, 1 << 16));
+  CHK(hipMemset(g_lnw, 0, 1 << 16));
+  CHK(hipMalloc(&g_lnb, 1 << 16));
+  CHK(hipMemset(g_lnb, 0, 1 << 16));
+  CHK(hipMalloc(&g_pos, 64));
+  CHK(hipMemset(g_pos, 0, 64));
+
+  // reference points: empty-ish and byte-matched stream kernels
+  run_stream<256, 0, 0>("stream: nothing", 96);
+  run_stream<256, 6, 6>("stream: out-proj bytes", 96);
+  run_stream<256, 6, 6>("stream: out-proj bytes, 192 wgs", 192);
+
+  // out / xo projection: A = T rows, bias, residual f32 in place, 16-bit copy
+  GemmArgs o = base(768, 768, 0);
+  o.A = g_a; o.bias = g_bias; o.resid = g_x; o.out = g_x; o.out_f32 = 1; o.out16 = g_x16;
+  run<1, 4, 6, 0>("out: bias+resid+f32+x16 (library)", o, 48);
+  run_lean("out", o);
+  run<2, 4, 6, 0>("out: MF=2", o, 48);
+  run<1, 8, 3, 0>("out: NW=8", o, 48);
+  run<2, 8, 3, 0>("out: MF=2 NW=8", o, 48);
+  GemmArgs o2 = o; o2.out16 = nullptr;
+  run<1, 4, 6, 0>("out: no x16", o2, 48);
+  GemmArgs o3 = o; o3.resid = nullptr; o3.out16 = nullptr; o3.out_f32 = 0; o3.out = g_out; o3.bias = nullptr;
+  run<1, 4, 6, 0>("out: plain T out", o3, 48);
+  // LN-fused projections (A = LN of the 16-bit residual copy)
+  GemmArgs q = base(2304, 768, 0);
+  q.ln_w = g_lnw; q.ln_b = g_lnb; q.ln_a16 = g_x16; q.A = g_x; q.lda = 768; q.bias = g_bias;
+  q.out = g_out; q.mode = 2; q.n_split = 768; q.kv_out = g_kv; q.hs_B = 32; q.hs_H = 12; q.kv_T = 80; q.pos = g_pos;
+  run<1, 4, 6, 2>("qkv: LN16 + kv append (library)", q, 144);
+  run_lean("qkv", q);
+  run<2, 4, 6, 2>("qkv: MF=2", q, 144);
+  GemmArgs xq = base(768, 768, 0);
+  xq.ln_w = g_lnw; xq.ln_b = g_lnb; xq.ln_a16 = g_x16; xq.A = g_x; xq.bias = g_bias; xq.out = g_out;
+  run<1, 4, 6, 2>("xq: LN16 (library)", xq, 48);
+  run_lean("xq", xq);
+  run<2, 4, 6, 2>("xq: MF=2", xq, 48);
+  GemmArgs xq0 = xq; xq0.ln_w = xq0.ln_b = nullptr; xq0.ln_a16 = nullptr; xq0.A = g_a;
+  run<1, 4, 6, 0>("xq without LN", xq0, 48);
+  GemmArgs f1 = base(3072, 768, 0);
+  f1.ln_w = g_lnw; f1.ln_b = g_lnb; f1.ln_a16 = g_x16; f1.A = g_x; f1.bias = g_bias; f1.out = g_out; f1.act = 1;
+  run<1, 4, 6, 2>("fc1: LN16 + gelu (library)", f1, 192);
+  run_lean("fc1", f1);
+  run<2, 4, 6, 2>("fc1: MF=2", f1, 192);
+  GemmArgs f2 = base(768, 3072, 0);
+  f2.A = g_a; f2.bias = g_bias; f2.resid = g_x; f2.out = g_x; f2.out_f32 = 1; f2.out16 = g_x16;
+  run<1, 8, 12, 0>("fc2: K=3072 (library)", f2, 48);
+  run_lean("fc2", f2);
+  run<2, 8, 12, 0>("fc2: MF=2", f2, 48);
+  run<1, 16, 6, 0>("fc2: NW=16", f2, 48);
+  // grouped q' = W_k,h^T q_h (K = 64)
+  GemmArgs kq = base(9216, 64, 0);
+  kq.A = g_a; kq.lda = 768; kq.out = g_out; kq.ldc = 9216; kq.a_grp_n = 768; kq.a_grp_off = 64;
+  run<1, 2, 1, 3>("kq: grouped K=64 (library)", kq, 576);
+  run_lean("kq", kq);
+  run<2, 2, 1, 3>("kq: MF=2", kq, 576);
+  return 0;
+}

@@ -874,12 +874,20 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
   int sel_bi[EP];
 #pragma unroll
   for (int it = 0; it < EP; ++it) { sel_best[it] = -INFINITY; sel_bi[it] = 0x7fffffff; }
+  // bias-boost root bits of the tile's 16 columns (one 32-bit word: tiles are 16-aligned), fetched one
+  // tile ahead with the weights (read in the epilogue they cost a dependent round trip per tile)
+  const bool boost = g.sel_val && g.sel_lam != 0.f;
+  uint32_t rbw = boost ? g.sel_root_bits[(ct * 16) >> 5] : 0u, rbn = 0u;
   int buf = 0;
   for (; ct < ntile; ct += gridDim.x) {
     const int n0 = ct * 16;
     // P (persistent column walk): the next tile's weights are in flight behind this tile (clamped:
     // an unconditional load keeps hipcc from draining the queue at the loop head)
-    if constexpr (P) load_w(wn, min(ct + (int)gridDim.x, ntile - 1));
+    if constexpr (P) {
+      const int cn = min(ct + (int)gridDim.x, ntile - 1);
+      load_w(wn, cn);
+      if (boost) rbn = g.sel_root_bits[(cn * 16) >> 5];
+    }
     if constexpr (AM == 3) {
       const T* A = reinterpret_cast<const T*>(g.A) + (long)(n0 / g.a_grp_n) * g.a_grp_off;
 #pragma unroll
@@ -948,7 +956,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
         if (valid) {
           x = v;
           if (g.sel_lam != 0.f)
-            x = bias_bonus(x, g.sel_lam, pf_rb[it] + (int)((g.sel_root_bits[nn >> 5] >> (nn & 31)) & 1u));
+            x = bias_bonus(x, g.sel_lam, pf_rb[it] + (int)((rbw >> (nn & 31)) & 1u));
           if (mask_eos && nn == g.sel_eos) x = -INFINITY;
           xi = nn;
         }
@@ -966,6 +974,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
     if constexpr (P) {
 #pragma unroll
       for (int ks = 0; ks < KPW; ++ks) wc[ks] = wn[ks];
+      rbw = rbn;
     } else {
       break;
     }
@@ -979,6 +988,222 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
         g.sel_idx[(long)row * gridDim.x + blockIdx.x] = sel_bi[it];
       }
     }
+  }
+}
+
+// Lean decode projection (dec_lean_kernel): the single-tile launches of gemm_dec_kernel (every decode
+// projection of <= 64 rows except the LM head) with the same arithmetic — the same K split over the
+// waves, LayerNorm statistics and normalisation, MFMA order and wave-partial sum order, so the
+// outputs are bit-identical — restructured for the launch-latency floor measured in
+// tools/dec_kernel_bench.hip (a byte-matched stream kernel 2.0 µs per chained launch against 3.8-8.4
+// µs for gemm_dec_kernel): (a) a compact argument block (DecLean, one scalar load batch, where
+// GemmArgs took three dependent kernel-argument round trips before the activation loads were
+// issued); (b) every vector load of the launch — weights, activations, LayerNorm γ/β (per lane,
+// straight from global memory: no LDS staging), bias, residual, the device-side cache position — in
+// one unconditional burst (clamped indices; a conditional load made hipcc drain the queue with
+// vmcnt(0) before the LayerNorm parameters, i.e. a second memory round trip); (c) an epilogue of 4
+// consecutive columns per thread (16-byte f32 and 8-byte 16-bit stores).
+//   EPI 0: out (T) = act(acc + bias);  1: x (f32) += acc + bias, x16 = T(x);  2: QKV — columns below
+//   n_split → out (T), the rest → the self-attention KV cache at the device-side position.
+//   GRP: block-diagonal A (q'_h = W_k,hᵀ q_h: K = 64, the A row of column block n0 starts
+//   (n0 / grp_n)·grp_off further), no bias.
+template <typename T> struct DecLean {
+  const T* W; const T* A; const float* bias; const float* gam; const float* bet;
+  float* x; T* out; T* kv; const int* pos;
+  int M, N, lda, ldo;
+  int n_split, kvB, kvH, kvT;
+  int grp_n, grp_off;
+};
+
+template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP>
+__global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
+  using Frag = typename DT<T>::frag;
+  constexpr int NT = NW * 64, K = NW * KPW * 32, R = MF * 16;
+  static_assert(R * 4 <= NT, "epilogue: 4 columns per thread");
+  __shared__ __attribute__((aligned(16))) float red[NW][R][17];
+  __shared__ float2 rst[LN ? NW : 1][LN ? R : 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ct = blockIdx.x, mb = blockIdx.y * R, n0 = ct * 16;
+  const int kb = wave * (KPW * 32) + 8 * (lane >> 4);
+  // ---------------- the launch's loads, one burst
+  Frag w[KPW];
+  {
+    const T* Wr = p.W + (long)min(n0 + (lane & 15), p.N - 1) * K + kb;
+#pragma unroll
+    for (int ks = 0; ks < KPW; ++ks) w[ks] = __builtin_nontemporal_load(reinterpret_cast<const Frag*>(Wr + ks * 32));
+  }
+  Frag a[MF][KPW];
+  {
+    const T* A0 = p.A + (GRP ? (long)(n0 / p.grp_n) * p.grp_off : 0L) + kb;
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const T* ar = A0 + (long)min(mb + i * 16 + (lane & 15), p.M - 1) * p.lda;
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) a[i][ks] = load_frag<T>(ar + ks * 32);
+    }
+  }
+  f32x4 lg[LN ? KPW : 1][2], lb[LN ? KPW : 1][2];
+  if constexpr (LN) {
+#pragma unroll
+    for (int ks = 0; ks < KPW; ++ks) {
+      lg[ks][0] = *reinterpret_cast<const f32x4*>(p.gam + kb + ks * 32);
+      lg[ks][1] = *reinterpret_cast<const f32x4*>(p.gam + kb + ks * 32 + 4);
+      lb[ks][0] = *reinterpret_cast<const f32x4*>(p.bet + kb + ks * 32);
+      lb[ks][1] = *reinterpret_cast<const f32x4*>(p.bet + kb + ks * 32 + 4);
+    }
+  }
+  // epilogue operands: thread → row er (local), columns ec .. ec + 3
+  const int er = tid >> 2, ec = n0 + (tid & 3) * 4;
+  const int erow = min(mb + min(er, R - 1), p.M - 1);
+  const int ecc = min(ec, p.N - 4);
+  f32x4 bias4 = f32x4{0.f, 0.f, 0.f, 0.f}, res4 = bias4;
+  if constexpr (!GRP) bias4 = *reinterpret_cast<const f32x4*>(p.bias + ecc);
+  if constexpr (EPI == 1) res4 = *reinterpret_cast<const f32x4*>(p.x + (long)erow * p.ldo + ecc);
+  int pos = 0;
+  if constexpr (EPI == 2) pos = __builtin_nontemporal_load(p.pos);
+  __builtin_amdgcn_sched_barrier(0);
+  // ---------------- LayerNorm of the A rows (gemm_dec_kernel AM = 2 arithmetic)
+  if constexpr (LN) {
+    float xv[MF][KPW][8];
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float v;
+          if constexpr (__is_same(T, bf16_t)) v = bf16_to_f((bf16_t)a[i][ks][e]);
+          else v = float(a[i][ks][e]);
+          xv[i][ks][e] = v;
+          s1 += v;
+          s2 = fmaf(v, v, s2);
+        }
+      }
+      s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
+      if (lane < 16) rst[wave][i * 16 + lane] = float2{s1, s2};
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) { const float2 t = rst[q][i * 16 + (lane & 15)]; s1 += t.x; s2 += t.y; }
+      const float mean = s1 / K;
+      const float rstd = rsqrtf(fmaxf(s2 / K - mean * mean, 0.f) + 1e-5f);
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gw = lg[ks][e >> 2][e & 3], gb = lb[ks][e >> 2][e & 3];
+          const float v = (xv[i][ks][e] - mean) * rstd * gw + gb;
+          a[i][ks][e] = __builtin_bit_cast(typename std::remove_reference<decltype(a[0][0][0])>::type, DT<T>::fromf(v));
+        }
+      }
+    }
+  }
+  // ---------------- MFMA over this wave's K slice, partial tiles through LDS
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KPW; ++ks) acc = mma16(a[i][ks], w[ks], acc);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[wave][i * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[e];
+  }
+  __syncthreads();
+  // ---------------- epilogue: 4 consecutive columns of one row per thread
+  if (er >= R) return;
+  const int row = mb + er;
+  if (row >= p.M || ec >= p.N) return;
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) s += red[q][er][(tid & 3) * 4 + e];
+    v[e] = s + bias4[e];
+    if constexpr (GELU) v[e] = gelu_t<T>(v[e]);
+  }
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  if constexpr (EPI == 1) {
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = v[e] + res4[e];
+    const long off = (long)row * p.ldo + ec;
+    *reinterpret_cast<f32x4*>(p.x + off) = o;
+    s4 h;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) h[e] = __builtin_bit_cast(short, DT<T>::fromf(o[e]));
+    *reinterpret_cast<s4*>(p.out + off) = h;
+  } else {
+    s4 hv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) hv[e] = __builtin_bit_cast(short, DT<T>::fromf(v[e]));
+    if (EPI == 2 && ec >= p.n_split) {   // k / v of the new token → self-attention KV cache
+      const int n2 = ec - p.n_split, hh = n2 >> 6, dd = n2 & 63;
+      const int kvs = hh / p.kvH, hd = hh % p.kvH;
+      const long off = ((((long)kvs * p.kvB + row) * p.kvH + hd) * p.kvT + pos) * 64 + dd;
+      *reinterpret_cast<s4*>(p.kv + off) = hv;
+    } else {
+      *reinterpret_cast<s4*>(p.out + (long)row * p.ldo + ec) = hv;
+    }
+  }
+}
+
+template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP>
+static void launch_lean_k(const GemmArgs& g, hipStream_t s) {
+  DecLean<T> p;
+  p.W = reinterpret_cast<const T*>(g.W);
+  p.A = reinterpret_cast<const T*>(LN ? g.ln_a16 : g.A);
+  p.bias = g.bias; p.gam = g.ln_w; p.bet = g.ln_b;
+  p.x = EPI == 1 ? reinterpret_cast<float*>(g.out) : nullptr;
+  p.out = reinterpret_cast<T*>(EPI == 1 ? g.out16 : g.out);
+  p.kv = reinterpret_cast<T*>(g.kv_out); p.pos = g.pos;
+  p.M = g.M; p.N = g.N; p.lda = (int)g.lda; p.ldo = (int)g.ldc;
+  p.n_split = g.n_split; p.kvB = g.hs_B; p.kvH = g.hs_H; p.kvT = g.kv_T;
+  p.grp_n = g.a_grp_n; p.grp_off = (int)g.a_grp_off;
+  const dim3 grid((g.N + 15) / 16, (g.M + MF * 16 - 1) / (MF * 16));
+  WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP>), grid, dim3(NW * 64), 0, s, p);
+}
+
+// the lean form where it applies (16-bit, <= 64 rows, single-tile decode projections); false: the
+// caller takes gemm_dec_kernel. Same (waves, k-steps) table as launch_dec_mf: bit-identical outputs.
+template <typename T>
+static bool launch_lean(const GemmArgs& g, hipStream_t s) {
+  if constexpr (sizeof(T) != 2) {
+    return false;
+  } else {
+    if (g.M > 64 || g.sel_val || g.st_out || g.addrow || g.tile || g.a_Mb || g.c_Mb || g.N % 16 || g.ldc % 4) return false;
+    if (g.mode != 0 && g.mode != 2) return false;
+    if (g.mode == 2 && (g.kv_rps > 1 || !g.kv_out || !g.pos || g.n_split % 64 || g.out_f32 || g.resid)) return false;
+    if (g.a_grp_n) {   // q'_h = W_k,hᵀ q_h
+      if (g.K != 64 || g.bias || g.ln_w || g.resid || g.act || g.mode || g.out_f32 || g.a_grp_n % 16) return false;
+      launch_lean_k<T, 1, 2, 1, false, 0, false, true>(g, s);
+      return true;
+    }
+    if (!g.bias || g.clamp != 0.f) return false;
+    if (g.ln_w) {
+      if (!g.ln_a16 || !g.ln_b || g.resid || g.out_f32 || (g.act && g.mode)) return false;
+#define WCB_LN(k, nw, kpw)                                                                          \
+  if (g.K == k) {                                                                                   \
+    if (g.mode == 2) launch_lean_k<T, 1, nw, kpw, true, 2, false, false>(g, s);                     \
+    else if (g.act) launch_lean_k<T, 1, nw, kpw, true, 0, true, false>(g, s);                       \
+    else launch_lean_k<T, 1, nw, kpw, true, 0, false, false>(g, s);                                 \
+    return true;                                                                                    \
+  }
+      WCB_LN(512, 4, 4) WCB_LN(768, 4, 6) WCB_LN(1024, 4, 8) WCB_LN(1280, 8, 5)
+#undef WCB_LN
+      return false;
+    }
+    // residual writers: x (f32, in place) += A·Wᵀ + b, and its 16-bit copy
+    if (g.mode || g.act || !g.resid || g.resid != g.out || !g.out_f32 || !g.out16) return false;
+#define WCB_RS(k, nw, kpw) if (g.K == k) { launch_lean_k<T, 1, nw, kpw, false, 1, false, false>(g, s); return true; }
+    WCB_RS(512, 4, 4) WCB_RS(768, 4, 6) WCB_RS(1024, 4, 8) WCB_RS(1280, 8, 5) WCB_RS(2048, 8, 8) WCB_RS(3072, 8, 12)
+    WCB_RS(4096, 16, 8) WCB_RS(5120, 16, 10)
+#undef WCB_RS
+    return false;
   }
 }
 
@@ -1122,6 +1347,7 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
     // decode GEMM (K in its table; else the older skinny kernel below): 16-row workgroups up to 64
     // rows (measured C2: 1.074 vs 1.147 ms/token with 32-row workgroups); the LM head walks the
     // vocabulary persistently with 32-row workgroups, reading every weight tile once
+    if (g.lean && launch_lean<T>(g, s)) return;
     const bool mf1 = (g.M <= 64 && !(g.sel_val && g.M > 16)) || g.K >= 4096;
     const bool ok = mf1 ? launch_dec_mf<T, 1>(g, s) : launch_dec_mf<T, 2>(g, s);
     if (ok) return;

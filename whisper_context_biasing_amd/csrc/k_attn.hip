@@ -412,9 +412,95 @@ __global__ __launch_bounds__(64) void attn_self_kernel(AttnArgs a) {
   }
 }
 
+// attn_self_kernel<T, false> (greedy rows, keys in place) with a compact argument block: the
+// AttnArgs form took three dependent scalar round trips (kernel arguments, the device-side key count,
+// the remaining arguments) before its K/V loads were issued; here every argument arrives in one
+// scalar batch, the q / K / V loads go out first and the key count after them. Same arithmetic,
+// bit-identical outputs.
+struct SelfLean {
+  const void* q; const void* k; const void* v; void* o;
+  const int* nkeys_dev;
+  long k_sb, k_sh;
+  int ldq, ldo, H, cap, nkeys_add, row0, b_div;
+};
+
+template <typename T>
+__global__ __launch_bounds__(64) void attn_self_lean_kernel(SelfLean a) {
+  const int b = blockIdx.y / a.H, h = blockIdx.y % a.H, lane = threadIdx.x;
+  const int seg = lane & 7, kg = lane >> 3;
+  const long base = (long)((a.row0 + b) / a.b_div) * a.k_sb + (long)h * a.k_sh + seg * 8;
+  const T* kb = reinterpret_cast<const T*>(a.k) + base;
+  const T* vb = reinterpret_cast<const T*>(a.v) + base;
+  const T* q = reinterpret_cast<const T*>(a.q) + (long)b * a.ldq + h * 64;
+  float qv[8], kv[8][8], vv[8][8];
+  load8f<T>(q + seg * 8, qv);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) load8f<T>(kb + (long)min(u * 8 + kg, a.cap) * 64, kv[u]);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) load8f<T>(vb + (long)min(u * 8 + kg, a.cap) * 64, vv[u]);
+  const int nk = __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(a.nkeys_dev)) + a.nkeys_add;
+  float m = -INFINITY, l = 0.f;
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < nk; j0 += 64) {
+    if (j0) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) load8f<T>(kb + (long)min(min(j0 + u * 8 + kg, nk - 1), a.cap) * 64, kv[u]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) load8f<T>(vb + (long)min(min(j0 + u * 8 + kg, nk - 1), a.cap) * 64, vv[u]);
+    }
+    float sc[8];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d = fmaf(qv[e], kv[u][e], d);
+#pragma unroll
+      for (int x = 1; x < 8; x <<= 1) d += __shfl_xor(d, x, 64);
+      sc[u] = (j0 + u * 8 + kg < nk) ? d : -INFINITY;
+      mx = fmaxf(mx, sc[u]);
+    }
+    const float mn = fmaxf(m, wave_max(mx));
+    const float r = __expf(m - mn);
+    l *= r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] *= r;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool live = j0 + u * 8 + kg < nk;
+      const float p = live ? __expf(sc[u] - mn) : 0.f;
+      if (seg == 0) l += p;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = live ? fmaf(p, vv[u][e], o[e]) : o[e];
+    }
+    m = mn;
+  }
+  l = wave_sum(l);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o[e] += __shfl_xor(o[e], 8, 64);
+    o[e] += __shfl_xor(o[e], 16, 64);
+    o[e] += __shfl_xor(o[e], 32, 64);
+  }
+  if (kg == 0) {
+    float r[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = o[e] / l;
+    store8<T>(reinterpret_cast<T*>(a.o) + (long)b * a.ldo + h * 64 + seg * 8, r);
+  }
+}
+
 template <typename T>
 static void launch_decode(const AttnArgs& b, dim3 grid, int variant, hipStream_t s) {
   if (b.kv_rows > 0 && b.Sq == 1 && b.nsplit == 1) {   // decoder self-attention, one new token
+    if (!b.phys && b.nkeys_dev && b.k_sk == 64 && b.q_Sb == 1 && b.o_Sb == 1 && sizeof(T) == 2) {
+      SelfLean c;
+      c.q = b.q; c.k = b.k; c.v = b.v; c.o = b.o; c.nkeys_dev = b.nkeys_dev;
+      c.k_sb = b.k_sb; c.k_sh = b.k_sh; c.ldq = (int)b.ldq; c.ldo = (int)b.ldo; c.H = b.H;
+      c.cap = b.kv_rows - 1; c.nkeys_add = b.nkeys_add; c.row0 = b.row0; c.b_div = b.b_div > 0 ? b.b_div : 1;
+      WCB_LAUNCH((attn_self_lean_kernel<T>), dim3(1, grid.y), dim3(64), 0, s, c);
+      return;
+    }
     if (b.phys) WCB_LAUNCH((attn_self_kernel<T, true>), dim3(1, grid.y), dim3(64), 0, s, b);
     else WCB_LAUNCH((attn_self_kernel<T, false>), dim3(1, grid.y), dim3(64), 0, s, b);
     return;

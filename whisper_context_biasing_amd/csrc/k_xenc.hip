@@ -459,8 +459,17 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
 #pragma unroll
     for (int k = 0; k < CPL; ++k) wf[p][k] = load_frag<T>(wr + k * 128);
   }
-  if (tid < kXencMaxSplit)
-    sv[tid] = tid < ns ? *reinterpret_cast<const float2*>(a.ml + (((long)b * ns + tid) * a.H + h) * 2) : float2{0.f, 0.f};
+  // the range partials of this thread's 4 columns and the ranges' (max, Σp) go out in the same burst
+  // as the weights (issued behind the (max, Σp) exchange they cost a second memory round trip);
+  // D <= 1024: one 4-column group per thread, threads past D re-load the last group and discard it
+  static_assert(D <= 1024, "one 4-column group per thread");
+  const float* pp = a.part + ((long)b * ns * a.H + h) * D;
+  const int c = min(tid * 4, D - 4);
+  f32x4 pv[kXencMaxSplit];
+#pragma unroll
+  for (int s = 0; s < kXencMaxSplit; ++s) pv[s] = *reinterpret_cast<const f32x4*>(pp + (long)min(s, ns - 1) * a.H * D + c);
+  const float2 mlv = *reinterpret_cast<const float2*>(a.ml + (((long)b * ns + min(tid, ns - 1)) * a.H + h) * 2);
+  if (tid < kXencMaxSplit) sv[tid] = tid < ns ? mlv : float2{0.f, 0.f};
   __syncthreads();
   float2 v[kXencMaxSplit];
 #pragma unroll
@@ -477,18 +486,14 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
     L += w[s] * v[s].y;
   }
   const float inv = 1.f / L;
-  const float* pp = a.part + ((long)b * ns * a.H + h) * D;
-  for (int c = tid * 4; c < D; c += 1024) {
-    f32x4 pv[kXencMaxSplit];
-#pragma unroll
-    for (int s = 0; s < kXencMaxSplit; ++s) pv[s] = *reinterpret_cast<const f32x4*>(pp + (long)min(s, ns - 1) * a.H * D + c);
+  {
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < kXencMaxSplit; ++s) acc += w[s] * pv[s];
     acc *= inv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc[e] = DT<T>::tof(DT<T>::fromf(acc[e]));   // u in T, as stored unfused
-    *reinterpret_cast<f32x4*>(us + c) = acc;
+    if (tid * 4 < D) *reinterpret_cast<f32x4*>(us + c) = acc;
   }
   __syncthreads();
 #pragma unroll

@@ -87,6 +87,9 @@ struct GemmArgs {
   // f16 encoder layers: the layer output is clamped to ±(finfo(f16).max − 1000)
   // ([tf] modeling_whisper.py:409-411); 0 = off
   float clamp = 0.f;
+  // decode projection: the lean single-tile kernel (gemm_impl.h dec_lean_kernel, bit-identical to
+  // gemm_dec_kernel) where its shape / epilogue table covers the launch
+  int lean = 0;
 };
 
 void gemm(DType t, const GemmArgs& g, hipStream_t s);

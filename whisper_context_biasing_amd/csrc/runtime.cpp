@@ -206,6 +206,9 @@ struct wcb_handle {
   int ln16 = 1;
   int vocab_pad = 0;    // LM-head rows padded to a multiple of 128 (zero rows): the MFMA tile path's N
   int steps_per_graph = 8;   // decode steps captured per replayed graph (WCB_STEPS_PER_GRAPH)
+  // decode projections of <= 64 rows on dec_lean_kernel (gemm_impl.h; bit-identical to
+  // gemm_dec_kernel, one kernel-argument round trip and one load burst per launch; option "lean")
+  int lean = 1;
   // decode projections on gemm_dec_kernel (K supported): the LayerNorm consumers compute their row
   // statistics from the rows they load, so the producers publish no per-16-column partial sums
   bool dec_gemm = false;
@@ -549,6 +552,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       h->ring_kt = value;
     } else if (n == "xqk") {
       h->xqk = value != 0;
+    } else if (n == "lean") {
+      h->lean = value != 0;
     } else if (n == "merge_v") {
       h->merge_v = value != 0;
     } else if (n == "ln_fold") {
@@ -1029,6 +1034,8 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       }
       g.tile = ring ? 2 : 1; g.skinny = 0; g.ring_kt = h->ring_kt;
       if (ring && g.resid && g.out16 && lnf_ok) g.rst_out = rst;   // residual writer: stats for the next LN
+    } else {
+      g.lean = h->lean;   // <= 64 rows: the lean single-tile kernel where it covers the launch
     }
     dgemm(h, cls, g, st_);
   };
@@ -1782,7 +1789,14 @@ int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void*
     a.k = k; a.v = v; a.k_sb = (long)H * Sk * 64; a.k_sh = (long)Sk * 64; a.k_sk = 64;
     a.o = o; a.ldo = (long)H * 64; a.o_Sb = 1; a.B = B; a.H = H; a.nkeys = Sk;
     a.variant = variant;
-    if (variant == 6) a.kv_rows = Sk;   // the one-token self-attention kernel (speculative first keys)
+    if (variant == 6 || variant == 7) a.kv_rows = Sk;   // the one-token self-attention kernel (speculative first keys)
+    static DevBuf nk_dev;
+    if (variant == 7) {   // the key count read on the device (decode graphs): the lean self-attention kernel
+      nk_dev.ensure(4);
+      const int nk1 = Sk - 1;
+      HIPCHK(hipMemcpyAsync(nk_dev.p, &nk1, 4, hipMemcpyHostToDevice, (hipStream_t)stream));
+      a.nkeys_dev = nk_dev.as<int>(); a.nkeys_add = 1;
+    }
     static DevBuf part, ticket;
     if (nsplit > 1) {
       a.nsplit = nsplit;
