@@ -5,7 +5,9 @@
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I whisper_context_biasing_amd/csrc tools/dec_kernel_bench.hip -o tools/dec_kernel_bench
 #include "gemm_impl.h"
 
+#include <algorithm>
 #include <functional>
+#include <vector>
 
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
@@ -98,6 +100,74 @@ void run_lean(const char* name, GemmArgs g0) {
   fflush(stdout);
 }
 
+// per-workgroup phase stamps of every launch of a 100-launch chain (s_memrealtime, 10 ns ticks):
+// median over launches 10..99 of: dispatch gap (first start - previous launch's last end), start spread,
+// loads landed, LN + MFMA + LDS exchange, epilogue + store drain, launch span
+void run_lean_stamped(const char* name, GemmArgs g0) {
+  const long wbytes = (long)g0.N * g0.K * 2;
+  const long nreg = (long)(kW / wbytes);
+  const int nwg = ((g0.N + 15) / 16) * ((g0.M + 15) / 16);
+  const int n = 100;
+  unsigned long long* st;
+  CHK(hipMalloc(&st, (size_t)n * nwg * 32));
+  CHK(hipMemset(st, 0, (size_t)n * nwg * 32));
+  time_graph(n, [&](int i, hipStream_t s) {
+    GemmArgs g = g0;
+    g.W = g_w + (i % nreg) * wbytes;
+    g_lean_stamp = st + (long)i * nwg * 4;
+    launch_lean<bf16_t>(g, s);
+    g_lean_stamp = nullptr;
+  });
+  std::vector<unsigned long long> h((size_t)n * nwg * 4);
+  CHK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+  CHK(hipFree(st));
+  auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+  std::vector<double> gap, spread, ld, mid, ep, span, wgdur;
+  for (int i = 10; i < n; ++i) {
+    const unsigned long long* a = &h[(size_t)i * nwg * 4];
+    const unsigned long long* b = &h[(size_t)(i - 1) * nwg * 4];
+    unsigned long long s0 = ~0ull, s1 = 0, e1 = 0, pe = 0;
+    std::vector<double> l, m, e, d;
+    for (int w = 0; w < nwg; ++w) {
+      s0 = std::min(s0, a[w * 4]); s1 = std::max(s1, a[w * 4]); e1 = std::max(e1, a[w * 4 + 3]);
+      pe = std::max(pe, b[w * 4 + 3]);
+      l.push_back((a[w * 4 + 1] - a[w * 4]) * 0.01); m.push_back((a[w * 4 + 2] - a[w * 4 + 1]) * 0.01);
+      e.push_back((a[w * 4 + 3] - a[w * 4 + 2]) * 0.01); d.push_back((a[w * 4 + 3] - a[w * 4]) * 0.01);
+    }
+    gap.push_back(((double)s0 - (double)pe) * 0.01); spread.push_back((s1 - s0) * 0.01);
+    ld.push_back(med(l)); mid.push_back(med(m)); ep.push_back(med(e)); wgdur.push_back(med(d)); span.push_back((e1 - s0) * 0.01);
+  }
+  printf("%-22s stamps (us, medians): gap %5.2f  start-spread %5.2f  loads %5.2f  ln+mfma+lds %5.2f  epilogue %5.2f  wg %5.2f  span %5.2f\n",
+         name, med(gap), med(spread), med(ld), med(mid), med(ep), med(wgdur), med(span));
+  fflush(stdout);
+}
+
+// the lean out-projection with fragment-major weights (layout only: the bench's weights are zeros)
+template <int NW, int KPW, bool LN, int EPI>
+void run_wfm(const char* name, GemmArgs g0, bool stamped) {
+  const long wbytes = (long)g0.N * g0.K * 2;
+  const long nreg = (long)(kW / wbytes);
+  const int nwg = ((g0.N + 15) / 16) * ((g0.M + 15) / 16);
+  unsigned long long* st = nullptr;
+  if (stamped) { CHK(hipMalloc(&st, (size_t)100 * nwg * 32)); CHK(hipMemset(st, 0, (size_t)100 * nwg * 32)); }
+  double us = time_graph(100, [&](int i, hipStream_t s) {
+    DecLean<bf16_t> p;
+    p.W = reinterpret_cast<const bf16_t*>(g_w + (i % nreg) * wbytes);
+    p.A = reinterpret_cast<const bf16_t*>(LN ? g0.ln_a16 : g0.A); p.bias = g0.bias; p.gam = g0.ln_w; p.bet = g0.ln_b;
+    p.x = EPI == 1 ? reinterpret_cast<float*>(g0.out) : nullptr;
+    p.out = reinterpret_cast<bf16_t*>(EPI == 1 ? g0.out16 : g0.out);
+    p.kv = reinterpret_cast<bf16_t*>(g0.kv_out); p.pos = g0.pos;
+    p.M = g0.M; p.N = g0.N; p.lda = (int)g0.lda; p.ldo = (int)g0.ldc;
+    p.n_split = g0.n_split; p.kvB = g0.hs_B; p.kvH = g0.hs_H; p.kvT = g0.kv_T; p.grp_n = 0; p.grp_off = 0;
+    p.stamp = st ? st + (long)i * nwg * 4 : nullptr;
+    hipLaunchKernelGGL((dec_lean_kernel<bf16_t, 1, NW, KPW, LN, EPI, false, false, true>), dim3((g0.N + 15) / 16, (g0.M + 15) / 16),
+                       dim3(NW * 64), 0, s, p);
+  });
+  printf("%-40s lean, fragment-major W: %6.2f us/launch\n", name, us);
+  if (st) CHK(hipFree(st));
+  fflush(stdout);
+}
+
 template <int NT, int WPL, int APL>
 void run_stream(const char* name, int grid) {
   const long per_wg = (long)NT * WPL, per_launch = per_wg * grid;
@@ -145,6 +215,8 @@ int main() {
   o.A = g_a; o.bias = g_bias; o.resid = g_x; o.out = g_x; o.out_f32 = 1; o.out16 = g_x16;
   run<1, 4, 6, 0>("out: bias+resid+f32+x16 (library)", o, 48);
   run_lean("out", o);
+  run_lean_stamped("out", o);
+  run_wfm<4, 6, false, 1>("out", o, false);
   run<2, 4, 6, 0>("out: MF=2", o, 48);
   run<1, 8, 3, 0>("out: NW=8", o, 48);
   run<2, 8, 3, 0>("out: MF=2 NW=8", o, 48);
@@ -158,11 +230,15 @@ int main() {
   q.out = g_out; q.mode = 2; q.n_split = 768; q.kv_out = g_kv; q.hs_B = 32; q.hs_H = 12; q.kv_T = 80; q.pos = g_pos;
   run<1, 4, 6, 2>("qkv: LN16 + kv append (library)", q, 144);
   run_lean("qkv", q);
+  run_lean_stamped("qkv", q);
+  run_wfm<4, 6, true, 2>("qkv", q, false);
   run<2, 4, 6, 2>("qkv: MF=2", q, 144);
   GemmArgs xq = base(768, 768, 0);
   xq.ln_w = g_lnw; xq.ln_b = g_lnb; xq.ln_a16 = g_x16; xq.A = g_x; xq.bias = g_bias; xq.out = g_out;
   run<1, 4, 6, 2>("xq: LN16 (library)", xq, 48);
   run_lean("xq", xq);
+  run_lean_stamped("xq", xq);
+  run_wfm<4, 6, true, 0>("xq", xq, false);
   run<2, 4, 6, 2>("xq: MF=2", xq, 48);
   GemmArgs xq0 = xq; xq0.ln_w = xq0.ln_b = nullptr; xq0.ln_a16 = nullptr; xq0.A = g_a;
   run<1, 4, 6, 0>("xq without LN", xq0, 48);
@@ -175,6 +251,9 @@ int main() {
   f2.A = g_a; f2.bias = g_bias; f2.resid = g_x; f2.out = g_x; f2.out_f32 = 1; f2.out16 = g_x16;
   run<1, 8, 12, 0>("fc2: K=3072 (library)", f2, 48);
   run_lean("fc2", f2);
+  run_lean_stamped("fc2", f2);
+  run_wfm<8, 12, false, 1>("fc2", f2, false);
+  run_wfm<16, 6, false, 1>("fc2 NW=16", f2, false);
   run<2, 8, 12, 0>("fc2: MF=2", f2, 48);
   run<1, 16, 6, 0>("fc2: NW=16", f2, 48);
   // grouped q' = W_k,h^T q_h (K = 64)

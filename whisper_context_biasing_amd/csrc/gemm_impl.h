@@ -1013,9 +1013,10 @@ template <typename T> struct DecLean {
   int M, N, lda, ldo;
   int n_split, kvB, kvH, kvT;
   int grp_n, grp_off;
+  unsigned long long* stamp = nullptr;   // tools/dec_kernel_bench: per-workgroup phase stamps (null: off)
 };
 
-template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP>
+template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP, bool WFM = false>
 __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   using Frag = typename DT<T>::frag;
   constexpr int NT = NW * 64, K = NW * KPW * 32, R = MF * 16;
@@ -1025,9 +1026,14 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ct = blockIdx.x, mb = blockIdx.y * R, n0 = ct * 16;
   const int kb = wave * (KPW * 32) + 8 * (lane >> 4);
+  const unsigned long long t0 = p.stamp ? stamp_now() : 0ull;
   // ---------------- the launch's loads, one burst
   Frag w[KPW];
-  {
+  if constexpr (WFM) {   // fragment-major weights: [tile][wave][k-step][lane][8], 1 KiB per wave-instruction
+    const T* Wr = p.W + (((long)ct * NW + wave) * KPW * 64 + lane) * 8;
+#pragma unroll
+    for (int ks = 0; ks < KPW; ++ks) w[ks] = __builtin_nontemporal_load(reinterpret_cast<const Frag*>(Wr + ks * 512));
+  } else {
     const T* Wr = p.W + (long)min(n0 + (lane & 15), p.N - 1) * K + kb;
 #pragma unroll
     for (int ks = 0; ks < KPW; ++ks) w[ks] = __builtin_nontemporal_load(reinterpret_cast<const Frag*>(Wr + ks * 32));
@@ -1062,6 +1068,8 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   int pos = 0;
   if constexpr (EPI == 2) pos = __builtin_nontemporal_load(p.pos);
   __builtin_amdgcn_sched_barrier(0);
+  unsigned long long t1 = 0, t2 = 0;
+  if (p.stamp) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); t1 = stamp_now(); }
   // ---------------- LayerNorm of the A rows (gemm_dec_kernel AM = 2 arithmetic)
   if constexpr (LN) {
     float xv[MF][KPW][8];
@@ -1113,6 +1121,7 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
     for (int e = 0; e < 4; ++e) red[wave][i * 16 + (lane >> 4) * 4 + e][lane & 15] = acc[e];
   }
   __syncthreads();
+  if (p.stamp) t2 = stamp_now();
   // ---------------- epilogue: 4 consecutive columns of one row per thread
   if (er >= R) return;
   const int row = mb + er;
@@ -1150,12 +1159,20 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
       *reinterpret_cast<s4*>(p.out + (long)row * p.ldo + ec) = hv;
     }
   }
+  if (p.stamp && tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned long long* st = p.stamp + (long)(blockIdx.y * gridDim.x + blockIdx.x) * 4;
+    st[0] = t0; st[1] = t1; st[2] = t2; st[3] = stamp_now();
+  }
 }
+
+inline thread_local unsigned long long* g_lean_stamp = nullptr;   // tools/dec_kernel_bench only
 
 template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP>
 static void launch_lean_k(const GemmArgs& g, hipStream_t s) {
   DecLean<T> p;
-  p.W = reinterpret_cast<const T*>(g.W);
+  p.stamp = g_lean_stamp;
+  p.W = reinterpret_cast<const T*>(g.W_fm ? g.W_fm : g.W);
   p.A = reinterpret_cast<const T*>(LN ? g.ln_a16 : g.A);
   p.bias = g.bias; p.gam = g.ln_w; p.bet = g.ln_b;
   p.x = EPI == 1 ? reinterpret_cast<float*>(g.out) : nullptr;
@@ -1165,7 +1182,8 @@ static void launch_lean_k(const GemmArgs& g, hipStream_t s) {
   p.n_split = g.n_split; p.kvB = g.hs_B; p.kvH = g.hs_H; p.kvT = g.kv_T;
   p.grp_n = g.a_grp_n; p.grp_off = (int)g.a_grp_off;
   const dim3 grid((g.N + 15) / 16, (g.M + MF * 16 - 1) / (MF * 16));
-  WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP>), grid, dim3(NW * 64), 0, s, p);
+  if (g.W_fm) WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true>), grid, dim3(NW * 64), 0, s, p);
+  else WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP>), grid, dim3(NW * 64), 0, s, p);
 }
 
 // the lean form where it applies (16-bit, <= 64 rows, single-tile decode projections); false: the

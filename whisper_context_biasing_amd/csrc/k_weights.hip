@@ -109,6 +109,30 @@ void scale_cols(DType t, const void* W, int N, int K, const float* gam, void* Wg
   }
 }
 
+template <typename T>
+__global__ __launch_bounds__(256) void frag_major_kernel(const T* W, long n_el, int K, int nw, int kpw, T* dst) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n_el; i += (long)gridDim.x * 256) {
+    const int e = (int)(i & 7), lane = (int)((i >> 3) & 63);
+    long r = i >> 9;                       // (ct, wave, ks)
+    const int ks = (int)(r % kpw); r /= kpw;
+    const int wave = (int)(r % nw);
+    const long ct = r / nw;
+    const long n = ct * 16 + (lane & 15);
+    const int k = wave * kpw * 32 + ks * 32 + 8 * (lane >> 4) + e;
+    dst[i] = W[n * K + k];
+  }
+}
+
+void frag_major(DType t, const void* W, int N, int K, int nw, int kpw, void* dst, hipStream_t s) {
+  const long n = (long)N * K;
+  const dim3 grid((unsigned)std::min<long>((n + 255) / 256, 8192));
+  switch (t) {
+    case kBF16: WCB_LAUNCH(frag_major_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)W, n, K, nw, kpw, (bf16_t*)dst); break;
+    case kF16: WCB_LAUNCH(frag_major_kernel<f16_t>, grid, dim3(256), 0, s, (const f16_t*)W, n, K, nw, kpw, (f16_t*)dst); break;
+    case kF32: break;
+  }
+}
+
 void ln_fold(DType t, const void* W, int N, int K, const float* gam, const float* bet, const float* bias, float* u,
              float* c, hipStream_t s) {
   switch (t) {

@@ -88,8 +88,10 @@ struct GemmArgs {
   // ([tf] modeling_whisper.py:409-411); 0 = off
   float clamp = 0.f;
   // decode projection: the lean single-tile kernel (gemm_impl.h dec_lean_kernel, bit-identical to
-  // gemm_dec_kernel) where its shape / epilogue table covers the launch
+  // gemm_dec_kernel) where its shape / epilogue table covers the launch; W_fm = the weight's
+  // fragment-major copy (frag_major, same K split) when the runtime built one
   int lean = 0;
+  const void* W_fm = nullptr;
 };
 
 void gemm(DType t, const GemmArgs& g, hipStream_t s);
@@ -266,6 +268,13 @@ void ln_fold(DType t, const void* W, int N, int K, const float* gam, const float
 
 // Wg[n][k] = T(γ_k · W[n][k]) (the folded LayerNorm's weights)
 void scale_cols(DType t, const void* W, int N, int K, const float* gam, void* Wg, hipStream_t s);
+// Fragment-major copy of a 16-bit weight [N][K] (N % 16 == 0) for the lean decode projections
+// (gemm_impl.h dec_lean_kernel, WFM): dst[ct][wave][ks][lane][8] = W[16·ct + lane % 16][wave·kpw·32 +
+// ks·32 + 8·(lane / 16) + e], so every weight wave-instruction reads 1 KiB contiguous (the row-major
+// MFMA B-fragment loads touch 16 rows × 64 B)
+void frag_major(DType t, const void* W, int N, int K, int nw, int kpw, void* dst, hipStream_t s);
+// (waves, k-steps per wave) of the lean decode projection at this K (false: not covered)
+bool lean_cfg(int K, int& nw, int& kpw);
 void fill_i32(int* p, int v, long n, hipStream_t s);
 // dst[0..n) = host values, passed by value in the kernel arguments (stream-ordered, no host buffer
 // lifetime or pageable-copy ordering to worry about)

@@ -93,6 +93,9 @@ struct LayerW {
   float *ln1_u = nullptr, *ln1_c = nullptr, *lnx_u = nullptr, *lnx_c = nullptr, *ln2_u = nullptr, *ln2_c = nullptr;
   // encoder-space cross-attention (k_xenc.hip): W_k,hᵀ repacked [H][d][64], W_v [d][d], b_v
   void* xkt_w = nullptr; void* xv_w = nullptr; float* xv_b = nullptr;
+  // decoder, 16-bit: fragment-major copies for the lean decode projections (kernels.h frag_major)
+  void *qkv_fm = nullptr, *o_fm = nullptr, *xq_fm = nullptr, *xkt_fm = nullptr, *xo_fm = nullptr, *fc1_fm = nullptr,
+       *fc2_fm = nullptr;
 };
 
 struct ProfEntry {
@@ -737,6 +740,22 @@ int wcb_finalize_weights(wcb_handle* h) {
         fold(lw.qkv_w, 3 * d, lw.ln1_w, lw.ln1_b, lw.qkv_b, lw.qkv_wg, lw.ln1_u, lw.ln1_c);
         fold(lw.xq_w, d, lw.lnx_w, lw.lnx_b, lw.xq_b, lw.xq_wg, lw.lnx_u, lw.lnx_c);
         fold(lw.fc1_w, F, lw.ln2_w, lw.ln2_b, lw.fc1_b, lw.fc1_wg, lw.ln2_u, lw.ln2_c);
+        // fragment-major copies for the lean decode projections (<= 64 rows): each weight wave-instruction
+        // then reads 1 KiB contiguous (tools/dec_kernel_bench.hip: out 3.75 -> 3.16, fc2 8.39 -> 6.43 µs)
+        auto fm = [&](const void* W, int N, int K) -> void* {
+          int nw = 0, kpw = 0;
+          if (!W || N % 16 || !lean_cfg(K, nw, kpw)) return nullptr;
+          void* p = h->own((size_t)N * K * e);
+          frag_major(h->dt, W, N, K, nw, kpw, p, st);
+          return p;
+        };
+        lw.qkv_fm = fm(lw.qkv_w, 3 * d, d);
+        lw.o_fm = fm(lw.o_w, d, d);
+        lw.xq_fm = fm(lw.xq_w, d, d);
+        lw.xo_fm = fm(lw.xo_w, d, d);
+        lw.fc1_fm = fm(lw.fc1_w, F, d);
+        lw.fc2_fm = fm(lw.fc2_w, d, F);
+        if (lw.xkt_w) lw.xkt_fm = fm(lw.xkt_w, H * d, 64);
       }
     }
     h->enc_ln_w = F_("model.encoder.layer_norm.weight", d);
@@ -1048,7 +1067,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     GemmArgs q = drow(x, d, w.qkv_w, M, 3 * d, d, dq, d);    // LayerNorm fused (f32 A rows)
     q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nbk; q.ln_a16 = lna;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
-    q.kv_rps = rps; q.ln_u = w.ln1_u; q.ln_c = w.ln1_c; q.ln_wg = w.qkv_wg;
+    q.kv_rps = rps; q.ln_u = w.ln1_u; q.ln_c = w.ln1_c; q.ln_wg = w.qkv_wg; q.W_fm = w.qkv_fm;
     proj("dec_qkv", q);
     AttnArgs a;
     a.q = dq; a.ldq = d; a.q_Sb = rps; a.Sq = rps; a.causal = rps > 1;
@@ -1064,7 +1083,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
                [&] { attention_decode(h->dt, a, st_); });
     }
     GemmArgs o = drow(datt, d, w.o_w, M, d, d, x, d);
-    o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st_pub; o.st_nb = nbk; o.out16 = x16;
+    o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st_pub; o.st_nb = nbk; o.out16 = x16; o.W_fm = w.o_fm;
     proj("dec_out", o);
     if (c.xmode == 1) {
       // cross attention in encoder space: q'_h = W_k,hᵀ q_h (block-diagonal GEMM, K = 64), one pass
@@ -1080,10 +1099,10 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       } else {
         GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
         xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
-        xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg;
+        xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg; xq.W_fm = w.xq_fm;
         proj("dec_xq", xq);
         GemmArgs kq = drow(dq, d, w.xkt_w, M, H * d, 64, dqp, (long)H * d);
-        kq.a_grp_n = d; kq.a_grp_off = 64;
+        kq.a_grp_n = d; kq.a_grp_off = 64; kq.W_fm = w.xkt_fm;
         proj("dec_kq", kq);
       }
       XencArgs xa;
@@ -1116,7 +1135,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       // cross attention over the precomputed encoder K/V
       GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
       xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
-      xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg;
+      xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg; xq.W_fm = w.xq_fm;
       proj("dec_xq", xq);
       AttnArgs xa;
       const char* xkv = (const char*)h->xkv2[c.buf].p + l * xkv_l * e;
@@ -1152,15 +1171,15 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       });
     }
     GemmArgs xo = drow(datt, d, w.xo_w, M, d, d, x, d);
-    xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st_pub; xo.st_nb = nbk; xo.out16 = x16;
+    xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st_pub; xo.st_nb = nbk; xo.out16 = x16; xo.W_fm = w.xo_fm;
     proj("dec_xo", xo);
     // MLP
     GemmArgs f1 = drow(x, d, w.fc1_w, M, h->d.ffn, d, dffn, h->d.ffn);
     f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nbk; f1.ln_a16 = lna;
-    f1.bias = w.fc1_b; f1.act = 1; f1.ln_u = w.ln2_u; f1.ln_c = w.ln2_c; f1.ln_wg = w.fc1_wg;
+    f1.bias = w.fc1_b; f1.act = 1; f1.ln_u = w.ln2_u; f1.ln_c = w.ln2_c; f1.ln_wg = w.fc1_wg; f1.W_fm = w.fc1_fm;
     proj("dec_fc1", f1);
     GemmArgs f2 = drow(dffn, h->d.ffn, w.fc2_w, M, d, h->d.ffn, x, d);
-    f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st_pub; f2.st_nb = nbk; f2.out16 = x16;
+    f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st_pub; f2.st_nb = nbk; f2.out16 = x16; f2.W_fm = w.fc2_fm;
     proj("dec_fc2", f2);
   }
   if (c.lm_head) {
