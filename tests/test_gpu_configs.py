@@ -304,3 +304,18 @@ def test_lean_decode_projections_bit_identical(size, dtype, B):
         out.append(m.generate(x, max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0).cpu().numpy())
         del m
     assert np.array_equal(out[0], out[1]), np.argwhere(out[0] != out[1])[:8]
+
+
+@pytest.mark.parametrize("raster", [4, 8])
+def test_encoder_tile_raster_bit_identical(raster):
+    """Option enc_raster reorders the encoder GEMM tiles over the workgroups (bands of row panels): each
+    tile's arithmetic is unchanged, so the encoder output must be bit-identical (whisper-small, bf16)."""
+    dims = get_dims("small")
+    sd = weights("small", 0, "diverse")
+    x = mel_of(dims, 4)
+    out = []
+    for r in (0, raster):
+        m = WhisperCB.from_state_dict(dims, sd, dtype="bf16", options={"enc_raster": r})
+        out.append(m.encode(x).float().cpu())
+        del m
+    assert torch.equal(out[0], out[1])

@@ -294,7 +294,17 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
   const int wm = wave / WN, wn = wave % WN;
   const int tiles_n = (g.N + BN - 1) / BN;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (wg / tiles_n) * BM, n0 = (wg % tiles_n) * BN;
+  int m0, n0;
+  if (g.raster > 0) {   // bands of `raster` row panels, column tiles outer within a band (the
+                        // concurrently resident tiles of one XCD share A and W panels in its L2)
+    const int tiles_m = (g.M + BM - 1) / BM, band = g.raster * tiles_n;
+    const int fm = (wg / band) * g.raster, gm = min(tiles_m - fm, g.raster), r = wg % band;
+    m0 = (fm + r % gm) * BM;
+    n0 = (r / gm) * BN;
+  } else {
+    m0 = (wg / tiles_n) * BM;
+    n0 = (wg % tiles_n) * BN;
+  }
 
   const T* A = reinterpret_cast<const T*>(g.A);
   const T* W = reinterpret_cast<const T*>(g.W);
@@ -1014,9 +1024,10 @@ template <typename T> struct DecLean {
   int n_split, kvB, kvH, kvT;
   int grp_n, grp_off;
   unsigned long long* stamp = nullptr;   // tools/dec_kernel_bench: per-workgroup phase stamps (null: off)
+  int cfm_nw = 0, cfm_kpw = 0;           // EPI 0: out written fragment-major for a consumer with this split (0: rows)
 };
 
-template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP, bool WFM = false>
+template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP, bool WFM = false, bool AFM = false>
 __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   using Frag = typename DT<T>::frag;
   constexpr int NT = NW * 64, K = NW * KPW * 32, R = MF * 16;
@@ -1039,7 +1050,14 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
     for (int ks = 0; ks < KPW; ++ks) w[ks] = __builtin_nontemporal_load(reinterpret_cast<const Frag*>(Wr + ks * 32));
   }
   Frag a[MF][KPW];
-  {
+  if constexpr (AFM) {   // fragment-major activations [row block][wave][k-step][lane][8] (the producer's layout)
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const T* ar = p.A + ((((long)(mb / 16 + i) * NW + wave) * KPW * 64) + lane) * 8;
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) a[i][ks] = load_frag<T>(ar + ks * 512);
+    }
+  } else {
     const T* A0 = p.A + (GRP ? (long)(n0 / p.grp_n) * p.grp_off : 0L) + kb;
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
@@ -1155,6 +1173,10 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
       const int kvs = hh / p.kvH, hd = hh % p.kvH;
       const long off = ((((long)kvs * p.kvB + row) * p.kvH + hd) * p.kvT + pos) * 64 + dd;
       *reinterpret_cast<s4*>(p.kv + off) = hv;
+    } else if (EPI == 0 && p.cfm_nw) {   // fragment-major for the consumer's (waves, k-steps): 4 elements of one fragment
+      const int kw = p.cfm_kpw * 32, w2 = ec / kw, ks2 = (ec % kw) >> 5, lg = (ec & 31) >> 3;
+      const long off = ((((long)(row >> 4) * p.cfm_nw + w2) * p.cfm_kpw + ks2) * 64 + lg * 16 + (row & 15)) * 8 + (ec & 7);
+      *reinterpret_cast<s4*>(p.out + off) = hv;
     } else {
       *reinterpret_cast<s4*>(p.out + (long)row * p.ldo + ec) = hv;
     }
@@ -1181,9 +1203,15 @@ static void launch_lean_k(const GemmArgs& g, hipStream_t s) {
   p.M = g.M; p.N = g.N; p.lda = (int)g.lda; p.ldo = (int)g.ldc;
   p.n_split = g.n_split; p.kvB = g.hs_B; p.kvH = g.hs_H; p.kvT = g.kv_T;
   p.grp_n = g.a_grp_n; p.grp_off = (int)g.a_grp_off;
+  if (g.c_fm) lean_cfg(g.N, p.cfm_nw, p.cfm_kpw);   // the consumer's split of K = this N
   const dim3 grid((g.N + 15) / 16, (g.M + MF * 16 - 1) / (MF * 16));
-  if (g.W_fm) WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true>), grid, dim3(NW * 64), 0, s, p);
-  else WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP>), grid, dim3(NW * 64), 0, s, p);
+  if (g.a_fm) {
+    if constexpr (!LN && !GRP) WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, true>), grid, dim3(NW * 64), 0, s, p);
+  } else if (g.W_fm) {
+    WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true>), grid, dim3(NW * 64), 0, s, p);
+  } else {
+    WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP>), grid, dim3(NW * 64), 0, s, p);
+  }
 }
 
 // the lean form where it applies (16-bit, <= 64 rows, single-tile decode projections); false: the
@@ -1194,6 +1222,10 @@ static bool launch_lean(const GemmArgs& g, hipStream_t s) {
     return false;
   } else {
     if (g.M > 64 || g.sel_val || g.st_out || g.addrow || g.tile || g.a_Mb || g.c_Mb || g.N % 16 || g.ldc % 4) return false;
+    // fragment-major operands (the runtime pairs fc1 → fc2 only where both take this path): a_fm needs
+    // the weights' fragment-major copy too (the residual writer table), c_fm the LN + GELU table
+    if (g.a_fm && (!g.W_fm || g.ln_w || g.a_grp_n)) return false;
+    if (g.c_fm && (!g.ln_w || !g.act)) return false;
     if (g.mode != 0 && g.mode != 2) return false;
     if (g.mode == 2 && (g.kv_rps > 1 || !g.kv_out || !g.pos || g.n_split % 64 || g.out_f32 || g.resid)) return false;
     if (g.a_grp_n) {   // q'_h = W_k,hᵀ q_h
@@ -1366,6 +1398,10 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
     // rows (measured C2: 1.074 vs 1.147 ms/token with 32-row workgroups); the LM head walks the
     // vocabulary persistently with 32-row workgroups, reading every weight tile once
     if (g.lean && launch_lean<T>(g, s)) return;
+    if (g.a_fm || g.c_fm) {   // the runtime pairs fragment-major operands only where the lean path takes both
+      fprintf(stderr, "wcb: internal error: fragment-major operand on a launch the lean kernel does not cover\n");
+      abort();
+    }
     const bool mf1 = (g.M <= 64 && !(g.sel_val && g.M > 16)) || g.K >= 4096;
     const bool ok = mf1 ? launch_dec_mf<T, 1>(g, s) : launch_dec_mf<T, 2>(g, s);
     if (ok) return;

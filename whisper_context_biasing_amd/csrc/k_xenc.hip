@@ -442,13 +442,13 @@ __global__ __launch_bounds__(256) void xenc_merge_kernel(XencArgs a, T* u, long 
 // 16 lanes per output (each 16-byte weight load of a lane group covers 256 contiguous bytes of a
 // W_v row), 64 outputs in 4 passes of the 4 waves. Every weight load is issued before the partials
 // arrive (they do not depend on them).
-template <typename T, int D>
+template <typename T, int D, int MS = kXencMaxSplit>
 __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* wv, const float* bv, T* out, long ldo) {
   using Frag = typename DT<T>::frag;
   constexpr int CPL = D / 128;          // 16-byte chunks per lane per output row (D/8 chunks over 16 lanes)
   const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ns = a.nsplit;
-  __shared__ float2 sv[kXencMaxSplit];
+  __shared__ float2 sv[MS];
   __shared__ __attribute__((aligned(16))) float us[D];
   // weights first: pass p, output j = 16p + 4·wave + (lane >> 4), chunks (k·16 + (lane & 15))
   Frag wf[4][CPL];
@@ -465,23 +465,23 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
   static_assert(D <= 1024, "one 4-column group per thread");
   const float* pp = a.part + ((long)b * ns * a.H + h) * D;
   const int c = min(tid * 4, D - 4);
-  f32x4 pv[kXencMaxSplit];
+  f32x4 pv[MS];
 #pragma unroll
-  for (int s = 0; s < kXencMaxSplit; ++s) pv[s] = *reinterpret_cast<const f32x4*>(pp + (long)min(s, ns - 1) * a.H * D + c);
+  for (int s = 0; s < MS; ++s) pv[s] = *reinterpret_cast<const f32x4*>(pp + (long)min(s, ns - 1) * a.H * D + c);
   const float2 mlv = *reinterpret_cast<const float2*>(a.ml + (((long)b * ns + min(tid, ns - 1)) * a.H + h) * 2);
-  if (tid < kXencMaxSplit) sv[tid] = tid < ns ? mlv : float2{0.f, 0.f};
+  if (tid < MS) sv[tid] = tid < ns ? mlv : float2{0.f, 0.f};
   __syncthreads();
-  float2 v[kXencMaxSplit];
+  float2 v[MS];
 #pragma unroll
-  for (int s = 0; s < kXencMaxSplit; ++s) v[s] = sv[s];
+  for (int s = 0; s < MS; ++s) v[s] = sv[s];
   float mx = -INFINITY;
 #pragma unroll
-  for (int s = 0; s < kXencMaxSplit; ++s)
+  for (int s = 0; s < MS; ++s)
     if (s < ns && v[s].y > 0.f) mx = fmaxf(mx, v[s].x);
-  float w[kXencMaxSplit];
+  float w[MS];
   float L = 0.f;
 #pragma unroll
-  for (int s = 0; s < kXencMaxSplit; ++s) {
+  for (int s = 0; s < MS; ++s) {
     w[s] = (s < ns && v[s].y > 0.f) ? __expf(v[s].x - mx) : 0.f;   // empty ranges publish Σp = 0
     L += w[s] * v[s].y;
   }
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
   {
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < kXencMaxSplit; ++s) acc += w[s] * pv[s];
+    for (int s = 0; s < MS; ++s) acc += w[s] * pv[s];
     acc *= inv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc[e] = DT<T>::tof(DT<T>::fromf(acc[e]));   // u in T, as stored unfused
@@ -773,7 +773,13 @@ void xenc_merge(DType t, const XencArgs& a, void* u, long ldu, hipStream_t s) {
 template <typename T>
 static void launch_merge_v_t(const XencArgs& a, const void* wv, const float* bv, void* o, long ldo, hipStream_t s) {
   const dim3 grid(a.H, a.rows);
-#define WCB_XC(DD) case DD: WCB_LAUNCH((xenc_merge_v_kernel<T, DD>), grid, dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo); break;
+  // MS: the partial loads per thread (the key-range count rounded up to 8 or 16; ranges past nsplit
+  // carry weight 0)
+#define WCB_XC(DD)                                                                                                    \
+  case DD:                                                                                                            \
+    if (a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8>), grid, dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo); \
+    else WCB_LAUNCH((xenc_merge_v_kernel<T, DD>), grid, dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo);            \
+    break;
   switch (a.D) { WCB_XC(128) WCB_XC(256) WCB_XC(384) WCB_XC(512) WCB_XC(768) WCB_XC(1024) default: break; }
 #undef WCB_XC
 }

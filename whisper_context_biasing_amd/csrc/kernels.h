@@ -92,6 +92,12 @@ struct GemmArgs {
   // fragment-major copy (frag_major, same K split) when the runtime built one
   int lean = 0;
   const void* W_fm = nullptr;
+  // lean path, fragment-major activations (fc1 → fc2): c_fm = write the output in the layout its
+  // consumer (K = this N, lean_cfg split) reads; a_fm = A is in that layout for this launch's split
+  int c_fm = 0, a_fm = 0;
+  // LDS-ring tiles (encoder GEMMs): tile order in bands of `raster` row panels, column tiles outer
+  // within a band (0: row-major tile order)
+  int raster = 0;
 };
 
 void gemm(DType t, const GemmArgs& g, hipStream_t s);

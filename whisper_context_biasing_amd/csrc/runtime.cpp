@@ -212,6 +212,9 @@ struct wcb_handle {
   // decode projections of <= 64 rows on dec_lean_kernel (gemm_impl.h; bit-identical to
   // gemm_dec_kernel, one kernel-argument round trip and one load burst per launch; option "lean")
   int lean = 1;
+  // encoder GEMM tile order (option "enc_raster"): bands of n row panels with the column tiles outer
+  // (GemmArgs::raster; 0 = row-major)
+  int enc_raster = 0;
   // decode projections on gemm_dec_kernel (K supported): the LayerNorm consumers compute their row
   // statistics from the rows they load, so the producers publish no per-16-column partial sums
   bool dec_gemm = false;
@@ -555,6 +558,9 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       h->ring_kt = value;
     } else if (n == "xqk") {
       h->xqk = value != 0;
+    } else if (n == "enc_raster") {
+      REQUIRE(value >= 0 && value <= 64, "option enc_raster: 0..64");
+      h->enc_raster = value;
     } else if (n == "lean") {
       h->lean = value != 0;
     } else if (n == "merge_v") {
@@ -851,7 +857,9 @@ void dgemm(wcb_handle* h, const char* cls, const GemmArgs& g, hipStream_t st) {
   h->timed(cls, 2.0 * g.M * g.N * g.K, gemm_bytes(h, g), st, [&] { gemm(h->dt, g, st); });
 }
 
-void run_gemm(wcb_handle* h, const char* cls, const GemmArgs& g) {
+void run_gemm(wcb_handle* h, const char* cls, const GemmArgs& g0) {
+  GemmArgs g = g0;
+  g.raster = h->enc_raster;
   h->timed(cls, 2.0 * g.M * g.N * g.K, 0.0, h->he, [&] { gemm(h->dt, g, h->he); });
 }
 
@@ -951,7 +959,7 @@ void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode
     D.dh.ensure((size_t)rows * d * e);
     D.dq.ensure((size_t)rows * d * e);
     D.datt.ensure((size_t)rows * d * e);
-    D.dffn.ensure((size_t)rows * h->d.ffn * e);
+    D.dffn.ensure((size_t)(rows + 15) / 16 * 16 * h->d.ffn * e);   // fragment-major: whole 16-row blocks
     D.dstats.ensure((size_t)rows * (d / 16) * 2 * 4);
     D.drst.ensure((size_t)rows * (d / 32) * 2 * 4);
     D.xpart.ensure(std::max((size_t)rows * h->H() * kXSplit * 66, (size_t)rows * h->xenc_split * h->H() * d) * 4);
@@ -1173,13 +1181,20 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     GemmArgs xo = drow(datt, d, w.xo_w, M, d, d, x, d);
     xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st_pub; xo.st_nb = nbk; xo.out16 = x16; xo.W_fm = w.xo_fm;
     proj("dec_xo", xo);
-    // MLP
+    // MLP. Lean path (<= 64 rows, 16-bit): fc1 writes its output fragment-major in the layout fc2's
+    // split of K = ffn reads (every A wave-instruction of fc2 then reads 1 KiB contiguous: its 98 KB of
+    // activations per workgroup at d = 768 were the largest operand of the decode step)
+    const bool afm = !tiled && h->lean && h->dt != kF32 && lna && w.fc1_fm && w.fc2_fm && M <= 64 &&
+                     (d == 512 || d == 768 || d == 1024 || d == 1280) &&
+                     (h->d.ffn == 2048 || h->d.ffn == 3072 || h->d.ffn == 4096 || h->d.ffn == 5120);
     GemmArgs f1 = drow(x, d, w.fc1_w, M, h->d.ffn, d, dffn, h->d.ffn);
     f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nbk; f1.ln_a16 = lna;
     f1.bias = w.fc1_b; f1.act = 1; f1.ln_u = w.ln2_u; f1.ln_c = w.ln2_c; f1.ln_wg = w.fc1_wg; f1.W_fm = w.fc1_fm;
+    f1.c_fm = afm;
     proj("dec_fc1", f1);
     GemmArgs f2 = drow(dffn, h->d.ffn, w.fc2_w, M, d, h->d.ffn, x, d);
     f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st_pub; f2.st_nb = nbk; f2.out16 = x16; f2.W_fm = w.fc2_fm;
+    f2.a_fm = afm;
     proj("dec_fc2", f2);
   }
   if (c.lm_head) {
