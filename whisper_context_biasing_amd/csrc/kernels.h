@@ -279,8 +279,22 @@ void scale_cols(DType t, const void* W, int N, int K, const float* gam, void* Wg
 // ks·32 + 8·(lane / 16) + e], so every weight wave-instruction reads 1 KiB contiguous (the row-major
 // MFMA B-fragment loads touch 16 rows × 64 B)
 void frag_major(DType t, const void* W, int N, int K, int nw, int kpw, void* dst, hipStream_t s);
-// (waves, k-steps per wave) of the lean decode projection at this K (false: not covered)
-bool lean_cfg(int K, int& nw, int& kpw);
+// (waves, k-steps per wave) of the lean decode projection at this K (false: not covered): the 16-bit
+// rows of gemm_impl.h launch_dec_mf, so the lean and general decode kernels split K alike
+inline bool lean_cfg(int K, int& nw, int& kpw) {
+  switch (K) {
+    case 64: nw = 2; kpw = 1; return true;
+    case 512: nw = 4; kpw = 4; return true;
+    case 768: nw = 4; kpw = 6; return true;
+    case 1024: nw = 4; kpw = 8; return true;
+    case 1280: nw = 8; kpw = 5; return true;
+    case 2048: nw = 8; kpw = 8; return true;
+    case 3072: nw = 8; kpw = 12; return true;
+    case 4096: nw = 16; kpw = 8; return true;
+    case 5120: nw = 16; kpw = 10; return true;
+    default: return false;
+  }
+}
 void fill_i32(int* p, int v, long n, hipStream_t s);
 // dst[0..n) = host values, passed by value in the kernel arguments (stream-ordered, no host buffer
 // lifetime or pageable-copy ordering to worry about)
