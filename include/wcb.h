@@ -115,7 +115,8 @@ int wcb_encode(wcb_handle* h, const float* mel, int B, void* enc_out, void* stre
  * [tf] generation/utils.py:3208) from [decoder_start] (+ optional prefix), bias boost,
  * out_ids int32 DEVICE [B][cfg->max_new_tokens] (finished rows padded with pad_token_id; beams: the
  * best finished sequence of each clip), *out_steps = number of generated columns (greedy: all rows
- * finished or max_new_tokens; beams: the longest best sequence). Beam search always blocks.
+ * finished or max_new_tokens; beams: the longest best sequence — with async_out, max_new_tokens: the
+ * length is not read back, columns past a clip's best sequence hold pad_token_id).
  * The front end/encoder run on one library stream and the decode on another, with two cross-K/V
  * buffers: call i+1's encoder overlaps call i's decode (async_out = 1 keeps `stream` free). */
 int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg, const wcb_bias* bias,

@@ -180,3 +180,20 @@ def test_greedy_and_beam_calls_interleave_on_one_handle():
     b3 = m.generate(x, max_length=20, num_beams=5).cpu().numpy()
     assert np.array_equal(g1, g2) and np.array_equal(b1, b3)
     assert np.array_equal(b2, generate_beam(om, enc=enc, num_beams=3, max_length=20))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_beam_async_output_equals_blocking(dtype):
+    """block=False beam search (the serving / bench pipeline: no host read-back of the best length) writes
+    every max_length column: the blocking call's generated columns, then pad_token_id."""
+    dims, om, mel, _ = case("tiny.en", 0, "diverse", 3)
+    m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=0, recipe="diverse"), dtype=dtype)
+    x = torch.from_numpy(mel)
+    ref = m.generate(x, max_length=10, num_beams=5, return_dict_in_generate=True).sequences[:, 1:].cpu().numpy()
+    out = m.generate(x, max_length=10, num_beams=5, block=False)
+    m.synchronize()
+    got = out.cpu().numpy()
+    assert got.shape == (3, 10)
+    L = ref.shape[1]
+    assert np.array_equal(got[:, :L], ref), (got, ref)
+    assert (got[:, L:] == dims.pad_token_id).all()

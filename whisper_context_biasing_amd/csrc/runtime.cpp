@@ -1504,8 +1504,14 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     }
     if (nb > 1) {   // best finished sequence of every utterance; its columns = the longest of them
       beam_output(bm, D.hs);
-      int olen = 0;
       HIPCHK(hipMemcpyAsync(out_ids, D.outbuf.p, (size_t)B * out_ld * 4, hipMemcpyDeviceToDevice, D.hs));
+      if (cfg->async_out) {   // serving pipelines: every max_new column (pad past each best sequence), no
+                              // host wait, so the next call's front end + encoder overlap this decode
+        HIPCHK(hipEventRecord(h->ev_dec[buf], D.hs));
+        *out_steps = max_new;
+        return;
+      }
+      int olen = 0;
       HIPCHK(hipMemcpyAsync(&olen, ints + I_UNFIN, 4, hipMemcpyDeviceToHost, D.hs));
       HIPCHK(hipEventRecord(h->ev_dec[buf], D.hs));
       HIPCHK(hipStreamSynchronize(D.hs));

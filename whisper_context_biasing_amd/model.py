@@ -292,7 +292,8 @@ class WhisperCB:
         `block=False` (serving pipelines): the caller's stream is not made to wait for the decode, so
         the next call's front end + encoder overlap this decode; the returned ids (and the inputs)
         must be kept alive and are valid only after `synchronize()`. Only meaningful with
-        `min_new_tokens >= max_length` (no early-exit polling).
+        `min_new_tokens >= max_length` (no early-exit polling). Beam search returns all `max_length`
+        columns then (pad past each clip's best sequence: its length is not read back).
         """
         if not self._loaded:
             raise _lib.WcbError("weights not loaded")
@@ -329,8 +330,6 @@ class WhisperCB:
         max_new = min(max_length, self.dims.n_text_ctx - len(prefix))
         if max_new < 1:
             raise ValueError("prompt leaves no room for new tokens")
-        if num_beams > 1:
-            block = True                           # the best-sequence length is read back on the host
         phrases = bias_list
         if phrases is None and bias_boost > 0 and bias_spans is not None:
             phrases = self._spans_to_phrases(bias_spans)
