@@ -442,14 +442,14 @@ __global__ __launch_bounds__(256) void xenc_merge_kernel(XencArgs a, T* u, long 
 // 16 lanes per output (each 16-byte weight load of a lane group covers 256 contiguous bytes of a
 // W_v row), 64 outputs in 4 passes of the 4 waves. Every weight load is issued before the partials
 // arrive (they do not depend on them).
-template <typename T, int D, int MS = kXencMaxSplit>
+template <typename T, int D, int MS = kXencMaxSplit, int RPW = 1>
 __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* wv, const float* bv, T* out, long ldo) {
   using Frag = typename DT<T>::frag;
   constexpr int CPL = D / 128;          // 16-byte chunks per lane per output row (D/8 chunks over 16 lanes)
-  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ns = a.nsplit;
-  __shared__ float2 sv[MS];
-  __shared__ __attribute__((aligned(16))) float us[D];
+  __shared__ float2 sv[RPW][MS];
+  __shared__ __attribute__((aligned(16))) float us[RPW][D];
   // weights first: pass p, output j = 16p + 4·wave + (lane >> 4), chunks (k·16 + (lane & 15))
   Frag wf[4][CPL];
 #pragma unroll
@@ -461,62 +461,72 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
   }
   // the range partials of this thread's 4 columns and the ranges' (max, Σp) go out in the same burst
   // as the weights (issued behind the (max, Σp) exchange they cost a second memory round trip);
-  // D <= 1024: one 4-column group per thread, threads past D re-load the last group and discard it
+  // D <= 1024: one 4-column group per thread, threads past D re-load the last group and discard it.
+  // RPW rows per workgroup share the head's W_v,h registers (rows past the batch re-read the last row)
   static_assert(D <= 1024, "one 4-column group per thread");
-  const float* pp = a.part + ((long)b * ns * a.H + h) * D;
   const int c = min(tid * 4, D - 4);
-  f32x4 pv[MS];
+  f32x4 pv[RPW][MS];
 #pragma unroll
-  for (int s = 0; s < MS; ++s) pv[s] = *reinterpret_cast<const f32x4*>(pp + (long)min(s, ns - 1) * a.H * D + c);
-  const float2 mlv = *reinterpret_cast<const float2*>(a.ml + (((long)b * ns + min(tid, ns - 1)) * a.H + h) * 2);
-  if (tid < MS) sv[tid] = tid < ns ? mlv : float2{0.f, 0.f};
-  __syncthreads();
-  float2 v[MS];
+  for (int r = 0; r < RPW; ++r) {
+    const int b = min(blockIdx.y * RPW + r, a.rows - 1);
+    const float* pp = a.part + ((long)b * ns * a.H + h) * D;
 #pragma unroll
-  for (int s = 0; s < MS; ++s) v[s] = sv[s];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int s = 0; s < MS; ++s)
-    if (s < ns && v[s].y > 0.f) mx = fmaxf(mx, v[s].x);
-  float w[MS];
-  float L = 0.f;
-#pragma unroll
-  for (int s = 0; s < MS; ++s) {
-    w[s] = (s < ns && v[s].y > 0.f) ? __expf(v[s].x - mx) : 0.f;   // empty ranges publish Σp = 0
-    L += w[s] * v[s].y;
+    for (int s = 0; s < MS; ++s) pv[r][s] = *reinterpret_cast<const f32x4*>(pp + (long)min(s, ns - 1) * a.H * D + c);
+    const float2 mlv = *reinterpret_cast<const float2*>(a.ml + (((long)b * ns + min(tid, ns - 1)) * a.H + h) * 2);
+    if (tid < MS) sv[r][tid] = tid < ns ? mlv : float2{0.f, 0.f};
   }
-  const float inv = 1.f / L;
-  {
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    float2 v[MS];
+#pragma unroll
+    for (int s = 0; s < MS; ++s) v[s] = sv[r][s];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < MS; ++s)
+      if (s < ns && v[s].y > 0.f) mx = fmaxf(mx, v[s].x);
+    float w[MS];
+    float L = 0.f;
+#pragma unroll
+    for (int s = 0; s < MS; ++s) {
+      w[s] = (s < ns && v[s].y > 0.f) ? __expf(v[s].x - mx) : 0.f;   // empty ranges publish Σp = 0
+      L += w[s] * v[s].y;
+    }
+    const float inv = 1.f / L;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < MS; ++s) acc += w[s] * pv[s];
+    for (int s = 0; s < MS; ++s) acc += w[s] * pv[r][s];
     acc *= inv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc[e] = DT<T>::tof(DT<T>::fromf(acc[e]));   // u in T, as stored unfused
-    if (tid * 4 < D) *reinterpret_cast<f32x4*>(us + c) = acc;
+    if (tid * 4 < D) *reinterpret_cast<f32x4*>(&us[r][c]) = acc;
   }
   __syncthreads();
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    float dsum = 0.f;
+  for (int r = 0; r < RPW; ++r) {
+    const int b = blockIdx.y * RPW + r;
 #pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-      const int c = (k * 16 + (lane & 15)) * 8;
-      const f32x4 u0 = *reinterpret_cast<const f32x4*>(us + c);
-      const f32x4 u1 = *reinterpret_cast<const f32x4*>(us + c + 4);
+    for (int p = 0; p < 4; ++p) {
+      float dsum = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float wv_e;
-        if constexpr (__is_same(T, bf16_t)) wv_e = bf16_to_f((bf16_t)wf[p][k][e]);
-        else wv_e = float(wf[p][k][e]);
-        dsum = fmaf(wv_e, e < 4 ? u0[e] : u1[e - 4], dsum);
+      for (int k = 0; k < CPL; ++k) {
+        const int cc = (k * 16 + (lane & 15)) * 8;
+        const f32x4 u0 = *reinterpret_cast<const f32x4*>(&us[r][cc]);
+        const f32x4 u1 = *reinterpret_cast<const f32x4*>(&us[r][cc + 4]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float wv_e;
+          if constexpr (__is_same(T, bf16_t)) wv_e = bf16_to_f((bf16_t)wf[p][k][e]);
+          else wv_e = float(wf[p][k][e]);
+          dsum = fmaf(wv_e, e < 4 ? u0[e] : u1[e - 4], dsum);
+        }
       }
-    }
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) dsum += __shfl_xor(dsum, o, 64);
-    if ((lane & 15) == 0) {
-      const int n = h * 64 + 16 * p + 4 * wave + (lane >> 4);
-      out[(long)b * ldo + n] = DT<T>::fromf(dsum + bv[n]);
+      for (int o = 1; o < 16; o <<= 1) dsum += __shfl_xor(dsum, o, 64);
+      if ((lane & 15) == 0 && b < a.rows) {
+        const int n = h * 64 + 16 * p + 4 * wave + (lane >> 4);
+        out[(long)b * ldo + n] = DT<T>::fromf(dsum + bv[n]);
+      }
     }
   }
 }
@@ -775,9 +785,13 @@ static void launch_merge_v_t(const XencArgs& a, const void* wv, const float* bv,
   const dim3 grid(a.H, a.rows);
   // MS: the partial loads per thread (the key-range count rounded up to 8 or 16; ranges past nsplit
   // carry weight 0)
+  // two rows per workgroup (the head's W_v,h registers serve both: half the weight re-reads) where the
+  // rows split evenly and the split count fits the 8-range form
 #define WCB_XC(DD)                                                                                                    \
   case DD:                                                                                                            \
-    if (a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8>), grid, dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo); \
+    if (a.nsplit <= 8 && a.rows % 2 == 0)                                                                             \
+      WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8, 2>), dim3(a.H, a.rows / 2), dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo); \
+    else if (a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8>), grid, dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo); \
     else WCB_LAUNCH((xenc_merge_v_kernel<T, DD>), grid, dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo);            \
     break;
   switch (a.D) { WCB_XC(128) WCB_XC(256) WCB_XC(384) WCB_XC(512) WCB_XC(768) WCB_XC(1024) default: break; }
