@@ -421,12 +421,14 @@ struct SelfLean {
   const void* q; const void* k; const void* v; void* o;
   const int* nkeys_dev;
   long k_sb, k_sh;
-  int ldq, ldo, H, cap, nkeys_add, row0, b_div;
+  int ldq, ldo, H, cap, nkeys_add, row0, b_div, npairs;
 };
 
-template <typename T>
-__global__ __launch_bounds__(64) void attn_self_lean_kernel(SelfLean a) {
-  const int b = blockIdx.y / a.H, h = blockIdx.y % a.H, lane = threadIdx.x;
+template <typename T, int WPG = 1>
+__global__ __launch_bounds__(64 * WPG) void attn_self_lean_kernel(SelfLean a) {
+  // WPG (row, head) pairs per workgroup, one per wave (pairs past the batch re-run the last one)
+  const int pair = min(blockIdx.y * WPG + (int)(threadIdx.x >> 6), a.npairs - 1);
+  const int b = pair / a.H, h = pair % a.H, lane = threadIdx.x & 63;
   const int seg = lane & 7, kg = lane >> 3;
   const long base = (long)((a.row0 + b) / a.b_div) * a.k_sb + (long)h * a.k_sh + seg * 8;
   const T* kb = reinterpret_cast<const T*>(a.k) + base;
@@ -498,7 +500,10 @@ static void launch_decode(const AttnArgs& b, dim3 grid, int variant, hipStream_t
       c.q = b.q; c.k = b.k; c.v = b.v; c.o = b.o; c.nkeys_dev = b.nkeys_dev;
       c.k_sb = b.k_sb; c.k_sh = b.k_sh; c.ldq = (int)b.ldq; c.ldo = (int)b.ldo; c.H = b.H;
       c.cap = b.kv_rows - 1; c.nkeys_add = b.nkeys_add; c.row0 = b.row0; c.b_div = b.b_div > 0 ? b.b_div : 1;
-      WCB_LAUNCH((attn_self_lean_kernel<T>), dim3(1, grid.y), dim3(64), 0, s, c);
+      c.npairs = (int)grid.y;
+      // one (row, head) pair per 64-thread workgroup (4 per 256-thread workgroup measured 0.5 ms slower per
+      // 72-token C2 call, tools/decode_ab.py)
+      WCB_LAUNCH((attn_self_lean_kernel<T, 1>), dim3(1, grid.y), dim3(64), 0, s, c);
       return;
     }
     if (b.phys) WCB_LAUNCH((attn_self_kernel<T, true>), dim3(1, grid.y), dim3(64), 0, s, b);
