@@ -122,6 +122,22 @@ int wcb_encode(wcb_handle* h, const float* mel, int B, void* enc_out, void* stre
 int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg, const wcb_bias* bias,
                  const int32_t* prefix, int prefix_len, int32_t* out_ids, int32_t* out_steps, void* stream);
 
+/* Step-wise greedy decoding (SURVEY §8(b) wcb_decode_begin / wcb_decode_step): the decode step of
+ * wcb_generate one token per call, for callers that inspect every step (the reference's surface is
+ * generate(); this is the streaming form of it). `enc` = encoder output [B][1500][d] in the model dtype
+ * (DEVICE, copied / projected at begin: not retained), `prefix` = per-row prompt [B][prefix_len] (HOST,
+ * NULL: decoder_start_token_id only; positions 0 .. prefix_len-2 are prefilled, the last one is the first
+ * step's input), num_beams must be 1 (beam search reorders past tokens: wcb_generate), EOS masked while
+ * fewer than min_new_tokens were generated. One active state per handle (it owns decode context 3, so
+ * decode_contexts must be <= 3). wcb_decode_step writes next_ids [B] (int32, DEVICE) and, when non-NULL,
+ * scores [B] (f32, DEVICE: the chosen token's logit + bias boost; 0 for finished rows); finished rows
+ * emit pad_token_id. The bias automaton must be the same (or NULL) at every step of one decode. */
+typedef struct wcb_state wcb_state;
+int wcb_decode_begin(wcb_handle* h, const void* enc, int B, int num_beams, const int32_t* prefix, int prefix_len,
+                     float bias_boost, int min_new_tokens, wcb_state** out, void* stream);
+int wcb_decode_step(wcb_handle* h, wcb_state* st, const wcb_bias* bias, int32_t* next_ids, float* scores, void* stream);
+int wcb_decode_end(wcb_handle* h, wcb_state* st);
+
 /* wait for every queued front-end / encoder / decode operation of the handle */
 int wcb_synchronize(wcb_handle* h);
 

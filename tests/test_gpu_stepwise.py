@@ -1,0 +1,38 @@
+"""GPU: step-wise greedy decoding (wcb_decode_begin / wcb_decode_step) against
+generate() on the same clips: the same decode step one token per call, so the ids must be identical
+(f32 K/V cross-attention and bf16 encoder-space paths, the bias boost, a prompt prefix)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import whisper_np as W  # noqa: E402
+from whisper_context_biasing_amd.config import get_dims  # noqa: E402
+from whisper_context_biasing_amd.model import WhisperCB  # noqa: E402
+from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list  # noqa: E402
+from whisper_context_biasing_amd.weights import make_weights  # noqa: E402
+
+
+@pytest.mark.parametrize("size,dtype,prompt", [("tiny.en", "f32", False), ("small", "bf16", False),
+                                               ("small", "bf16", True)])
+def test_stepwise_decode_equals_generate(size, dtype, prompt):
+    dims = get_dims(size)
+    m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=0, recipe="diverse"), dtype=dtype)
+    B, n = 4, 12
+    x = torch.from_numpy(W.log_mel(synth_batch(B), dims.n_mel))
+    phrases = synth_bias_list(200, eot=dims.eos_token_id)
+    pr = [50360, 1000, 2000, 3000] if prompt else None   # <|startofprev|>-style prefix tokens
+    ref = m.generate(x, max_length=n, min_new_tokens=n, bias_list=phrases, bias_boost=2.0, prompt_ids=pr,
+                     return_dict_in_generate=True).sequences
+    ref = ref[:, ref.shape[1] - n:].cpu().numpy()
+    dec = m.decode_begin(m.encode(x), prompt_ids=pr, bias_list=phrases, bias_boost=2.0, min_new_tokens=n)
+    ids, scores = zip(*[dec.step() for _ in range(n)])
+    dec.close()
+    got = torch.stack(ids, 1).cpu().numpy()
+    assert np.array_equal(got, ref), (got, ref)
+    assert torch.isfinite(torch.stack(scores)).all()
+    # a second decode on the same handle (the state was released)
+    dec = m.decode_begin(m.encode(x), min_new_tokens=2)
+    dec.step()
+    dec.close()

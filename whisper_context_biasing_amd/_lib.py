@@ -47,6 +47,9 @@ SIGNATURES = {
     "wcb_generate": (C.c_int, [_P, _P, C.c_int, C.POINTER(WcbGenCfg), _P, _P, C.c_int, _P,
                                C.POINTER(C.c_int32), _P]),
     "wcb_synchronize": (C.c_int, [_P]),
+    "wcb_decode_begin": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_float, C.c_int, C.POINTER(_P), _P]),
+    "wcb_decode_step": (C.c_int, [_P, _P, _P, _P, _P, _P]),
+    "wcb_decode_end": (C.c_int, [_P, _P]),
     "wcb_forward": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, _P, _P, _P]),
     "wcb_bias_create": (C.c_int, [_P, _P, _P, C.c_int, _P, C.POINTER(_P)]),
     "wcb_bias_destroy": (None, [_P]),

@@ -106,6 +106,7 @@ __global__ __launch_bounds__(64) void select_finalize_kernel(SelectArgs a) {
     a.rowbase[m] = a.st_keep[dst] - a.st_depth[dst];
     a.next_ids[m] = tok;
     a.out_ids[(long)m * a.out_ld + step] = tok;
+    if (a.out_score) a.out_score[m] = fin ? 0.f : bv;
     const bool nf = fin || tok == a.eos;
     a.finished[m] = nf ? 1 : 0;
     if (!nf) atomicAdd(a.unfinished, 1);

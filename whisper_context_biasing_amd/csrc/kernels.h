@@ -213,6 +213,7 @@ struct SelectArgs {
   float* part_val = nullptr; int* part_idx = nullptr; int nchunk = 0;
   int* all_done = nullptr;
   int* ticket = nullptr; int* unfinished = nullptr;   // zero between steps (reset by the last row)
+  float* out_score = nullptr;        // optional: the chosen token's (boosted) logit per row (0 for finished rows)
 };
 void select_greedy(const SelectArgs& a, hipStream_t s);          // vocabulary pass + finalize
 void select_finalize(const SelectArgs& a, hipStream_t s);        // partials already written (fused LM head)

@@ -212,6 +212,7 @@ struct wcb_handle {
   // decode projections of <= 64 rows on dec_lean_kernel (gemm_impl.h; bit-identical to
   // gemm_dec_kernel, one kernel-argument round trip and one load burst per launch; option "lean")
   int lean = 1;
+  struct wcb_state* step_state = nullptr;   // the active step-wise decode (wcb_decode_begin), if any
   // encoder GEMM tile order (option "enc_raster"): bands of n row panels with the column tiles outer
   // (GemmArgs::raster; 0 = row-major)
   int enc_raster = 0;
@@ -934,21 +935,24 @@ int prefill_chunk(int R) { return std::max(1, kPrefillRows / std::max(R, 1)); }
 
 // decode workspace: B decoder rows (clips x beams) reading `clips` encoder outputs; activation
 // buffers for `rows` >= B rows (a prefill pass carries several positions per decoder row)
-void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode, int rows = 0) {
+// contexts [c0, c1) (default: the generate() contexts 0 .. nctx-1; the step-wise decode state owns
+// context kMaxCtx-1)
+void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode, int rows = 0, int c0 = 0, int c1 = -1) {
+  if (c1 < 0) c1 = h->nctx;
   rows = std::max(rows, B);
   const size_t e = esize(h->d.dtype), d = h->d.d_model, L = h->d.n_layers, S = h->S();
-  const DecCtx& D0 = h->dc[h->nctx - 1];   // every context is sized together
+  const DecCtx& D0 = h->dc[c1 - 1];   // every context of the range is sized together
   const size_t xbuf = xmode ? (size_t)clips * S * d * e : 2 * L * (size_t)clips * S * d * e;
   const size_t need[] = {xbuf, 2 * L * (size_t)B * T * d * e, (size_t)rows * d * 4,
                          (size_t)rows * h->d.ffn * e, (size_t)B * h->vocab_pad * 4, (size_t)(I_NEXT + 4 * B + 16) * 4,
                          (size_t)B * out_ld * 4};
-  const DevBuf* have[] = {&h->xkv2[h->nctx - 1], &D0.kvself, &D0.dx, &D0.dffn, &D0.logits, &D0.ints, &D0.outbuf};
+  const DevBuf* have[] = {&h->xkv2[c1 - 1], &D0.kvself, &D0.dx, &D0.dffn, &D0.logits, &D0.ints, &D0.outbuf};
   bool grow = false;
   for (int i = 0; i < 7; ++i) grow |= need[i] > have[i]->bytes;
   if (!grow && B <= D0.dec_B && T <= D0.dec_T) return;
   quiesce(h);
   drop_graphs(h);
-  for (int ci = 0; ci < h->nctx; ++ci) {
+  for (int ci = c0; ci < c1; ++ci) {
     DecCtx& D = h->dc[ci];
     h->xkv2[ci].ensure(need[0]);
     D.kvself.ensure(need[1]);
@@ -998,6 +1002,7 @@ struct StepCfg {
   const int* phys = nullptr;           // beam search: cache row of every key position [B][T]
   const BeamArgs* beam = nullptr;      // beam search selection (replaces the greedy select)
   int rps = 1;                         // positions per decoder row in this pass (> 1: causal prefill)
+  float* score_out = nullptr;          // greedy select: the chosen token's (boosted) logit per row (step-wise API)
 };
 
 // the folded LayerNorm of the > 64-row projections is available (16-bit, d a multiple of 32)
@@ -1272,6 +1277,7 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     s.part_val = D.part_val.as<float>(); s.part_idx = D.part_idx.as<int>(); s.nchunk = D.nchunk;
     s.all_done = ints + I_DONE;
     s.ticket = ints + I_TICKET; s.unfinished = ints + I_UNFIN;
+    s.out_score = c.score_out;
     h->timed("dec_select", 0, (double)B * D.nchunk * 8, D.hs, [&] { select_finalize(s, D.hs); });
   } else {
     advance_forced(next_ids, c.forced, B, c.forced_ld, pos, D.hs);
@@ -1523,6 +1529,105 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     HIPCHK(hipEventRecord(h->ev_dec[buf], D.hs));
     *out_steps = std::min(done, max_new);
     if (!cfg->async_out) sync_out(h, stream, D.hs);
+  });
+}
+
+// ---- step-wise greedy decoding (SURVEY §8(b) wcb_decode_begin / wcb_decode_step): the decode step
+// of wcb_generate, one token per call, on the decode context kMaxCtx-1 (its own stream and buffers,
+// so generate() calls on contexts 0 .. nctx-1 are unaffected); eager launches (the caller inspects
+// every step). One active state per handle.
+struct wcb_state {
+  wcb_handle* h = nullptr;
+  int B = 0, P = 1, T = 0, steps = 0, max_new = 0, min_new = 0, xmode = 1;
+  float lam = 0.f;
+  uint64_t bias_id = 0;
+};
+
+int wcb_decode_begin(wcb_handle* h, const void* enc, int B, int num_beams, const int32_t* prefix, int prefix_len,
+                     float bias_boost, int min_new_tokens, wcb_state** out, void* stream) {
+  return guarded(h, [&] {
+    REQUIRE(h && enc && out && B > 0 && B <= 64, "bad argument (1 <= B <= 64, enc and out required)");
+    if (!h->ready) throw WcbError(WCB_ERR_STATE, "weights not finalized");
+    REQUIRE(num_beams == 1, "step-wise decoding is greedy: beam search reorders past tokens, use wcb_generate");
+    REQUIRE(h->nctx < wcb_handle::kMaxCtx, "step-wise decoding needs a free decode context (decode_contexts <= 3)");
+    REQUIRE(!h->step_state, "a step-wise decode is already active on this handle (wcb_decode_end first)");
+    REQUIRE(bias_boost >= 0.f && min_new_tokens >= 0, "bias_boost and min_new_tokens must be >= 0");
+    const int P = prefix ? prefix_len : 1;
+    REQUIRE(P >= 1 && P < h->d.n_text_ctx, "prefix_len must be in [1, max_target_positions)");
+    const int ci = wcb_handle::kMaxCtx - 1;
+    const int T = h->d.n_text_ctx, max_new = h->d.n_text_ctx - P;
+    const int xm = h->xmode;
+    ensure_dec_ws(h, B, B, T, max_new, xm, P > 1 ? B * std::min(prefill_chunk(B), P - 1) : B, ci, ci + 1);
+    DecCtx& D = h->dc[ci];
+    sync_in(h, stream, D.hs);
+    // the caller's encoder output [B][1500][d] (model dtype) is copied / projected into owned buffers
+    const size_t e = esize(h->d.dtype);
+    if (xm == 1) {
+      HIPCHK(hipMemcpyAsync(h->xkv2[ci].p, enc, (size_t)B * h->S() * h->d.d_model * e, hipMemcpyDeviceToDevice, D.hs));
+    } else {
+      sync_in(h, stream, h->he);
+      cross_kv(h, B, ci, enc);                        // on the encoder stream
+      HIPCHK(hipStreamSynchronize(h->he));
+    }
+    int* ints = D.ints.as<int>();
+    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 4 * B) * 4, D.hs));
+    if (prefix) {   // per-row prefixes [B][P] (host), positions 0 .. P-2 prefilled, P-1 is the first input
+      if ((size_t)B * P * 4 > D.forced.bytes) { quiesce(h); D.forced.ensure((size_t)B * P * 4); }
+      HIPCHK(hipMemcpyAsync(D.forced.p, prefix, (size_t)B * P * 4, hipMemcpyHostToDevice, D.hs));
+      HIPCHK(hipStreamSynchronize(D.hs));   // pageable host source
+    } else {
+      fill_i32(ints + I_NEXT, h->d.decoder_start_token_id, B, D.hs);
+    }
+    StepCfg sc{B, T, max_new, ci, false, false, D.logits.as<float>(), (long)h->vocab_pad, h->empty_bias.get(),
+               bias_boost, min_new_tokens, D.forced.as<int>(), P};
+    sc.clips = B;
+    sc.xmode = xm;
+    for (int p0 = 0, np; p0 + 1 < P; p0 += np) {
+      np = std::min(prefill_chunk(B), P - 1 - p0);
+      prefill_step(h, sc, np, D.forced.as<int>(), P);
+    }
+    if (prefix) gather_col(ints + I_NEXT, D.forced.as<int>(), B, P, P - 1, D.hs);
+    HIPCHK(hipStreamSynchronize(D.hs));
+    auto* st = new wcb_state;
+    st->h = h; st->B = B; st->P = P; st->T = T; st->max_new = max_new; st->min_new = min_new_tokens;
+    st->xmode = xm; st->lam = bias_boost;
+    h->step_state = st;
+    *out = st;
+    sync_out(h, stream, D.hs);
+  });
+}
+
+int wcb_decode_step(wcb_handle* h, wcb_state* st, const wcb_bias* bias, int32_t* next_ids, float* scores, void* stream) {
+  return guarded(h, [&] {
+    REQUIRE(h && st && st->h == h && h->step_state == st && next_ids, "bad argument (state of this handle, next_ids)");
+    REQUIRE(st->steps < st->max_new, "max_target_positions reached");
+    const wcb_bias* bs = bias ? bias : h->empty_bias.get();
+    REQUIRE(bs == h->empty_bias.get() || bs->owner == h, "bias automaton was created on another handle");
+    REQUIRE(bs->vocab == h->d.vocab, "bias automaton built for another vocabulary");
+    REQUIRE(st->steps == 0 || bs->id == st->bias_id, "the bias automaton must stay the same for the whole decode");
+    const int ci = wcb_handle::kMaxCtx - 1;
+    DecCtx& D = h->dc[ci];
+    sync_in(h, stream, D.hs);
+    StepCfg sc{st->B, st->T, st->max_new, ci, true, true, D.logits.as<float>(), (long)h->vocab_pad, bs, st->lam,
+               st->min_new, D.forced.as<int>(), 0};
+    sc.clips = st->B;
+    sc.xmode = st->xmode;
+    sc.host_pos = st->P - 1 + st->steps;
+    sc.score_out = scores;
+    decode_step(h, sc);
+    HIPCHK(hipMemcpyAsync(next_ids, D.ints.as<int>() + I_NEXT, (size_t)st->B * 4, hipMemcpyDeviceToDevice, D.hs));
+    st->bias_id = bs->id;
+    ++st->steps;
+    sync_out(h, stream, D.hs);
+  });
+}
+
+int wcb_decode_end(wcb_handle* h, wcb_state* st) {
+  return guarded(h, [&] {
+    REQUIRE(h && st && st->h == h && h->step_state == st, "bad argument (state of this handle)");
+    HIPCHK(hipStreamSynchronize(h->dc[wcb_handle::kMaxCtx - 1].hs));
+    h->step_state = nullptr;
+    delete st;
   });
 }
 

@@ -83,6 +83,33 @@ class BiasList:
             self._h = None
 
 
+class StepDecoder:
+    """One step-wise greedy decode (WhisperCB.decode_begin): step() -> (next ids [B] int32, scores [B]
+    f32: the chosen token's logit + bias boost), both on the model's device; close() ends it."""
+
+    def __init__(self, model, st, B, bias):
+        self.model, self._st, self.B, self._bias = model, st, B, bias
+
+    def step(self):
+        m = self.model
+        ids = torch.empty(self.B, dtype=torch.int32, device=m.device)
+        sc = torch.empty(self.B, dtype=torch.float32, device=m.device)
+        _lib.check(m._lib.wcb_decode_step(m._h, self._st, self._bias._h if self._bias else None, _ptr(ids), _ptr(sc),
+                                          _stream(m.device)), m._h, "wcb_decode_step")
+        return ids, sc
+
+    def close(self):
+        if self._st:
+            _lib.check(self.model._lib.wcb_decode_end(self.model._h, self._st), self.model._h, "wcb_decode_end")
+            self._st = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class WhisperCB:
     main_input_name = "input_features"
 
@@ -352,6 +379,27 @@ class WhisperCB:
             sot = torch.tensor(prefix, dtype=torch.int64, device=self.device)[None].expand(B, -1)
             return GenerateOutput(sequences=torch.cat([sot, ids], dim=1))
         return self._whisper_trim(ids)
+
+    def decode_begin(self, encoder_outputs, prompt_ids=None, bias_list=None, bias_boost: float = 0.0,
+                     min_new_tokens: int = 0) -> "StepDecoder":
+        """Step-wise greedy decoding from an encoder output [B, 1500, d] (this model's dtype, on its device):
+        the streaming form of generate() (wcb_decode_begin). `prompt_ids` = one prompt for every row or
+        a [B, P] array of per-row prompts (decoder_start_token_id is appended as generate() does)."""
+        enc = encoder_outputs.to(self.device, self.torch_dtype).contiguous()
+        B = enc.shape[0]
+        start = self.dims.decoder_start_token_id
+        if prompt_ids is None:
+            pre = None
+        else:
+            p = np.asarray(prompt_ids, dtype=np.int32)
+            p = np.broadcast_to(p, (B, p.shape[-1])) if p.ndim == 1 else p
+            pre = np.ascontiguousarray(np.concatenate([p, np.full((B, 1), start, np.int32)], axis=1))
+        bl = self.bias_list(bias_list) if (bias_list and bias_boost > 0) else None
+        st = C.c_void_p()
+        _lib.check(self._lib.wcb_decode_begin(self._h, _ptr(enc), B, 1, pre.ctypes.data if pre is not None else None,
+                                              pre.shape[1] if pre is not None else 1, float(bias_boost), int(min_new_tokens),
+                                              C.byref(st), _stream(self.device)), self._h, "wcb_decode_begin")
+        return StepDecoder(self, st, B, bl)
 
     @staticmethod
     def max_clips_per_call(num_beams: int = 1) -> int:
