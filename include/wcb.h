@@ -70,7 +70,10 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "xqk" 0/1          greedy encoder-space cross-attention query: LN + q_proj + W_k,hᵀ in one launch (1) or
  *                      two decode GEMMs (0, default: measured faster); bit-identical
  *   "lean" 0/1         decode projections of <= 64 rows (16-bit) on the lean single-tile kernel (1, default)
- *                      or the general decode GEMM (0); bit-identical
+ *                      or the general decode GEMM (0); bit-identical. With it the LM head reads the token
+ *                      embedding's fragment-major copy (built at finalize, vocab_pad x d_model 16-bit)
+ *   "lean_x" 0/1       lean path, one position per row: the residual writers also write the 16-bit rows
+ *                      fragment-major for the LayerNorm-fused QKV / xq / fc1 (1, default); bit-identical
  *   "decode_contexts" n  decode contexts in flight (1..4): calls decode on n streams from n buffers
  *   "ring_kt" 1/2      decode rows > 64: 64-deep K sub-tiles per LDS-ring stage of the projection tiles
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)

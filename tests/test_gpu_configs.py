@@ -299,11 +299,34 @@ def test_lean_decode_projections_bit_identical(size, dtype, B):
     x = mel_of(dims, B)
     phrases = synth_bias_list(1000, eot=dims.eos_token_id)
     out = []
-    for lean in (1, 0):
-        m = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options={"lean": lean})
+    for opts in ({"lean": 1}, {"lean": 1, "lean_x": 0}, {"lean": 0}):
+        m = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options=opts)
         out.append(m.generate(x, max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0).cpu().numpy())
         del m
-    assert np.array_equal(out[0], out[1]), np.argwhere(out[0] != out[1])[:8]
+    for o in out[1:]:
+        assert np.array_equal(out[0], o), np.argwhere(out[0] != o)[:8]
+
+
+@pytest.mark.parametrize("B,group_rows", [(24, 16), (40, 16), (5, 512)])
+def test_lean_fragment_major_residual_logits(B, group_rows):
+    """The residual's fragment-major copy (option "lean_x": embedding and out / xo / fc2 write it, QKV /
+    xq / fc1 read it) carries the same 16-bit values in another order: teacher-forced logits through the
+    prefill pass and eager steps, and greedy ids with row chains whose first row does not start a
+    16-row block (those chains read the row layout), are bit-identical to lean_x = 0 (whisper-small)."""
+    dims = get_dims("small")
+    sd = weights("small", 0, "diverse")
+    x = mel_of(dims, B)
+    rng = np.random.default_rng(B)
+    dec = np.concatenate([np.full((B, 1), dims.decoder_start_token_id), rng.integers(0, 50000, (B, 3))], 1)
+    phrases = synth_bias_list(200, eot=dims.eos_token_id)
+    logits, ids = [], []
+    for lx in (1, 0):
+        m = WhisperCB.from_state_dict(dims, sd, dtype="bf16", options={"lean_x": lx, "group_rows": group_rows})
+        logits.append(m.forward(x, decoder_input_ids=torch.from_numpy(dec)).logits.float().cpu())
+        ids.append(m.generate(x, max_length=20, min_new_tokens=20, bias_list=phrases, bias_boost=2.0).cpu().numpy())
+        del m
+    assert torch.equal(logits[0], logits[1])
+    assert np.array_equal(ids[0], ids[1]), np.argwhere(ids[0] != ids[1])[:8]
 
 
 @pytest.mark.parametrize("raster", [4, 8])

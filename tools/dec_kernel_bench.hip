@@ -168,6 +168,94 @@ void run_wfm(const char* name, GemmArgs g0, bool stamped) {
   fflush(stdout);
 }
 
+// weights cold in HBM vs Infinity-Cache resident, activations written by the previous launch vs
+// constant: the lean d x d projection (EPI 0, fragment-major W), `nl` launches per graph (100: 118 MB
+// of weights, replays hit the 256 MB Infinity Cache; 850: 1 GB, every replay from HBM)
+void run_cold(int nl, bool fresh) {
+  const long wbytes = 768L * 768 * 2;
+  const long nreg = (long)(kW / wbytes);
+  double us = time_graph(nl, [&](int i, hipStream_t s) {
+    DecLean<bf16_t> p;
+    p.W = reinterpret_cast<const bf16_t*>(g_w + (i % nreg) * wbytes);
+    bf16_t* a0 = g_a;
+    bf16_t* a1 = g_a + 32 * 768;
+    p.A = fresh ? ((i & 1) ? a1 : a0) : a0;
+    p.out = fresh ? ((i & 1) ? a0 : a1) : g_out;
+    p.bias = g_bias; p.gam = p.bet = nullptr; p.x = nullptr; p.kv = nullptr; p.pos = g_pos;
+    p.M = 32; p.N = 768; p.lda = 768; p.ldo = 768; p.n_split = 0; p.kvB = p.kvH = p.kvT = 0; p.grp_n = p.grp_off = 0;
+    hipLaunchKernelGGL((dec_lean_kernel<bf16_t, 1, 4, 6, false, 0, false, false, true>), dim3(48, 2), dim3(256), 0, s, p);
+  });
+  printf("lean d x d, fragment-major W: %4d launches/graph (%s weights), %s activations: %6.2f us/launch\n", nl,
+         nl * wbytes > (300L << 20) ? "HBM-cold" : "cache-resident", fresh ? "fresh (previous launch's output)" : "constant", us);
+  fflush(stdout);
+}
+
+// instruction-cache pressure: the same d x d projection chain, one kernel object vs a cycle through
+// 8 distinct instances of the lean kernel (different code, same work: EPI 0 with/without GELU, LN
+// on/off, 4 / 8 waves)
+template <int NW, int KPW, bool LN, bool GELU>
+void launch_var(int i, hipStream_t s) {
+  const long wbytes = 768L * 768 * 2;
+  const long nreg = (long)(kW / wbytes);
+  DecLean<bf16_t> p;
+  p.W = reinterpret_cast<const bf16_t*>(g_w + (i % nreg) * wbytes);
+  bf16_t* a0 = g_a;
+  bf16_t* a1 = g_a + 32 * 768;
+  p.A = (i & 1) ? a1 : a0;
+  p.out = (i & 1) ? a0 : a1;
+  p.bias = g_bias; p.gam = g_lnw; p.bet = g_lnb; p.x = nullptr; p.kv = nullptr; p.pos = g_pos;
+  p.M = 32; p.N = 768; p.lda = 768; p.ldo = 768; p.n_split = 0; p.kvB = p.kvH = p.kvT = 0; p.grp_n = p.grp_off = 0;
+  hipLaunchKernelGGL((dec_lean_kernel<bf16_t, 1, NW, KPW, LN, 0, GELU, false, true>), dim3(48, 2), dim3(NW * 64), 0, s, p);
+}
+void run_icache() {
+  double one = time_graph(400, [&](int i, hipStream_t s) { launch_var<4, 6, false, false>(i, s); });
+  double cyc = time_graph(400, [&](int i, hipStream_t s) {
+    switch (i % 8) {
+      case 0: launch_var<4, 6, false, false>(i, s); break;
+      case 1: launch_var<4, 6, false, true>(i, s); break;
+      case 2: launch_var<4, 6, true, false>(i, s); break;
+      case 3: launch_var<4, 6, true, true>(i, s); break;
+      case 4: launch_var<8, 3, false, false>(i, s); break;
+      case 5: launch_var<8, 3, false, true>(i, s); break;
+      case 6: launch_var<8, 3, true, false>(i, s); break;
+      default: launch_var<8, 3, true, true>(i, s); break;
+    }
+  });
+  double cyc_ln = time_graph(400, [&](int i, hipStream_t s) {   // the LN half alone, 2 objects
+    if (i & 1) launch_var<4, 6, true, false>(i, s); else launch_var<4, 6, true, true>(i, s);
+  });
+  printf("icache: one kernel object %6.2f us/launch, 8 objects cycled %6.2f us/launch, 2 LN objects %6.2f\n", one, cyc, cyc_ln);
+  fflush(stdout);
+}
+
+// the LM head: persistent column walk (gemm_dec_kernel P), LN-fused, argmax partials, with and
+// without the bias boost (root bits read per tile)
+void run_lm_head(bool boost) {
+  const int V = 51865, K = 768, M = 32;
+  static uint32_t* bits = nullptr;
+  static float *pv = nullptr;
+  static int *pi = nullptr, *rb = nullptr, *step = nullptr;
+  if (!bits) {
+    CHK(hipMalloc(&bits, (V / 32 + 1) * 4)); CHK(hipMemset(bits, 0x55, (V / 32 + 1) * 4));
+    CHK(hipMalloc(&pv, M * kDecWalkers * 4)); CHK(hipMalloc(&pi, M * kDecWalkers * 4));
+    CHK(hipMalloc(&rb, M * 4)); CHK(hipMemset(rb, 0, M * 4));
+    CHK(hipMalloc(&step, 4)); CHK(hipMemset(step, 0, 4));
+  }
+  const long wbytes = (long)V * K * 2;
+  double us = time_graph(20, [&](int i, hipStream_t s) {
+    GemmArgs g = base(V, K, 0);
+    g.M = M; g.ldc = V;
+    g.W = g_w + (i % 8) * wbytes;
+    g.A = g_x; g.lda = K; g.ln_w = g_lnw; g.ln_b = g_lnb; g.ln_a16 = g_x16; g.out_f32 = 1; g.out = nullptr;
+    g.sel_val = pv; g.sel_idx = pi; g.sel_root_bits = bits; g.sel_lam = boost ? 2.f : 0.f; g.sel_rowbase = rb;
+    g.sel_eos = 50257; g.sel_step = step; g.sel_min_new = 0;
+    const int gx = std::min((V + 15) / 16, kDecWalkers);
+    hipLaunchKernelGGL((gemm_dec_kernel<bf16_t, 2, 4, 6, 2, true>), dim3(gx, 1), dim3(256), 0, s, g);
+  });
+  printf("lm head (V=%d, 32 rows, %d walkers)%s: %6.2f us/launch\n", V, kDecWalkers, boost ? " + boost" : "", us);
+  fflush(stdout);
+}
+
 template <int NT, int WPL, int APL>
 void run_stream(const char* name, int grid) {
   const long per_wg = (long)NT * WPL, per_launch = per_wg * grid;
@@ -210,6 +298,13 @@ int main() {
   run_stream<256, 6, 6>("stream: out-proj bytes", 96);
   run_stream<256, 6, 6>("stream: out-proj bytes, 192 wgs", 192);
 
+  run_lm_head(false);
+  run_lm_head(true);
+  run_icache();
+  run_cold(100, false);
+  run_cold(850, false);
+  run_cold(100, true);
+  run_cold(850, true);
   // out / xo projection: A = T rows, bias, residual f32 in place, 16-bit copy
   GemmArgs o = base(768, 768, 0);
   o.A = g_a; o.bias = g_bias; o.resid = g_x; o.out = g_x; o.out_f32 = 1; o.out16 = g_x16;

@@ -754,7 +754,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(GemmArgs g) {
 //    one (row, column) output: bias, GELU, residual, f32 / T / x16 stores, KV-cache append (mode 2),
 //    per-16-column LN partial sums (st_out, the older skinny consumers) and the LM head's argmax
 //    partial (sel_val: per workgroup and row, the running best over the tiles it walks).
-template <typename T, int MF, int NW, int KPW, int AM, bool P>
+template <typename T, int MF, int NW, int KPW, int AM, bool P, bool WFM = false>
 __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
   using Frag = typename DT<T>::frag;
   constexpr int NT = NW * 64, K = NW * KPW * 32, R = MF * 16;
@@ -771,10 +771,16 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
   const bool mask_eos = g.sel_val && *g.sel_step < g.sel_min_new;
 
   auto load_w = [&](Frag (&w)[KPW], int ct) {
-    const long n = min(ct * 16 + (lane & 15), g.N - 1);
-    const T* W = reinterpret_cast<const T*>(g.W) + n * g.ldw + kb;
+    if constexpr (WFM) {   // fragment-major copy (kernels.h frag_major, this NW / KPW): 1 KiB per wave-instruction
+      const T* W = reinterpret_cast<const T*>(g.W_fm) + (((long)ct * NW + wave) * KPW * 64 + lane) * 8;
 #pragma unroll
-    for (int ks = 0; ks < KPW; ++ks) w[ks] = __builtin_nontemporal_load(reinterpret_cast<const Frag*>(W + ks * 32));
+      for (int ks = 0; ks < KPW; ++ks) w[ks] = __builtin_nontemporal_load(reinterpret_cast<const Frag*>(W + ks * 512));
+    } else {
+      const long n = min(ct * 16 + (lane & 15), g.N - 1);
+      const T* W = reinterpret_cast<const T*>(g.W) + n * g.ldw + kb;
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) w[ks] = __builtin_nontemporal_load(reinterpret_cast<const Frag*>(W + ks * 32));
+    }
   };
   // ---------------- every load of the launch is issued here
   Frag wc[KPW], wn[P ? KPW : 1];
@@ -1025,6 +1031,7 @@ template <typename T> struct DecLean {
   int grp_n, grp_off;
   unsigned long long* stamp = nullptr;   // tools/dec_kernel_bench: per-workgroup phase stamps (null: off)
   int cfm_nw = 0, cfm_kpw = 0;           // EPI 0: out written fragment-major for a consumer with this split (0: rows)
+  T* out2 = nullptr;                     // EPI 1: the 16-bit copy again, fragment-major with (cfm_nw, cfm_kpw)
 };
 
 template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP, bool WFM = false, bool AFM = false>
@@ -1164,6 +1171,11 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) h[e] = __builtin_bit_cast(short, DT<T>::fromf(o[e]));
     *reinterpret_cast<s4*>(p.out + off) = h;
+    if (p.out2) {   // fragment-major copy for the LN-fused consumers (4 elements of one fragment)
+      const int kw = p.cfm_kpw * 32, w2 = ec / kw, ks2 = (ec % kw) >> 5, lg = (ec & 31) >> 3;
+      *reinterpret_cast<s4*>(p.out2 + ((((long)(row >> 4) * p.cfm_nw + w2) * p.cfm_kpw + ks2) * 64 + lg * 16 + (row & 15)) * 8 +
+                             (ec & 7)) = h;
+    }
   } else {
     s4 hv;
 #pragma unroll
@@ -1203,10 +1215,11 @@ static void launch_lean_k(const GemmArgs& g, hipStream_t s) {
   p.M = g.M; p.N = g.N; p.lda = (int)g.lda; p.ldo = (int)g.ldc;
   p.n_split = g.n_split; p.kvB = g.hs_B; p.kvH = g.hs_H; p.kvT = g.kv_T;
   p.grp_n = g.a_grp_n; p.grp_off = (int)g.a_grp_off;
-  if (g.c_fm) lean_cfg(g.N, p.cfm_nw, p.cfm_kpw);   // the consumer's split of K = this N
+  if (g.c_fm || g.out16_fm) lean_cfg(g.N, p.cfm_nw, p.cfm_kpw);   // the consumer's split of K = this N
+  p.out2 = reinterpret_cast<T*>(g.out16_fm);
   const dim3 grid((g.N + 15) / 16, (g.M + MF * 16 - 1) / (MF * 16));
   if (g.a_fm) {
-    if constexpr (!LN && !GRP) WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, true>), grid, dim3(NW * 64), 0, s, p);
+    if constexpr (!GRP) WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, true>), grid, dim3(NW * 64), 0, s, p);
   } else if (g.W_fm) {
     WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true>), grid, dim3(NW * 64), 0, s, p);
   } else {
@@ -1224,8 +1237,9 @@ static bool launch_lean(const GemmArgs& g, hipStream_t s) {
     if (g.M > 64 || g.sel_val || g.st_out || g.addrow || g.tile || g.a_Mb || g.c_Mb || g.N % 16 || g.ldc % 4) return false;
     // fragment-major operands (the runtime pairs fc1 → fc2 only where both take this path): a_fm needs
     // the weights' fragment-major copy too (the residual writer table), c_fm the LN + GELU table
-    if (g.a_fm && (!g.W_fm || g.ln_w || g.a_grp_n)) return false;
+    if (g.a_fm && (!g.W_fm || g.a_grp_n)) return false;
     if (g.c_fm && (!g.ln_w || !g.act)) return false;
+    if (g.out16_fm && (g.ln_w || !g.resid || !g.out16)) return false;
     if (g.mode != 0 && g.mode != 2) return false;
     if (g.mode == 2 && (g.kv_rps > 1 || !g.kv_out || !g.pos || g.n_split % 64 || g.out_f32 || g.resid)) return false;
     if (g.a_grp_n) {   // q'_h = W_k,hᵀ q_h
@@ -1271,6 +1285,14 @@ static void launch_dec_k(const GemmArgs& g, hipStream_t s) {
     WCB_LAUNCH((gemm_dec_kernel<T, MF, NW, KPW, AM, false>), dim3(ntile, gy), dim3(NW * 64), 0, s, g);
   } else {   // the LM head: kDecWalkers column walkers per row block (= argmax partials per row)
     const int gx = std::min(ntile, kDecWalkers);
+    int nw = 0, kpw = 0;
+    if constexpr (sizeof(T) == 2 && AM != 3) {
+      // the copy's split matches; it covers whole 16-column tiles (the LM head's rows are padded with zeros)
+      if (g.W_fm && lean_cfg(g.K, nw, kpw) && nw == NW && kpw == KPW) {
+        WCB_LAUNCH((gemm_dec_kernel<T, MF, NW, KPW, AM, true, true>), dim3(gx, gy), dim3(NW * 64), 0, s, g);
+        return;
+      }
+    }
     WCB_LAUNCH((gemm_dec_kernel<T, MF, NW, KPW, AM == 3 ? 0 : AM, true>), dim3(gx, gy), dim3(NW * 64), 0, s, g);
   }
 }
@@ -1404,7 +1426,7 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
     // rows (measured C2: 1.074 vs 1.147 ms/token with 32-row workgroups); the LM head walks the
     // vocabulary persistently with 32-row workgroups, reading every weight tile once
     if (g.lean && launch_lean<T>(g, s)) return;
-    if (g.a_fm || g.c_fm) {   // the runtime pairs fragment-major operands only where the lean path takes both
+    if (g.a_fm || g.c_fm || g.out16_fm) {   // the runtime pairs fragment-major operands only where the lean path takes both
       fprintf(stderr, "wcb: internal error: fragment-major operand on a launch the lean kernel does not cover\n");
       abort();
     }

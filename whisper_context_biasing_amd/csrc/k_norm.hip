@@ -82,7 +82,8 @@ void layernorm(DType t, const float* x, const float* w, const float* b, void* y,
 template <typename T>
 __global__ __launch_bounds__(256) void embed_kernel(const T* __restrict__ emb, const T* __restrict__ pemb, const int* __restrict__ ids,
                                                     const int* __restrict__ pos, float* __restrict__ x, float* __restrict__ st,
-                                                    int M, int d, T* __restrict__ x16, int V, int rps, int st_w) {
+                                                    int M, int d, T* __restrict__ x16, int V, int rps, int st_w,
+                                                    T* __restrict__ x16fm, int fm_nw, int fm_kpw) {
   const int row = blockIdx.x;
   const int p = *pos + row % rps;
   const int raw = ids[row];
@@ -94,6 +95,10 @@ __global__ __launch_bounds__(256) void embed_kernel(const T* __restrict__ emb, c
       v = DT<T>::tof(emb[id * d + c]) + DT<T>::tof(pemb[(long)p * d + c]);
       x[(long)row * d + c] = v;
       if (x16) x16[(long)row * d + c] = DT<T>::fromf(v);
+      if (x16fm) {   // fragment-major copy for the lean LN-fused projections (gemm_impl.h dec_lean_kernel AFM)
+        const int kw = fm_kpw * 32, w2 = c / kw, ks2 = (c % kw) >> 5, lg = (c & 31) >> 3;
+        x16fm[((((long)(row >> 4) * fm_nw + w2) * fm_kpw + ks2) * 64 + lg * 16 + (row & 15)) * 8 + (c & 7)] = DT<T>::fromf(v);
+      }
     }
     if (st) {
       // one partial per group of st_w lanes (= columns), fixed butterfly order
@@ -114,15 +119,17 @@ __global__ __launch_bounds__(256) void embed_kernel(const T* __restrict__ emb, c
 }
 
 void embed(DType t, const void* emb, const void* pemb, const int* ids, const int* pos, float* x, float* st, int M,
-           int d, hipStream_t s, void* x16, int V, int rps, int st_w) {
+           int d, hipStream_t s, void* x16, int V, int rps, int st_w, void* x16fm) {
   rps = rps > 1 ? rps : 1;
+  int nw = 0, kpw = 0;
+  if (x16fm && !lean_cfg(d, nw, kpw)) x16fm = nullptr;
   switch (t) {
     case kBF16: WCB_LAUNCH(embed_kernel<bf16_t>, dim3(M), dim3(256), 0, s, (const bf16_t*)emb,
-                                   (const bf16_t*)pemb, ids, pos, x, st, M, d, (bf16_t*)x16, V, rps, st_w); break;
+                                   (const bf16_t*)pemb, ids, pos, x, st, M, d, (bf16_t*)x16, V, rps, st_w, (bf16_t*)x16fm, nw, kpw); break;
     case kF16: WCB_LAUNCH(embed_kernel<f16_t>, dim3(M), dim3(256), 0, s, (const f16_t*)emb,
-                                  (const f16_t*)pemb, ids, pos, x, st, M, d, (f16_t*)x16, V, rps, st_w); break;
+                                  (const f16_t*)pemb, ids, pos, x, st, M, d, (f16_t*)x16, V, rps, st_w, (f16_t*)x16fm, nw, kpw); break;
     case kF32: WCB_LAUNCH(embed_kernel<float>, dim3(M), dim3(256), 0, s, (const float*)emb,
-                                  (const float*)pemb, ids, pos, x, st, M, d, (float*)x16, V, rps, st_w); break;
+                                  (const float*)pemb, ids, pos, x, st, M, d, (float*)x16, V, rps, st_w, (float*)nullptr, 0, 0); break;
   }
 }
 

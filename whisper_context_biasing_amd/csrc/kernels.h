@@ -95,6 +95,9 @@ struct GemmArgs {
   // lean path, fragment-major activations (fc1 → fc2): c_fm = write the output in the layout its
   // consumer (K = this N, lean_cfg split) reads; a_fm = A is in that layout for this launch's split
   int c_fm = 0, a_fm = 0;
+  // lean residual writers: also the 16-bit rows in the fragment-major layout of the LN-fused consumers
+  // (their A: a_fm with ln_a16 = this copy)
+  void* out16_fm = nullptr;
   // LDS-ring tiles (encoder GEMMs): tile order in bands of `raster` row panels, column tiles outer
   // within a band (0: row-major tile order)
   int raster = 0;
@@ -110,8 +113,10 @@ void layernorm(DType t, const float* x, const float* w, const float* b, void* y,
 // x[r][:] = emb[ids[r]][:] + pos_emb[*pos + r_pos][:] (f32 out), r_pos = r % rows_per_seq.
 // stats: per-st_w-column partial sums (Σx, Σx²) of the new rows (16: the older skinny consumers; 32:
 // the ring tiles' folded LayerNorm, GemmArgs::rst_in)
+// x16fm: also the 16-bit rows in the fragment-major layout of the lean LN-fused projections (lean_cfg(d))
 void embed(DType t, const void* emb, const void* pos_emb, const int* ids, const int* pos, float* x,
-           float* stats, int M, int d, hipStream_t s, void* x16 = nullptr, int V = 1 << 30, int rps = 1, int st_w = 16);
+           float* stats, int M, int d, hipStream_t s, void* x16 = nullptr, int V = 1 << 30, int rps = 1, int st_w = 16,
+           void* x16fm = nullptr);
 // prefill: ids[r·np + t] = src[r·ld + *pos + t] (ld 0: one prefix row shared by every row)
 void prefill_ids(int* ids, const int* src, int R, int np, int ld, const int* pos, hipStream_t s);
 void add_i32(int* p, int v, hipStream_t s);   // *p += v (one thread)

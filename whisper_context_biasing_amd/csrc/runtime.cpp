@@ -126,7 +126,7 @@ struct DecCtx {
   hipStream_t sub[kMaxSub] = {};                // row-group chains (fork/join inside the step graph)
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSub] = {};
   int dec_B = 0, dec_T = 0;
-  DevBuf kvself, dx, dx16, dh, dq, dqp, du, datt, dffn, dstats, drst, xpart, xml, xticket, logits, part_val, part_idx, ints,
+  DevBuf kvself, dx, dx16, dx16fm, dh, dq, dqp, du, datt, dffn, dstats, drst, xpart, xml, xticket, logits, part_val, part_idx, ints,
       pids, outbuf, forced, beam;
   int nchunk = 64;
   hipGraphExec_t gexec = nullptr;               // captured decode step
@@ -212,6 +212,9 @@ struct wcb_handle {
   // decode projections of <= 64 rows on dec_lean_kernel (gemm_impl.h; bit-identical to
   // gemm_dec_kernel, one kernel-argument round trip and one load burst per launch; option "lean")
   int lean = 1;
+  // lean path: the residual writers (embedding, out / xo / fc2 projections) also write the 16-bit rows
+  // fragment-major for the LayerNorm-fused consumers (QKV, xq, fc1); option "lean_x"
+  int lean_x = 1;
   struct wcb_state* step_state = nullptr;   // the active step-wise decode (wcb_decode_begin), if any
   // encoder GEMM tile order (option "enc_raster"): bands of n row panels with the column tiles outer
   // (GemmArgs::raster; 0 = row-major)
@@ -231,6 +234,7 @@ struct wcb_handle {
   float *enc_ln_w = nullptr, *enc_ln_b = nullptr, *dec_ln_w = nullptr, *dec_ln_b = nullptr;
   void* xkv_w = nullptr; float* xkv_b = nullptr;
   void *tok_emb = nullptr, *dec_pos = nullptr;
+  void* tok_emb_fm = nullptr;   // 16-bit: fragment-major copy of tok_emb for the greedy LM head
   // mel tables
   DevBuf dft, mel_lo, mel_hi, mel_w, clip_max;
   // encoder workspace
@@ -493,7 +497,7 @@ void wcb_destroy(wcb_handle* h) {
   for (DecCtx& D : h->dc) {
     if (D.gexec) (void)hipGraphExecDestroy(D.gexec);
     if (D.gexec_k) (void)hipGraphExecDestroy(D.gexec_k);
-    for (DevBuf* b : {&D.kvself, &D.dx, &D.dx16, &D.dh, &D.dq, &D.dqp, &D.du, &D.datt, &D.dffn, &D.dstats, &D.drst, &D.xpart, &D.xml, &D.xticket,
+    for (DevBuf* b : {&D.kvself, &D.dx, &D.dx16, &D.dx16fm, &D.dh, &D.dq, &D.dqp, &D.du, &D.datt, &D.dffn, &D.dstats, &D.drst, &D.xpart, &D.xml, &D.xticket,
                       &D.logits, &D.part_val, &D.part_idx, &D.ints, &D.outbuf, &D.forced, &D.beam})
       b->release();
     if (D.ev_fork) (void)hipEventDestroy(D.ev_fork);
@@ -564,6 +568,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       h->enc_raster = value;
     } else if (n == "lean") {
       h->lean = value != 0;
+    } else if (n == "lean_x") {
+      h->lean_x = value != 0;
     } else if (n == "merge_v") {
       h->merge_v = value != 0;
     } else if (n == "ln_fold") {
@@ -774,6 +780,13 @@ int wcb_finalize_weights(wcb_handle* h) {
     rp(false, h->tok_emb, h->W("model.decoder.embed_tokens.weight", (size_t)V * d), {1, 1, (int)((size_t)V * d)},
        {0, 0, 1}, {0, 0, 1});
     h->dec_pos = T_("model.decoder.embed_positions.weight", (size_t)h->d.n_text_ctx * d);
+    if (h->dt != kF32) {   // the greedy LM head's column walk reads a fragment-major copy (zero rows past V)
+      int nw = 0, kpw = 0;
+      if (lean_cfg(d, nw, kpw)) {
+        h->tok_emb_fm = h->own((size_t)h->vocab_pad * d * e);
+        frag_major(h->dt, h->tok_emb, h->vocab_pad, d, nw, kpw, h->tok_emb_fm, st);
+      }
+    }
     int bad_bias = 0, untied = 0;
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipMemcpy(&bad_bias, check.p, 4, hipMemcpyDeviceToHost));
@@ -963,7 +976,9 @@ void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode
     D.dh.ensure((size_t)rows * d * e);
     D.dq.ensure((size_t)rows * d * e);
     D.datt.ensure((size_t)rows * d * e);
-    D.dffn.ensure((size_t)(rows + 15) / 16 * 16 * h->d.ffn * e);   // fragment-major: whole 16-row blocks
+    // fragment-major copies: whole 16-row blocks, two blocks of slack (a 32-row workgroup past the rows)
+    D.dffn.ensure(((size_t)(rows + 15) / 16 * 16 + 32) * h->d.ffn * e);
+    D.dx16fm.ensure(((size_t)(rows + 15) / 16 * 16 + 32) * d * e);
     D.dstats.ensure((size_t)rows * (d / 16) * 2 * 4);
     D.drst.ensure((size_t)rows * (d / 32) * 2 * 4);
     D.xpart.ensure(std::max((size_t)rows * h->H() * kXSplit * 66, (size_t)rows * h->xenc_split * h->H() * d) * 4);
@@ -1005,6 +1020,18 @@ struct StepCfg {
   float* score_out = nullptr;          // greedy select: the chosen token's (boosted) logit per row (step-wise API)
 };
 
+// the residual's fragment-major copy applies (lean path): the lean LayerNorm table covers d, every
+// LN consumer and residual writer has its weights' fragment-major copy, and the decode GEMMs publish
+// no 16-column LayerNorm partials (the lean kernel writes none)
+bool xfm_possible(const wcb_handle* h) {
+  const int d = h->d.d_model;
+  if (!h->lean || !h->lean_x || h->dt == kF32 || !h->ln16 || !h->dec_gemm) return false;
+  if (d != 512 && d != 768 && d != 1024 && d != 1280) return false;
+  for (const LayerW& w : h->dec)
+    if (!w.qkv_fm || !w.o_fm || !w.xq_fm || !w.xo_fm || !w.fc1_fm || !w.fc2_fm) return false;
+  return true;
+}
+
 // the folded LayerNorm of the > 64-row projections is available (16-bit, d a multiple of 32)
 bool lnf_possible(const wcb_handle* h) {
   return h->ln_fold && h->dt != kF32 && h->d.d_model % 32 == 0 && h->d.d_model <= kLnfMaxK;
@@ -1044,6 +1071,13 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
   // the decode kernel (and keep writing the 16-bit residual copy its LayerNorm consumers read).
   const bool tiled = M > 64;
   const bool lnf_ok = tiled && h->dec_gemm && lnf_possible(h);
+  // fragment-major operands (lean path): this chain's rows start a 16-row block of the copies
+  const bool fm_ok = !tiled && h->lean && h->dt != kF32 && lna && r0 % 16 == 0 && M <= 64;
+  // the residual's fragment-major copy (written by the embedding and every residual writer, read by
+  // the LayerNorm-fused projections); decode_step's and prefill_step's embeddings write it for every
+  // row whenever xfm_possible
+  // (one position per row: the lean QKV appends one key per row)
+  char* x16fm = fm_ok && rps == 1 && xfm_possible(h) ? (char*)D.dx16fm.p + (size_t)r0 * d * e : nullptr;
   char* dh = (char*)D.dh.p + (size_t)r0 * d * e;
   auto proj = [&](const char* cls, GemmArgs g) {
     const bool lm = g.W == h->tok_emb;
@@ -1081,6 +1115,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nbk; q.ln_a16 = lna;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
     q.kv_rps = rps; q.ln_u = w.ln1_u; q.ln_c = w.ln1_c; q.ln_wg = w.qkv_wg; q.W_fm = w.qkv_fm;
+    if (x16fm) { q.ln_a16 = x16fm; q.a_fm = 1; }
     proj("dec_qkv", q);
     AttnArgs a;
     a.q = dq; a.ldq = d; a.q_Sb = rps; a.Sq = rps; a.causal = rps > 1;
@@ -1097,6 +1132,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     }
     GemmArgs o = drow(datt, d, w.o_w, M, d, d, x, d);
     o.bias = w.o_b; o.resid = x; o.out_f32 = 1; o.st_out = st_pub; o.st_nb = nbk; o.out16 = x16; o.W_fm = w.o_fm;
+    o.out16_fm = x16fm;
     proj("dec_out", o);
     if (c.xmode == 1) {
       // cross attention in encoder space: q'_h = W_k,hᵀ q_h (block-diagonal GEMM, K = 64), one pass
@@ -1113,6 +1149,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
         GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
         xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
         xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg; xq.W_fm = w.xq_fm;
+        if (x16fm) { xq.ln_a16 = x16fm; xq.a_fm = 1; }
         proj("dec_xq", xq);
         GemmArgs kq = drow(dq, d, w.xkt_w, M, H * d, 64, dqp, (long)H * d);
         kq.a_grp_n = d; kq.a_grp_off = 64; kq.W_fm = w.xkt_fm;
@@ -1149,6 +1186,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
       xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
       xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg; xq.W_fm = w.xq_fm;
+      if (x16fm) { xq.ln_a16 = x16fm; xq.a_fm = 1; }
       proj("dec_xq", xq);
       AttnArgs xa;
       const char* xkv = (const char*)h->xkv2[c.buf].p + l * xkv_l * e;
@@ -1185,21 +1223,24 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     }
     GemmArgs xo = drow(datt, d, w.xo_w, M, d, d, x, d);
     xo.bias = w.xo_b; xo.resid = x; xo.out_f32 = 1; xo.st_out = st_pub; xo.st_nb = nbk; xo.out16 = x16; xo.W_fm = w.xo_fm;
+    xo.out16_fm = x16fm;
     proj("dec_xo", xo);
     // MLP. Lean path (<= 64 rows, 16-bit): fc1 writes its output fragment-major in the layout fc2's
     // split of K = ffn reads (every A wave-instruction of fc2 then reads 1 KiB contiguous: its 98 KB of
     // activations per workgroup at d = 768 were the largest operand of the decode step)
-    const bool afm = !tiled && h->lean && h->dt != kF32 && lna && w.fc1_fm && w.fc2_fm && M <= 64 &&
+    const bool afm = fm_ok && w.fc1_fm && w.fc2_fm &&
                      (d == 512 || d == 768 || d == 1024 || d == 1280) &&
                      (h->d.ffn == 2048 || h->d.ffn == 3072 || h->d.ffn == 4096 || h->d.ffn == 5120);
     GemmArgs f1 = drow(x, d, w.fc1_w, M, h->d.ffn, d, dffn, h->d.ffn);
     f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nbk; f1.ln_a16 = lna;
     f1.bias = w.fc1_b; f1.act = 1; f1.ln_u = w.ln2_u; f1.ln_c = w.ln2_c; f1.ln_wg = w.fc1_wg; f1.W_fm = w.fc1_fm;
     f1.c_fm = afm;
+    if (x16fm) { f1.ln_a16 = x16fm; f1.a_fm = 1; }
     proj("dec_fc1", f1);
     GemmArgs f2 = drow(dffn, h->d.ffn, w.fc2_w, M, d, h->d.ffn, x, d);
     f2.bias = w.fc2_b; f2.resid = x; f2.out_f32 = 1; f2.st_out = st_pub; f2.st_nb = nbk; f2.out16 = x16; f2.W_fm = w.fc2_fm;
     f2.a_fm = afm;
+    f2.out16_fm = x16fm;
     proj("dec_fc2", f2);
   }
   if (c.lm_head) {
@@ -1209,6 +1250,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     const bool lm_tiled = tiled && rps == 1 && c.logits_ld >= h->vocab_pad;
     if (lm_tiled) lm.N = h->vocab_pad;
     lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b; lm.st_in = st; lm.st_nb = nbk; lm.ln_a16 = lna;
+    if (h->lean) lm.W_fm = h->tok_emb_fm;
     lm.out_f32 = 1;
     if (c.select && !c.beam) {   // argmax partials with the root boost + EOS mask fused into the LM head
       lm.sel_val = D.part_val.as<float>() + (size_t)b0 * D.nchunk;
@@ -1239,7 +1281,7 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
   h->timed("dec_embed", 0, (double)B * d * (2.0 * esize(h->d.dtype) + 4), D.hs, [&] {
     embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, D.dx.as<float>(),
           !h->dec_gemm ? D.dstats.as<float>() : r32 ? D.drst.as<float>() : nullptr, B, d, D.hs, D.dx16.p, h->d.vocab, 1,
-          r32 ? 32 : 16);
+          r32 ? 32 : 16, xfm_possible(h) ? D.dx16fm.p : nullptr);
   });
   // rows per chain: the skinny projections split rows over grid.y, so a chain can take any number
   // of rows (WCB_GROUP_ROWS; more chains overlap latency, fewer re-read the weights less often)
@@ -1302,7 +1344,7 @@ void prefill_step(wcb_handle* h, StepCfg c, int np, const int* src, int ld) {
     prefill_ids(D.pids.as<int>(), src, R, np, ld, pos, D.hs);
     const bool r32 = h->dec_gemm && lnf_possible(h);
     embed(h->dt, h->tok_emb, h->dec_pos, D.pids.as<int>(), pos, D.dx.as<float>(), r32 ? D.drst.as<float>() : nullptr, M,
-          d, D.hs, D.dx16.p, h->d.vocab, np, 32);
+          d, D.hs, D.dx16.p, h->d.vocab, np, 32, xfm_possible(h) ? D.dx16fm.p : nullptr);
   });
   decode_rows(h, c, 0, R, 0, D.hs);
   add_i32(pos, np, D.hs);
