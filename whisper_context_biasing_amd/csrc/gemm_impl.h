@@ -279,14 +279,22 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(GemmArgs g) {
 // KT: 64-deep sub-tiles per ring stage (2 for the small decode-row tiles: half the K-loop
 // iterations, and with them half the barriers, of a loop that is latency-bound at 2-8 MFMAs per wave
 // per sub-tile).
-template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1>
+// BKB: bytes of K per LDS row of a sub-tile: 128 (64-deep) or 64 (32-deep: half the stage bytes, so
+// twice the stages in the same LDS — the encoder's 256x256 tiles keep 3 stages in flight across the
+// barrier instead of 1). The MFMA sequence over K is the same: bit-identical outputs.
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1, int BKB = 128>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
   constexpr int NW = WM * WN, NT = NW * 64;
-  constexpr int BK = 64, CE = 8;
+  static_assert(BKB == 128 || BKB == 64, "LDS row: 128 or 64 bytes");
+  constexpr int BK = BKB / 2, CE = 8;
+  constexpr int CPR = BKB / 16, RPI = 64 / CPR, KS = BKB / 64;   // chunks per row, rows per glds, k-steps per sub-tile
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
-  constexpr int SUB = (BM + BN) * 128, STAGE = SUB * KT;
-  constexpr int IA = BM / 8 / NW, IB = BN / 8 / NW, GL = (IA + IB) * KT;   // glds per wave per stage
-  static_assert(IA * NW * 8 == BM && IB * NW * 8 == BN, "tile rows must split over waves");
+  constexpr int SUB = (BM + BN) * BKB, STAGE = SUB * KT;
+  constexpr int IA = BM / RPI / NW, IB = BN / RPI / NW, GL = (IA + IB) * KT;   // glds per wave per stage
+  static_assert(IA * NW * RPI == BM && IB * NW * RPI == BN, "tile rows must split over waves");
+  // 16-byte chunk c of LDS row r sits in slot c ^ swz(r): the 16 rows of a fragment read hit 16
+  // distinct 16-byte bank groups
+  auto swz = [](int r) { return BKB == 128 ? (r >> 1) & 7 : (r >> 2) & 3; };
   using Frag = typename DT<T>::frag;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -312,15 +320,15 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
   const T* b_src[IB];
 #pragma unroll
   for (int i = 0; i < IA; ++i) {
-    const int r = (wave + i * NW) * 8 + (lane >> 3);
+    const int r = (wave + i * NW) * RPI + lane / CPR;
     const int m = min(m0 + r, g.M - 1);
-    a_src[i] = A + a_row(g, m) + ((lane & 7) ^ ((r >> 1) & 7)) * CE;
+    a_src[i] = A + a_row(g, m) + ((lane % CPR) ^ swz(r)) * CE;
   }
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
-    const int r = (wave + i * NW) * 8 + (lane >> 3);
+    const int r = (wave + i * NW) * RPI + lane / CPR;
     const long n = min(n0 + r, g.N - 1);
-    b_src[i] = W + n * g.ldw + ((lane & 7) ^ ((r >> 1) & 7)) * CE;
+    b_src[i] = W + n * g.ldw + ((lane % CPR) ^ swz(r)) * CE;
   }
   auto stage = [&](int st, int k0) {
 #pragma unroll
@@ -329,7 +337,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < IA; ++i) glds16(a_src[i] + k0 + t * BK, base + (wave + i * NW) * 1024);
 #pragma unroll
-      for (int i = 0; i < IB; ++i) glds16(b_src[i] + k0 + t * BK, base + BM * 128 + (wave + i * NW) * 1024);
+      for (int i = 0; i < IB; ++i) glds16(b_src[i] + k0 + t * BK, base + BM * BKB + (wave + i * NW) * 1024);
     }
   };
 
@@ -383,20 +391,20 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
       if (nxt < nk) stage(sn, nxt * BK * KT);
     }
 #pragma unroll
-    for (int kq = 0; kq < 2 * KT; ++kq) {
-      const char* base = smem + st * STAGE + (kq >> 1) * SUB;
-      const int ks = kq & 1;
+    for (int kq = 0; kq < KS * KT; ++kq) {
+      const char* base = smem + st * STAGE + (kq / KS) * SUB;
+      const int ks = kq % KS;
       Frag a[FM], b[FN];
       const int c = ks * 4 + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wm * TM + i * 16 + (lane & 15);
-        a[i] = *reinterpret_cast<const Frag*>(base + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+        a[i] = *reinterpret_cast<const Frag*>(base + r * BKB + ((c ^ swz(r)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int r = wn * TN + j * 16 + (lane & 15);
-        b[j] = *reinterpret_cast<const Frag*>(base + BM * 128 + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+        b[j] = *reinterpret_cast<const Frag*>(base + BM * BKB + r * BKB + ((c ^ swz(r)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -427,8 +435,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
   }
   __syncthreads();   // every wave is done with the ring: the epilogue reuses its LDS
 
-  // epilogue: f32 tile through LDS (in WM passes of TM rows when the whole tile does not fit), then
-  // 8 columns per lane per store
+  // epilogue: f32 accumulators through LDS (in WM passes of TM rows when the whole tile does not
+  // fit), then 8 columns per lane: bias / GELU / row table applied there, by all the waves (in the
+  // LDS-write phase only the waves of one pass would), then the store
   constexpr int LDC = BN + 4;
   constexpr int PASSES = (BM * LDC * 4 <= 160 * 1024) ? 1 : WM;
   constexpr int PR = BM / PASSES;
@@ -439,24 +448,33 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int col = wn * TN + j * 16 + (lane & 15);
-        const int n = min(n0 + col, g.N - 1);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int row = wm * TM + i * 16 + (lane >> 4) * 4 + e;
-            const int m = min(m0 + row, g.M - 1);
             float v = acc[i][j][e];
-            if constexpr (LNF) v = lnst[2 * row + 1] * (v - lnst[2 * row] * g.ln_u[n]);
-            ct[(row - ps * PR) * LDC + col] = epi_pointwise<T, EPI>(g, m, n, v);
+            if constexpr (LNF) v = lnst[2 * row + 1] * (v - lnst[2 * row] * g.ln_u[min(n0 + col, g.N - 1)]);
+            ct[(row - ps * PR) * LDC + col] = v;
           }
       }
     }
     __syncthreads();
-    constexpr int C8 = BN / 8;
-#pragma unroll 2
-    for (int idx = tid; idx < PR * C8; idx += NT) {
-      const int row = idx / C8, c8 = idx % C8;
+    constexpr int C8 = BN / 8, RPIT = NT / C8;   // rows per iteration (threads past RPIT·C8 idle)
+    // a thread keeps its 8 columns over the store loop: their bias once, before it
+    const int c8 = tid % C8;
+    float b8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (has<EPI>(g, E_BIAS)) {
+      const int nb = min(n0 + c8 * 8, g.N - 8);
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(g.bias + nb);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(g.bias + nb + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { b8[e] = lo[e]; b8[e + 4] = hi[e]; }
+    }
+    const int row0 = tid < RPIT * C8 ? tid / C8 : PR;
+    constexpr int UNR = PR >= 2 * RPIT && EPI != E_RUNTIME ? 2 : 1;   // (E_RUNTIME: convergent shuffles)
+#pragma unroll UNR
+    for (int row = row0; row < PR; row += RPIT) {
       const int m = m0 + ps * PR + row;
       const int n = n0 + c8 * 8;
       const bool ok = m < g.M && n < g.N;
@@ -465,6 +483,13 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
       const f32x4 hi = *reinterpret_cast<const f32x4*>(ct + row * LDC + c8 * 8 + 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) { v[e] = lo[e]; v[e + 4] = hi[e]; }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {   // epi_pointwise's order: + bias, GELU, + row table
+        if (has<EPI>(g, E_BIAS)) v[e] += b8[e];
+        if (has<EPI>(g, E_GELU)) v[e] = gelu_t<T>(v[e]);
+        if (has<EPI>(g, E_ADDROW))
+          v[e] += g.addrow[(long)(g.c_Mb ? min(m, g.M - 1) % g.c_Mb : min(m, g.M - 1)) * g.N + min(n + e, g.N - 1)];
+      }
       if (ok) epi_store8<T, EPI>(g, m, n, v);
       if (EPI == E_RUNTIME && g.rst_out) {   // residual writer: (Σx, Σx²) of the new row per 32 columns
         float a1 = 0.f, a2 = 0.f;
@@ -479,10 +504,10 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
   }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1>
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1, int BKB = 128>
 static void launch_ring_e(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
-  constexpr int ring_bytes = NS * (BM + BN) * 128 * KT;
+  constexpr int ring_bytes = NS * (BM + BN) * BKB * KT;
   constexpr int epi_full = BM * (BN + 4) * 4;
   constexpr int epi_bytes = epi_full <= 160 * 1024 ? epi_full : epi_full / WM;
   constexpr int base = ring_bytes > epi_bytes ? ring_bytes : epi_bytes;
@@ -490,25 +515,25 @@ static void launch_ring_e(const GemmArgs& g, hipStream_t s) {
   static_assert(lds <= 160 * 1024, "LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT>,
+    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT, BKB>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
-  WCB_LAUNCH((gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
+  WCB_LAUNCH((gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT, BKB>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS>
+template <typename T, int BM, int BN, int WM, int WN, int NS, int BKB = 128>
 static void launch_ring(const GemmArgs& g, hipStream_t s) {
   const int bits = (g.bias ? E_BIAS : 0) | (g.act == 1 ? E_GELU : 0) | (g.resid ? E_RESID : 0) |
                    (g.out_f32 ? E_F32 : 0) | (g.addrow ? E_ADDROW : 0) | (g.mode == 1 ? E_HEAD : 0);
   switch (bits) {
-    case E_BIAS: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS>(g, s); break;
-    case E_BIAS | E_GELU: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_GELU>(g, s); break;
-    case E_BIAS | E_RESID | E_F32: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_RESID | E_F32>(g, s); break;
+    case E_BIAS: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS, false, 1, BKB>(g, s); break;
+    case E_BIAS | E_GELU: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_GELU, false, 1, BKB>(g, s); break;
+    case E_BIAS | E_RESID | E_F32: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_RESID | E_F32, false, 1, BKB>(g, s); break;
     case E_BIAS | E_GELU | E_F32 | E_ADDROW:
-      launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_GELU | E_F32 | E_ADDROW>(g, s); break;
-    case E_BIAS | E_HEAD: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_HEAD>(g, s); break;
-    default: launch_ring_e<T, BM, BN, WM, WN, NS, E_RUNTIME>(g, s); break;
+      launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_GELU | E_F32 | E_ADDROW, false, 1, BKB>(g, s); break;
+    case E_BIAS | E_HEAD: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_HEAD, false, 1, BKB>(g, s); break;
+    default: launch_ring_e<T, BM, BN, WM, WN, NS, E_RUNTIME, false, 1, BKB>(g, s); break;
   }
 }
 
@@ -1455,9 +1480,16 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
   // 16-bit encoder-size GEMMs: the LDS-ring kernel, 256x256 (2 stages) when N allows it (measured
   // 1128 vs 990 TFLOP/s at 48000x2304x768 class shapes), else 256x128 (3 stages); f32 ("exact"
   // mode) and small shapes: the two-stage tile kernel, 128x128 (4 waves 2x2) when N fills it, else 128x64.
+  // 256x192 where the 256-column grid leaves a short last round of tiles on the 256 CUs and the
+  // 192-column one does not, at its measured per-tile efficiency (0.9 of 256x256): whisper-small's
+  // d-wide out / fc2 (M = 48000, N = 768: 564 tiles = 2.2 rounds against 752 = 2.9), 12 % / 10 %
+  // faster (tools/enc_gemm_bench.hip); QKV / fc1 keep 256x256 (192 measured 9 / 15 % slower)
   if constexpr (sizeof(T) == 2) {
     if (g.N % 128 == 0 && g.M >= 4096) {
-      if (g.N % 256 == 0) launch_ring<T, 256, 256, 2, 4, 2>(g, s);
+      const long tm = (g.M + 255) / 256;
+      const long r256 = (tm * ((g.N + 255) / 256) + 255) / 256, r192 = (tm * ((g.N + 191) / 192) + 255) / 256;
+      if (g.N % 192 == 0 && r192 * 192 * 10 < r256 * 256 * 9) launch_ring<T, 256, 192, 2, 4, 2>(g, s);
+      else if (g.N % 256 == 0) launch_ring<T, 256, 256, 2, 4, 2>(g, s);
       else launch_ring<T, 256, 128, 4, 2, 3>(g, s);
       return;
     }
