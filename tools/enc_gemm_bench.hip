@@ -62,12 +62,19 @@ double time_graph(const std::function<void(hipStream_t)>& launch, hipStream_t s,
 int main(int argc, char** argv) {
   const int M = 48000;
   struct Shape { const char* name; int N, K, act; bool resid; };
-  const Shape shapes[] = {{"qkv", 2304, 768, 0, false}, {"out", 768, 768, 0, true},
-                          {"fc1", 3072, 768, 1, false}, {"fc2", 768, 3072, 0, true}};
+  std::vector<Shape> shapes = {{"qkv", 2304, 768, 0, false}, {"out", 768, 768, 0, true},
+                               {"fc1", 3072, 768, 1, false}, {"fc2", 768, 3072, 0, true}};
+  if (argc > 2) {   // "N:K:act:resid,..." custom shapes (M = 48000)
+    shapes.clear();
+    for (char* tok = strtok(argv[2], ","); tok; tok = strtok(nullptr, ",")) {
+      int n, k, a, r;
+      if (sscanf(tok, "%d:%d:%d:%d", &n, &k, &a, &r) == 4) shapes.push_back({"shape", n, k, a, r != 0});
+    }
+  }
   const Variant vars[] = {
-      {"256x256 BK64 NS2", launch_ring<bf, 256, 256, 2, 4, 2>},
-      {"256x192 BK64 NS2", launch_ring<bf, 256, 192, 2, 4, 2>},
-      {"256x128 BK64 NS3", launch_ring<bf, 256, 128, 4, 2, 3>},
+      {"256x256", launch_ring<bf, 256, 256, 2, 4, 2>},
+      {"256x256 no prio", launch_ring<bf, 256, 256, 2, 4, 2, 128, 0>},
+      {"256x192", launch_ring<bf, 256, 192, 2, 4, 2>},
   };
   const int nv = sizeof(vars) / sizeof(vars[0]);
   const int rounds = argc > 1 ? atoi(argv[1]) : 5;

@@ -282,7 +282,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(GemmArgs g) {
 // BKB: bytes of K per LDS row of a sub-tile: 128 (64-deep) or 64 (32-deep: half the stage bytes, so
 // twice the stages in the same LDS — the encoder's 256x256 tiles keep 3 stages in flight across the
 // barrier instead of 1). The MFMA sequence over K is the same: bit-identical outputs.
-template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1, int BKB = 128>
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1, int BKB = 128,
+          int PRIO = 0>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
   constexpr int NW = WM * WN, NT = NW * 64;
   static_assert(BKB == 128 || BKB == 64, "LDS row: 128 or 64 bytes");
@@ -406,10 +407,12 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
         const int r = wn * TN + j * 16 + (lane & 15);
         b[j] = *reinterpret_cast<const Frag*>(base + BM * BKB + r * BKB + ((c ^ swz(r)) << 4));
       }
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mma16(a[i], b[j], acc[i][j]);
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
     }
     st = st + 1 == NS ? 0 : st + 1;
   }
@@ -504,7 +507,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
   }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1, int BKB = 128>
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1, int BKB = 128,
+          int PRIO = 0>
 static void launch_ring_e(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
   constexpr int ring_bytes = NS * (BM + BN) * BKB * KT;
@@ -515,25 +519,27 @@ static void launch_ring_e(const GemmArgs& g, hipStream_t s) {
   static_assert(lds <= 160 * 1024, "LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT, BKB>,
+    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT, BKB, PRIO>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
-  WCB_LAUNCH((gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT, BKB>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
+  WCB_LAUNCH((gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT, BKB, PRIO>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS, int BKB = 128>
+// PRIO 1: s_setprio(1) around each MFMA cluster (keeps hipcc from moving the MFMAs across the
+// barriers, cdna_hip_programming.md T5): the encoder shapes 1-4 % faster (tools/enc_gemm_bench.hip)
+template <typename T, int BM, int BN, int WM, int WN, int NS, int BKB = 128, int PRIO = 1>
 static void launch_ring(const GemmArgs& g, hipStream_t s) {
   const int bits = (g.bias ? E_BIAS : 0) | (g.act == 1 ? E_GELU : 0) | (g.resid ? E_RESID : 0) |
                    (g.out_f32 ? E_F32 : 0) | (g.addrow ? E_ADDROW : 0) | (g.mode == 1 ? E_HEAD : 0);
   switch (bits) {
-    case E_BIAS: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS, false, 1, BKB>(g, s); break;
-    case E_BIAS | E_GELU: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_GELU, false, 1, BKB>(g, s); break;
-    case E_BIAS | E_RESID | E_F32: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_RESID | E_F32, false, 1, BKB>(g, s); break;
+    case E_BIAS: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS, false, 1, BKB, PRIO>(g, s); break;
+    case E_BIAS | E_GELU: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_GELU, false, 1, BKB, PRIO>(g, s); break;
+    case E_BIAS | E_RESID | E_F32: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_RESID | E_F32, false, 1, BKB, PRIO>(g, s); break;
     case E_BIAS | E_GELU | E_F32 | E_ADDROW:
-      launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_GELU | E_F32 | E_ADDROW, false, 1, BKB>(g, s); break;
-    case E_BIAS | E_HEAD: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_HEAD, false, 1, BKB>(g, s); break;
-    default: launch_ring_e<T, BM, BN, WM, WN, NS, E_RUNTIME, false, 1, BKB>(g, s); break;
+      launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_GELU | E_F32 | E_ADDROW, false, 1, BKB, PRIO>(g, s); break;
+    case E_BIAS | E_HEAD: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_HEAD, false, 1, BKB, PRIO>(g, s); break;
+    default: launch_ring_e<T, BM, BN, WM, WN, NS, E_RUNTIME, false, 1, BKB, PRIO>(g, s); break;
   }
 }
 
