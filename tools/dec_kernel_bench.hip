@@ -230,6 +230,7 @@ void run_icache() {
 
 // the LM head: persistent column walk (gemm_dec_kernel P), LN-fused, argmax partials, with and
 // without the bias boost (root bits read per tile)
+template <int AM = 2, bool WFM = false>
 void run_lm_head(bool boost) {
   const int V = 51865, K = 768, M = 32;
   static uint32_t* bits = nullptr;
@@ -246,13 +247,16 @@ void run_lm_head(bool boost) {
     GemmArgs g = base(V, K, 0);
     g.M = M; g.ldc = V;
     g.W = g_w + (i % 8) * wbytes;
-    g.A = g_x; g.lda = K; g.ln_w = g_lnw; g.ln_b = g_lnb; g.ln_a16 = g_x16; g.out_f32 = 1; g.out = nullptr;
+    g.A = AM == 0 ? (const void*)g_x16 : (const void*)g_x; g.lda = K; g.out_f32 = 1; g.out = nullptr;
+    if (AM == 2) { g.ln_w = g_lnw; g.ln_b = g_lnb; g.ln_a16 = g_x16; }
+    g.W_fm = g.W;
     g.sel_val = pv; g.sel_idx = pi; g.sel_root_bits = bits; g.sel_lam = boost ? 2.f : 0.f; g.sel_rowbase = rb;
     g.sel_eos = 50257; g.sel_step = step; g.sel_min_new = 0;
     const int gx = std::min((V + 15) / 16, kDecWalkers);
-    hipLaunchKernelGGL((gemm_dec_kernel<bf16_t, 2, 4, 6, 2, true>), dim3(gx, 1), dim3(256), 0, s, g);
+    hipLaunchKernelGGL((gemm_dec_kernel<bf16_t, 2, 4, 6, AM, true, WFM>), dim3(gx, 1), dim3(256), 0, s, g);
   });
-  printf("lm head (V=%d, 32 rows, %d walkers)%s: %6.2f us/launch\n", V, kDecWalkers, boost ? " + boost" : "", us);
+  printf("lm head (V=%d, 32 rows, %d walkers, AM %d, WFM %d)%s: %6.2f us/launch\n", V, kDecWalkers, AM, (int)WFM,
+         boost ? " + boost" : "", us);
   fflush(stdout);
 }
 
@@ -300,6 +304,12 @@ int main() {
 
   run_lm_head(false);
   run_lm_head(true);
+  run_lm_head<2, true>(true);
+  run_lm_head<0, true>(true);
+  run_lm_head<0, true>(false);
+  run_stream<256, 39, 0>("stream: LM-head bytes (80 MB), 512 wgs", 512);
+  run_stream<256, 20, 0>("stream: LM-head bytes (80 MB), 1024 wgs", 1024);
+  if (getenv("LM_ONLY")) return 0;
   run_icache();
   run_cold(100, false);
   run_cold(850, false);

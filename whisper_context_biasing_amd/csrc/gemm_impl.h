@@ -1308,6 +1308,64 @@ static bool launch_lean(const GemmArgs& g, hipStream_t s) {
   }
 }
 
+// The LayerNorm of gemm_dec_kernel AM = 2 (the same K split over NW waves × KPW k-steps, sum order
+// and normalisation) for 16-row blocks, written as 16-bit rows: the LM head's A operand.
+template <typename T, int NW, int KPW>
+__global__ __launch_bounds__(NW * 64) void ln_rows_kernel(const T* __restrict__ x16, long lda, const float* __restrict__ gw,
+                                                          const float* __restrict__ gb, T* __restrict__ out, int M) {
+  using Frag = typename DT<T>::frag;
+  constexpr int K = NW * KPW * 32;
+  __shared__ float2 rst[NW][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kb = wave * (KPW * 32) + 8 * (lane >> 4);
+  const int r = blockIdx.x * 16 + (lane & 15), row = min(r, M - 1);
+  Frag a[KPW];
+  f32x4 w[KPW][2], b[KPW][2];
+#pragma unroll
+  for (int ks = 0; ks < KPW; ++ks) {
+    a[ks] = load_frag<T>(x16 + (long)row * lda + kb + ks * 32);
+    w[ks][0] = *reinterpret_cast<const f32x4*>(gw + kb + ks * 32);
+    w[ks][1] = *reinterpret_cast<const f32x4*>(gw + kb + ks * 32 + 4);
+    b[ks][0] = *reinterpret_cast<const f32x4*>(gb + kb + ks * 32);
+    b[ks][1] = *reinterpret_cast<const f32x4*>(gb + kb + ks * 32 + 4);
+  }
+  float xv[KPW][8];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < KPW; ++ks) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v;
+      if constexpr (__is_same(T, bf16_t)) v = bf16_to_f((bf16_t)a[ks][e]);
+      else v = float(a[ks][e]);
+      xv[ks][e] = v;
+      s1 += v;
+      s2 = fmaf(v, v, s2);
+    }
+  }
+  s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
+  s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
+  if (lane < 16) rst[wave][lane] = float2{s1, s2};
+  __syncthreads();
+  s1 = 0.f; s2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) { const float2 t = rst[q][lane & 15]; s1 += t.x; s2 += t.y; }
+  const float mean = s1 / K;
+  const float rstd = rsqrtf(fmaxf(s2 / K - mean * mean, 0.f) + 1e-5f);
+  if (r >= M) return;
+#pragma unroll
+  for (int ks = 0; ks < KPW; ++ks) {
+    Frag o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gwe = e < 4 ? w[ks][0][e] : w[ks][1][e - 4], gbe = e < 4 ? b[ks][0][e] : b[ks][1][e - 4];
+      const float v = (xv[ks][e] - mean) * rstd * gwe + gbe;
+      o[e] = __builtin_bit_cast(typename std::remove_reference<decltype(o[0])>::type, DT<T>::fromf(v));
+    }
+    *reinterpret_cast<Frag*>(out + (long)r * K + kb + ks * 32) = o;
+  }
+}
+
 template <typename T, int MF, int NW, int KPW, int AM>
 static void launch_dec_k(const GemmArgs& g, hipStream_t s) {
   const int ntile = (g.N + 15) / 16, gy = (g.M + MF * 16 - 1) / (MF * 16);
@@ -1320,6 +1378,15 @@ static void launch_dec_k(const GemmArgs& g, hipStream_t s) {
     if constexpr (sizeof(T) == 2 && AM != 3) {
       // the copy's split matches; it covers whole 16-column tiles (the LM head's rows are padded with zeros)
       if (g.W_fm && lean_cfg(g.K, nw, kpw) && nw == NW && kpw == KPW) {
+        if (AM == 2 && g.ln_scratch && g.sel_val && g.a_Mb == 0) {   // LayerNorm once, then the walk on LN(x)
+          WCB_LAUNCH((ln_rows_kernel<T, NW, KPW>), dim3((g.M + 15) / 16), dim3(NW * 64), 0, s,
+                     reinterpret_cast<const T*>(g.ln_a16), g.lda, g.ln_w, g.ln_b, reinterpret_cast<T*>(g.ln_scratch), g.M);
+          GemmArgs h = g;
+          h.A = g.ln_scratch; h.lda = g.K;
+          h.ln_w = h.ln_b = nullptr; h.ln_a16 = nullptr; h.st_in = nullptr;
+          WCB_LAUNCH((gemm_dec_kernel<T, MF, NW, KPW, 0, true, true>), dim3(gx, gy), dim3(NW * 64), 0, s, h);
+          return;
+        }
         WCB_LAUNCH((gemm_dec_kernel<T, MF, NW, KPW, AM, true, true>), dim3(gx, gy), dim3(NW * 64), 0, s, g);
         return;
       }

@@ -98,6 +98,11 @@ struct GemmArgs {
   // lean residual writers: also the 16-bit rows in the fragment-major layout of the LN-fused consumers
   // (their A: a_fm with ln_a16 = this copy)
   void* out16_fm = nullptr;
+  // LM head (greedy select, fragment-major embedding): the final LayerNorm of the rows in a launch of
+  // its own into this scratch ([M][K] 16-bit, same arithmetic as the fused form: bit-identical), the
+  // vocabulary walk then without it (tools/dec_kernel_bench: the fused LayerNorm cost each of the 512
+  // walkers 10 µs of a 31 µs launch)
+  void* ln_scratch = nullptr;
   // LDS-ring tiles (encoder GEMMs): tile order in bands of `raster` row panels, column tiles outer
   // within a band (0: row-major tile order)
   int raster = 0;

@@ -1251,6 +1251,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     if (lm_tiled) lm.N = h->vocab_pad;
     lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b; lm.st_in = st; lm.st_nb = nbk; lm.ln_a16 = lna;
     if (h->lean) lm.W_fm = h->tok_emb_fm;
+    if (h->lean && !tiled && rps == 1) lm.ln_scratch = dh;   // the final LayerNorm in a launch of its own
     lm.out_f32 = 1;
     if (c.select && !c.beam) {   // argmax partials with the root boost + EOS mask fused into the LM head
       lm.sel_val = D.part_val.as<float>() + (size_t)b0 * D.nchunk;
