@@ -342,3 +342,23 @@ def test_encoder_tile_raster_bit_identical(raster):
         out.append(m.encode(x).float().cpu())
         del m
     assert torch.equal(out[0], out[1])
+
+
+# every non-default formulation a handle option selects, against the reference goldens (high-margin
+# recipe: greedy and beam-5 ids exact in bf16, as the defaults are in check_16bit_greedy / _beam5)
+ALT_OPTIONS = [{"merge_v": 0}, {"xenc_split": 4}, {"xenc_split": 12}, {"xenc_variant": 0}, {"xenc_variant": 2},
+               {"xenc_variant": 3}, {"decode_contexts": 1}, {"enc_flash": 2}, {"flash_split": 1},
+               {"beam_xattn": 1}, {"beam_xattn": 2}, {"ring_kt": 1}, {"lean": 0, "lean_x": 0}]
+
+
+@pytest.mark.parametrize("opts", ALT_OPTIONS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
+def test_small_bf16_option_formulations_match_reference(opts):
+    g, meta = golden("small", "margin", 1)
+    dims = get_dims("small")
+    m = WhisperCB.from_state_dict(dims, weights("small", 1, "margin"), dtype="bf16", options=opts)
+    x = mel_of(dims, meta["B"])
+    ids = m.generate(x, max_length=meta["n_tokens"]).cpu().numpy()
+    assert np.array_equal(ids, g["greedy_ids"]), (opts, ids, g["greedy_ids"])
+    b = m.generate(x, max_length=meta["beam_len"], num_beams=5).cpu().numpy()
+    assert b.shape == g["beam5_ids"].shape and np.array_equal(b, g["beam5_ids"]), (opts, b, g["beam5_ids"])
+    del m
