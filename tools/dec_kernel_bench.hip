@@ -143,7 +143,7 @@ void run_lean_stamped(const char* name, GemmArgs g0) {
 }
 
 // the lean out-projection with fragment-major weights (layout only: the bench's weights are zeros)
-template <int NW, int KPW, bool LN, int EPI>
+template <int NW, int KPW, bool LN, int EPI, int MF = 1>
 void run_wfm(const char* name, GemmArgs g0, bool stamped) {
   const long wbytes = (long)g0.N * g0.K * 2;
   const long nreg = (long)(kW / wbytes);
@@ -160,10 +160,10 @@ void run_wfm(const char* name, GemmArgs g0, bool stamped) {
     p.M = g0.M; p.N = g0.N; p.lda = (int)g0.lda; p.ldo = (int)g0.ldc;
     p.n_split = g0.n_split; p.kvB = g0.hs_B; p.kvH = g0.hs_H; p.kvT = g0.kv_T; p.grp_n = 0; p.grp_off = 0;
     p.stamp = st ? st + (long)i * nwg * 4 : nullptr;
-    hipLaunchKernelGGL((dec_lean_kernel<bf16_t, 1, NW, KPW, LN, EPI, false, false, true>), dim3((g0.N + 15) / 16, (g0.M + 15) / 16),
-                       dim3(NW * 64), 0, s, p);
+    hipLaunchKernelGGL((dec_lean_kernel<bf16_t, MF, NW, KPW, LN, EPI, false, false, true>),
+                       dim3((g0.N + 15) / 16, (g0.M + 16 * MF - 1) / (16 * MF)), dim3(NW * 64), 0, s, p);
   });
-  printf("%-40s lean, fragment-major W: %6.2f us/launch\n", name, us);
+  printf("%-40s lean, fragment-major W, %d-row wgs: %6.2f us/launch\n", name, 16 * MF, us);
   if (st) CHK(hipFree(st));
   fflush(stdout);
 }
@@ -322,6 +322,7 @@ int main() {
   run_lean("out", o);
   run_lean_stamped("out", o);
   run_wfm<4, 6, false, 1>("out", o, false);
+  run_wfm<4, 6, false, 1, 2>("out", o, false);
   run<2, 4, 6, 0>("out: MF=2", o, 48);
   run<1, 8, 3, 0>("out: NW=8", o, 48);
   run<2, 8, 3, 0>("out: MF=2 NW=8", o, 48);
@@ -344,6 +345,7 @@ int main() {
   run_lean("xq", xq);
   run_lean_stamped("xq", xq);
   run_wfm<4, 6, true, 0>("xq", xq, false);
+  run_wfm<4, 6, true, 0, 2>("xq", xq, false);
   run<2, 4, 6, 2>("xq: MF=2", xq, 48);
   GemmArgs xq0 = xq; xq0.ln_w = xq0.ln_b = nullptr; xq0.ln_a16 = nullptr; xq0.A = g_a;
   run<1, 4, 6, 0>("xq without LN", xq0, 48);
@@ -358,6 +360,7 @@ int main() {
   run_lean("fc2", f2);
   run_lean_stamped("fc2", f2);
   run_wfm<8, 12, false, 1>("fc2", f2, false);
+  run_wfm<8, 12, false, 1, 2>("fc2", f2, false);
   run_wfm<16, 6, false, 1>("fc2 NW=16", f2, false);
   run<2, 8, 12, 0>("fc2: MF=2", f2, 48);
   run<1, 16, 6, 0>("fc2: NW=16", f2, 48);
