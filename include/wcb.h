@@ -78,7 +78,8 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "ring_kt" 1/2      decode rows > 64: 64-deep K sub-tiles per LDS-ring stage of the projection tiles
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)
  *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave), 4 (64 queries, default)
- *   "enc_raster" n     encoder GEMM tile order: bands of n row panels, column tiles outer (0: row-major) */
+ *   "enc_raster" n     encoder GEMM tile order: bands of n row panels, column tiles outer (8, default;
+ *                      0: row-major); bit-identical */
 int wcb_set_option(wcb_handle* h, const char* name, int value);
 
 /* replaces from_pretrained / load_state_dict: one HF state-dict tensor (host f32, C order), staged

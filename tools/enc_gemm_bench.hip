@@ -73,8 +73,10 @@ int main(int argc, char** argv) {
   }
   const Variant vars[] = {
       {"256x256", launch_ring<bf, 256, 256, 2, 4, 2>},
-      {"256x256 no prio", launch_ring<bf, 256, 256, 2, 4, 2, 128, 0>},
+      {"256x256 raster 4", [](const GemmArgs& g, hipStream_t s) { GemmArgs h = g; h.raster = 4; launch_ring<bf, 256, 256, 2, 4, 2>(h, s); }},
+      {"256x256 raster 8", [](const GemmArgs& g, hipStream_t s) { GemmArgs h = g; h.raster = 8; launch_ring<bf, 256, 256, 2, 4, 2>(h, s); }},
       {"256x192", launch_ring<bf, 256, 192, 2, 4, 2>},
+      {"256x192 raster 8", [](const GemmArgs& g, hipStream_t s) { GemmArgs h = g; h.raster = 8; launch_ring<bf, 256, 192, 2, 4, 2>(h, s); }},
   };
   const int nv = sizeof(vars) / sizeof(vars[0]);
   const int rounds = argc > 1 ? atoi(argv[1]) : 5;

@@ -217,8 +217,9 @@ struct wcb_handle {
   int lean_x = 1;
   struct wcb_state* step_state = nullptr;   // the active step-wise decode (wcb_decode_begin), if any
   // encoder GEMM tile order (option "enc_raster"): bands of n row panels with the column tiles outer
-  // (GemmArgs::raster; 0 = row-major)
-  int enc_raster = 0;
+  // (GemmArgs::raster; 0 = row-major). 8 measured best with the round-3 ring kernel (whisper-small:
+  // QKV 185 -> 177, fc1 297 -> 281, out 118 -> 116 us, fc2 within noise; profiles/r03f_enc_gemm_bench.txt)
+  int enc_raster = 8;
   // decode projections on gemm_dec_kernel (K supported): the LayerNorm consumers compute their row
   // statistics from the rows they load, so the producers publish no per-16-column partial sums
   bool dec_gemm = false;
