@@ -79,15 +79,15 @@ def _cpu_share():
     return share, aff, quota
 
 
-def cpu_baseline(size: str, n_tokens: int, n_phr: int, boost: float, seed: int = 0, clips: int = 1, reps: int = 5,
+def cpu_baseline(size: str, n_tokens: int, n_phr: int, boost: float, seed: int = 0, clips: int = 1, reps: int = 10,
                  warmups: int = 3):
     """the fp32 PyTorch-CPU restatement of the reference path (oracle/whisper_torch.py,
     test infrastructure) on this host's CPU share (affinity mask / cgroup quota; os.cpu_count() counts
     the whole host), on a bounded sample of the same workload — `clips` clip(s) per run: log-mel +
     encoder + n_tokens greedy tokens with the same bias list and boost — in the reference's two decode
     modes: (i) use_cache=False exactly as scripts/evaluation.py:178 configures generate(), (ii)
-    KV-cached. `warmups` untimed runs, then the median of `reps` timed runs per mode (the runs of the
-    two modes interleaved). `value` = mode (ii), the faster one. Nothing is extrapolated: the sample
+    KV-cached. `warmups` untimed runs (three), then the median of `reps` (>= 10) timed
+    runs per mode (the runs of the two modes interleaved). `value` = mode (ii), the faster one. Nothing is extrapolated: the sample
     is `clips` clip(s) per run, not the 32-clip batch."""
     import torch
     from oracle import whisper_torch as WT

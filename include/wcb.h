@@ -65,16 +65,20 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "flash_split" n    key ranges per (clip, head) of the beam-search cross-attention (flash kernel), 1..8
  *   "beam_xattn" v     beam-search cross-attention: keys split over the waves of one (clip, head) workgroup
  *                      (1: 4 waves x 2 LDS stages, 2: 2 x 4, 3: 2 x 5) or the flash kernel over key ranges (0)
- *   "ln_fold" 0/1      decode rows > 64 (16-bit): LayerNorm folded into the projection, or its own launch
+ *   "ln_fold" 0/1      decode rows > 64 (16-bit): LayerNorm folded into the projection (1, default: finalize
+ *                      keeps W·diag(γ) copies of QKV / cross-q / fc1, ≈ +1/4 of the decoder weights), or its own
+ *                      launch (0); before finalize
  *   "merge_v" 0/1      greedy encoder-space cross-attention: range merge and W_v fused (1) or two launches
  *   "xqk" 0/1          greedy encoder-space cross-attention query: LN + q_proj + W_k,hᵀ in one launch (1) or
  *                      two decode GEMMs (0, default: measured faster); bit-identical
  *   "lean" 0/1         decode projections of <= 64 rows (16-bit) on the lean single-tile kernel (1, default)
- *                      or the general decode GEMM (0); bit-identical. With it the LM head reads the token
- *                      embedding's fragment-major copy (built at finalize, vocab_pad x d_model 16-bit)
+ *                      or the general decode GEMM (0); bit-identical. Before finalize: with it finalize keeps
+ *                      fragment-major copies of the decoder projection weights and the token embedding (the
+ *                      decoder weights once more in memory, e.g. ≈ +1.8 GB at large-v3 fp16)
  *   "lean_x" 0/1       lean path, one position per row: the residual writers also write the 16-bit rows
  *                      fragment-major for the LayerNorm-fused QKV / xq / fc1 (1, default); bit-identical
- *   "decode_contexts" n  decode contexts in flight (1..4): calls decode on n streams from n buffers
+ *   "decode_contexts" n  decode contexts in flight (1..4): calls decode on n streams from n buffers (4 is
+ *                      refused while a step-wise decode owns context 3)
  *   "ring_kt" 1/2      decode rows > 64: 64-deep K sub-tiles per LDS-ring stage of the projection tiles
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)
  *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave), 4 (64 queries, default)
@@ -149,6 +153,19 @@ int wcb_synchronize(wcb_handle* h);
  * dec_ids int32 DEVICE [B][T] → logits f32 DEVICE [B][T][vocab]; enc_out as in wcb_encode. */
 int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, int T, float* logits,
                 void* enc_out, void* stream);
+
+/* replaces forward(encoder_outputs=..., decoder_input_ids) (models/whisper_medical.py:54-55, 93-111, the
+ * decoder on a given encoder output, no re-encode): enc = encoder output [B][1500][d] in the model dtype
+ * (DEVICE, e.g. wcb_encode's enc_out; copied / projected, not retained) → logits as wcb_forward, bit for
+ * bit the logits wcb_forward computes from the mel that produced enc. */
+int wcb_forward_enc(wcb_handle* h, const void* enc, int B, const int32_t* dec_ids, int T, float* logits, void* stream);
+
+/* replaces forward(..., use_cache=True) / forward(..., past_key_values=...) (models/whisper_medical.py:54-55,
+ * 89-110: the decoder's self-attention KV cache carried between calls): `st` = a step-wise state begun with
+ * wcb_decode_begin(enc, B, 1, NULL, ...) (it owns the encoder output and the cache); each call appends
+ * positions [n, n + T) for dec_ids [B][T] (int32, DEVICE), n = the positions appended so far, and writes
+ * their logits [B][T][vocab] (f32, DEVICE). A state used here takes no wcb_decode_step. */
+int wcb_forward_cached(wcb_handle* h, wcb_state* st, const int32_t* dec_ids, int T, float* logits, void* stream);
 
 /* bias list: n_phrases token sequences, phrase i = tokens[offsets[i] .. offsets[i+1]) (host
  * arrays), built into an Aho-Corasick automaton on the device. word_start (host, [vocab] bytes, or

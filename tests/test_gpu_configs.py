@@ -22,7 +22,7 @@ from oracle import whisper_np as W  # noqa: E402
 from oracle.beam_np import generate_beam  # noqa: E402
 from whisper_context_biasing_amd.config import get_dims  # noqa: E402
 from whisper_context_biasing_amd.model import WhisperCB  # noqa: E402
-from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list  # noqa: E402
+from whisper_context_biasing_amd.synth import synth_batch, synth_bias_list, synth_word_start  # noqa: E402
 from whisper_context_biasing_amd.weights import make_weights  # noqa: E402
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -210,6 +210,46 @@ def test_c2_small_b32_1000_phrase_boost(recipe, seed, dtype):
             assert n >= 0.75 * ref.size, (n, ref.size)
 
 
+@pytest.mark.parametrize("recipe,seed,dtype", [("margin", 1, "bf16"), ("margin", 1, "f32"), ("diverse", 0, "bf16")])
+def test_c2_timed_path_pcm_to_ids(recipe, seed, dtype):
+    """The bench's timed step end to end (bench.py step(): 32 synthetic clips of PCM resident on the
+    device → wcb_log_mel → wcb_generate, 64 tokens with EOS masked, the 1000-phrase list behind the
+    word-start gate, lambda 2) against the oracle's own PCM → log-mel → greedy on the same clips
+    (data_utils/data_loader.py:171-172 → scripts/evaluation.py:199-206): rows 0-3 exact in f32 and
+    margin-gated in 16-bit with every checkable token checked. The whole batch decoded from the library's
+    mel must also equal the batch decoded from the oracle's mel (f32 exact; 16-bit on the high-margin
+    recipe exact as well), so the front end's 2e-5 differences flip nothing on the timed path."""
+    dims = get_dims("small")
+    m = model("small", seed, recipe, dtype)
+    ws = synth_word_start(dims.eos_token_id, dims.vocab)
+    phrases = synth_bias_list(1000, eot=dims.eos_token_id)
+    pcm = synth_batch(32)
+    m.set_word_start(ws)
+    try:
+        kw = dict(max_length=64, min_new_tokens=64, bias_list=phrases, bias_boost=2.0)
+        mel_lib = m.log_mel(torch.from_numpy(pcm).cuda())
+        ids = m.generate(mel_lib, **kw).cpu().numpy()
+        mel_ora = W.log_mel(pcm, dims.n_mel)
+        ids_ora_mel = m.generate(torch.from_numpy(mel_ora), **kw).cpu().numpy()
+    finally:
+        m.set_word_start(None)
+    assert ids.shape == (32, 64)
+    assert np.abs(mel_lib.cpu().numpy() - mel_ora).max() < 1e-4
+    om = W.OracleModel.from_dims(dims, weights("small", seed, recipe))
+    ref, margin = om.generate(mel_ora[:4], max_length=64, min_new_tokens=64, bias=phrases, bias_boost=2.0,
+                              word_start=ws, return_margins=True, trim=False)
+    if dtype == "f32":
+        assert np.array_equal(ids[:4], ref), (ids[:4], ref)
+        assert np.array_equal(ids, ids_ora_mel)
+    else:
+        checkable = sum(int(np.argmax(mg < TAU)) if (mg < TAU).any() else mg.size for mg in margin)
+        n = gated_equal(ids[:4], ref, margin, name=f"c2-timed-{dtype}-{recipe}")
+        assert n == checkable
+        if recipe == "margin":
+            assert n >= 0.75 * ref.size, (n, ref.size)
+            assert np.array_equal(ids, ids_ora_mel), np.argwhere(ids != ids_ora_mel)[:8]
+
+
 # ------------------------------------------------------------------ whisper-medium, 24 layers (C3)
 @pytest.mark.parametrize("recipe,seed", [("margin", 1), ("diverse", 0)])
 def test_medium_f32_greedy_and_beam5_match_reference(recipe, seed):
@@ -243,6 +283,32 @@ def test_c5_large_v3_f16_16clips_beam5_5000_phrase_boost():
     rows, fp16 with the encoder clamp, 5000 phrases (lambda 2), high-margin recipe: clip 0 identical
     to the oracle, clips 14-15 identical to a 2-clip call."""
     check_beam5_boost("large-v3", "f16", 5000, 16, 1)
+
+
+def test_c5_timed_path_pcm_to_beams():
+    """C5's timed step end to end: large-v3's 128-bin front end on the device (PCM → wcb_log_mel), then
+    16 clips x beam 5, fp16, the 5000-phrase list behind the word-start gate (lambda 2), against the oracle's
+    PCM → log-mel → beam search on clip 0 (high-margin recipe: identical beams), and the library's mel within
+    1e-4 of the oracle's."""
+    dims = get_dims("large-v3")
+    m = model("large-v3", 1, "margin", "f16")
+    ws = synth_word_start(dims.eos_token_id, dims.vocab)
+    phrases = synth_bias_list(5000, eot=dims.eos_token_id)
+    pcm = synth_batch(16)
+    m.set_word_start(ws)
+    try:
+        mel_lib = m.log_mel(torch.from_numpy(pcm).cuda())
+        ids = m.generate(mel_lib, max_length=8, num_beams=5, bias_list=phrases, bias_boost=2.0).cpu().numpy()
+    finally:
+        m.set_word_start(None)
+    assert ids.shape[0] == 16 and mel_lib.shape == (16, 128, 3000)
+    mel_ora = W.log_mel(pcm[:1], dims.n_mel)
+    assert np.abs(mel_lib[:1].cpu().numpy() - mel_ora).max() < 1e-4
+    om = W.OracleModel.from_dims(dims, weights("large-v3", 1, "margin"))
+    ref = generate_beam(om, mel=mel_ora, num_beams=5, max_length=8, bias=phrases, bias_boost=2.0, word_start=ws)
+    w = max(ids.shape[1], ref.shape[1])
+    pad = lambda a: np.pad(a, ((0, 0), (0, w - a.shape[1])), constant_values=dims.pad_token_id)
+    assert np.array_equal(pad(ids[:1]), pad(ref)), (ids[:1], ref)
 
 
 # ------------------------------------------------------------------ prompt-conditioned decode (causal prefill)

@@ -1,6 +1,10 @@
 """GPU: step-wise greedy decoding (wcb_decode_begin / wcb_decode_step) against
 generate() on the same clips: the same decode step one token per call, so the ids must be identical
-(f32 K/V cross-attention and bf16 encoder-space paths, the bias boost, a prompt prefix)."""
+(f32 K/V cross-attention and bf16 encoder-space paths, the bias boost, a prompt prefix); and the
+reference forward()'s encoder_outputs / past_key_values / use_cache arguments (wcb_forward_enc,
+wcb_forward_cached)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -57,3 +61,110 @@ def test_stepwise_scores_lm_head_layernorm_split_bit_identical(size, dtype, B):
         del m
     assert torch.equal(out[0][0], out[1][0])
     assert torch.equal(out[0][1], out[1][1])
+
+
+# ---------------------------------------------------------------- forward(encoder_outputs / past_key_values)
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+PROBE = np.array([0, 1, 2, 13, 220, 1000, 5000, 12345, 25000, 40000, 50255, 50256, 50257, 50258, 50300, 50363,
+                  51000, 51863])
+
+
+def test_forward_encoder_outputs_bit_identical_and_golden():
+    """forward(encoder_outputs=..., decoder_input_ids=...) decodes from the given encoder state without
+    re-encoding (models/whisper_medical.py:54-55, 93-111 → wcb_forward_enc): logits bit-identical to
+    forward(input_features=...) for every form HF accepts (tensor, tuple, BaseModelOutput-like), and within
+    5e-4 of the reference's teacher-forced logits (micro golden, f32); input_features=None works."""
+    from types import SimpleNamespace
+    g = np.load(os.path.join(GOLD, "model_micro_diverse_s0.npz"))
+    dims = get_dims("micro")
+    m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=0, recipe="diverse"), dtype="f32")
+    x = torch.from_numpy(W.log_mel(synth_batch(2), dims.n_mel))
+    ids = torch.from_numpy(g["tf_decoder_input_ids"])
+    full = m.forward(x, decoder_input_ids=ids)
+    enc = m.encode(x)
+    assert torch.equal(enc, full.encoder_last_hidden_state)
+    for form in (enc, (enc,), SimpleNamespace(last_hidden_state=enc)):
+        out = m.forward(encoder_outputs=form, decoder_input_ids=ids)
+        assert torch.equal(out.logits, full.logits)
+    np.testing.assert_allclose(full.logits.cpu().numpy()[:, :, PROBE], g["tf_logits_probe"], atol=5e-4, rtol=1e-4)
+    with pytest.raises(ValueError):
+        m.forward(decoder_input_ids=ids)                       # neither input_features nor encoder_outputs
+    with pytest.raises(ValueError):
+        m.forward(encoder_outputs=enc[:, :100], decoder_input_ids=ids)
+    with pytest.raises(NotImplementedError):
+        m.forward(x, decoder_input_ids=ids, decoder_inputs_embeds=torch.zeros(1))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_forward_encoder_outputs_bit_identical_small(dtype):
+    """The same at whisper-small (bf16: the encoder-space cross-attention reads the given encoder output)."""
+    dims = get_dims("small")
+    m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=1, recipe="margin"), dtype=dtype)
+    B = 5
+    x = torch.from_numpy(W.log_mel(synth_batch(B), dims.n_mel))
+    rng = np.random.default_rng(5)
+    ids = torch.from_numpy(np.concatenate([np.full((B, 1), dims.decoder_start_token_id),
+                                           rng.integers(0, 50000, (B, 9))], 1))
+    a = m.forward(x, decoder_input_ids=ids)
+    b = m.forward(encoder_outputs=a.encoder_last_hidden_state, decoder_input_ids=ids)
+    assert torch.equal(a.logits, b.logits)
+
+
+@pytest.mark.parametrize("split", [1, 4, 7])
+def test_forward_past_key_values_continues_the_cache(split):
+    """forward(..., use_cache=True) returns the decoder KV cache as past_key_values; forward(next ids,
+    past_key_values=cache) appends positions and returns only their logits (models/whisper_medical.py:
+    54-55, 89-110 → wcb_forward_cached). The two halves equal the one-pass logits (f32, within 1e-4:
+    the halves run as other row counts) and the reference golden within 5e-4."""
+    g = np.load(os.path.join(GOLD, "model_micro_diverse_s0.npz"))
+    dims = get_dims("micro")
+    m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=0, recipe="diverse"), dtype="f32")
+    x = torch.from_numpy(W.log_mel(synth_batch(2), dims.n_mel))
+    ids = torch.from_numpy(g["tf_decoder_input_ids"])
+    full = m.forward(x, decoder_input_ids=ids).logits
+    o1 = m.forward(x, decoder_input_ids=ids[:, :split], use_cache=True)
+    cache = o1.past_key_values
+    assert cache is not None and cache.get_seq_length() == split
+    parts = [o1.logits]
+    for t0 in range(split, ids.shape[1], 3):          # several continuation calls
+        o = m.forward(decoder_input_ids=ids[:, t0:t0 + 3], past_key_values=cache)
+        assert o.past_key_values is cache
+        parts.append(o.logits)
+    got = torch.cat(parts, 1)
+    assert cache.get_seq_length() == ids.shape[1]
+    torch.testing.assert_close(got, full, atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(got.cpu().numpy()[:, :, PROBE], g["tf_logits_probe"], atol=5e-4, rtol=1e-4)
+    with pytest.raises(TypeError):
+        m.forward(decoder_input_ids=ids[:, :1], past_key_values=((torch.zeros(1),),))
+    cache.close()
+    # the state slot is free again: a step-wise decode can start
+    dec = m.decode_begin(m.encode(x), min_new_tokens=2)
+    dec.step()
+    dec.close()
+
+
+def test_decode_contexts_guard_while_stepwise_decode_is_open():
+    """The step-wise state owns decode context 3: raising decode_contexts to 4 while it is
+    open is refused, and generate() calls interleaved with its steps at decode_contexts 3 leave both
+    decodes unchanged (micro f32)."""
+    from whisper_context_biasing_amd import _lib
+    dims = get_dims("micro")
+    m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=0, recipe="diverse"), dtype="f32")
+    x = torch.from_numpy(W.log_mel(synth_batch(3), dims.n_mel))
+    n = 10
+    ref_gen = m.generate(x, max_length=n, min_new_tokens=n).cpu().numpy()
+    dec = m.decode_begin(m.encode(x), min_new_tokens=n)
+    ref_steps = torch.stack([dec.step()[0] for _ in range(n)], 1).cpu().numpy()
+    dec.close()
+    m.set_option("decode_contexts", 3)
+    dec = m.decode_begin(m.encode(x), min_new_tokens=n)
+    with pytest.raises(_lib.WcbError, match="decode_contexts"):
+        m.set_option("decode_contexts", 4)
+    steps = []
+    for i in range(n):
+        steps.append(dec.step()[0])
+        if i % 3 == 0:                                    # generate() cycles through contexts 0-2 meanwhile
+            assert np.array_equal(m.generate(x, max_length=n, min_new_tokens=n).cpu().numpy(), ref_gen)
+    dec.close()
+    assert np.array_equal(torch.stack(steps, 1).cpu().numpy(), ref_steps)
+    m.set_option("decode_contexts", 4)                   # allowed again once the state is closed

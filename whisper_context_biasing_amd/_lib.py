@@ -51,6 +51,8 @@ SIGNATURES = {
     "wcb_decode_step": (C.c_int, [_P, _P, _P, _P, _P, _P]),
     "wcb_decode_end": (C.c_int, [_P, _P]),
     "wcb_forward": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, _P, _P, _P]),
+    "wcb_forward_enc": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, _P, _P]),
+    "wcb_forward_cached": (C.c_int, [_P, _P, _P, C.c_int, _P, _P]),
     "wcb_bias_create": (C.c_int, [_P, _P, _P, C.c_int, _P, C.POINTER(_P)]),
     "wcb_bias_destroy": (None, [_P]),
     "wcb_bias_num_states": (C.c_int, [_P]),

@@ -13,6 +13,7 @@
 //   workgroup's waves, fragments straight from global memory (weights are streamed once), wave
 //   partials reduced through LDS.
 #pragma once
+#include <stdexcept>
 #include "common.h"
 #include "kernels.h"
 
@@ -1524,10 +1525,8 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
     // rows (measured C2: 1.074 vs 1.147 ms/token with 32-row workgroups); the LM head walks the
     // vocabulary persistently with 32-row workgroups, reading every weight tile once
     if (g.lean && launch_lean<T>(g, s)) return;
-    if (g.a_fm || g.c_fm || g.out16_fm) {   // the runtime pairs fragment-major operands only where the lean path takes both
-      fprintf(stderr, "wcb: internal error: fragment-major operand on a launch the lean kernel does not cover\n");
-      abort();
-    }
+    if (g.a_fm || g.c_fm || g.out16_fm)   // the runtime pairs fragment-major operands only where the lean path takes both
+      throw std::runtime_error("internal error: fragment-major operand on a launch the lean kernel does not cover");
     const bool mf1 = (g.M <= 64 && !(g.sel_val && g.M > 16)) || g.K >= 4096;
     const bool ok = mf1 ? launch_dec_mf<T, 1>(g, s) : launch_dec_mf<T, 2>(g, s);
     if (ok) return;

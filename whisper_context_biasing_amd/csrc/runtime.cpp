@@ -181,7 +181,7 @@ struct wcb_handle {
   int merge_v = 1;
   // greedy cross-attention query (<= 64 rows, encoder space): LN + q_proj + W_k,hᵀ as one launch
   // (option "xqk"; 0 = the two decode GEMMs, bit-identical)
-  int xqk = 0;   // measured (C2 decode alone): 0.53-0.61 ms/token unfused vs 0.67-0.69 fused
+  int xqk = 0;   // measured slower fused (round 2, C2 decode alone); kept as a bit-identity check
   // decode rows > 64: 64-deep K sub-tiles per ring stage of the 64x32 / 32x32 tiles (option "ring_kt",
   // 1 or 2; C5 1,594 -> 1,644 audio-s/s)
   int ring_kt = 2;
@@ -545,6 +545,9 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       if (!h->xmode) h->beam_xmode = 0;
     } else if (n == "decode_contexts") {
       REQUIRE(value >= 1 && value <= wcb_handle::kMaxCtx, "option decode_contexts: 1..4");
+      // the step-wise state owns context kMaxCtx-1: generate() may not cycle into it while it is open
+      REQUIRE(!h->step_state || value < wcb_handle::kMaxCtx,
+              "option decode_contexts: 4 while a step-wise decode is active (wcb_decode_end first)");
       h->nctx = value;
     } else if (n == "group_rows") {
       REQUIRE(value >= 16 && value <= 512, "option group_rows: 16..512");
@@ -568,12 +571,16 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       REQUIRE(value >= 0 && value <= 64, "option enc_raster: 0..64");
       h->enc_raster = value;
     } else if (n == "lean") {
+      // the lean path's fragment-major weight copies are built at finalize only when it is on
+      REQUIRE(!h->ready, "option lean selects weight layouts: set it before wcb_finalize_weights");
       h->lean = value != 0;
     } else if (n == "lean_x") {
       h->lean_x = value != 0;
     } else if (n == "merge_v") {
       h->merge_v = value != 0;
     } else if (n == "ln_fold") {
+      // the folded W·diag(γ) copies are built at finalize only when it is on
+      REQUIRE(!h->ready, "option ln_fold selects weight layouts: set it before wcb_finalize_weights");
       h->ln_fold = value != 0;
     } else if (n == "beam_xattn") {
       REQUIRE(value >= 0 && value <= 3, "option beam_xattn: 0..3");
@@ -751,14 +758,16 @@ int wcb_finalize_weights(wcb_handle* h) {
           ln_fold(h->dt, W, N, d, gam, bet, bias, u, c, st);          // c (u overwritten below)
           ln_fold(h->dt, Wg, N, d, nullptr, nullptr, nullptr, u, nullptr, st);
         };
-        fold(lw.qkv_w, 3 * d, lw.ln1_w, lw.ln1_b, lw.qkv_b, lw.qkv_wg, lw.ln1_u, lw.ln1_c);
-        fold(lw.xq_w, d, lw.lnx_w, lw.lnx_b, lw.xq_b, lw.xq_wg, lw.lnx_u, lw.lnx_c);
-        fold(lw.fc1_w, F, lw.ln2_w, lw.ln2_b, lw.fc1_b, lw.fc1_wg, lw.ln2_u, lw.ln2_c);
+        if (h->ln_fold) {   // (decode rows > 64 only; memory: QKV + xq + fc1 weights once more per layer)
+          fold(lw.qkv_w, 3 * d, lw.ln1_w, lw.ln1_b, lw.qkv_b, lw.qkv_wg, lw.ln1_u, lw.ln1_c);
+          fold(lw.xq_w, d, lw.lnx_w, lw.lnx_b, lw.xq_b, lw.xq_wg, lw.lnx_u, lw.lnx_c);
+          fold(lw.fc1_w, F, lw.ln2_w, lw.ln2_b, lw.fc1_b, lw.fc1_wg, lw.ln2_u, lw.ln2_c);
+        }
         // fragment-major copies for the lean decode projections (<= 64 rows): each weight wave-instruction
         // then reads 1 KiB contiguous (tools/dec_kernel_bench.hip: out 3.75 -> 3.16, fc2 8.39 -> 6.43 µs)
         auto fm = [&](const void* W, int N, int K) -> void* {
           int nw = 0, kpw = 0;
-          if (!W || N % 16 || !lean_cfg(K, nw, kpw)) return nullptr;
+          if (!h->lean || !W || N % 16 || !lean_cfg(K, nw, kpw)) return nullptr;   // (lean path only)
           void* p = h->own((size_t)N * K * e);
           frag_major(h->dt, W, N, K, nw, kpw, p, st);
           return p;
@@ -783,7 +792,7 @@ int wcb_finalize_weights(wcb_handle* h) {
     h->dec_pos = T_("model.decoder.embed_positions.weight", (size_t)h->d.n_text_ctx * d);
     if (h->dt != kF32) {   // the greedy LM head's column walk reads a fragment-major copy (zero rows past V)
       int nw = 0, kpw = 0;
-      if (lean_cfg(d, nw, kpw)) {
+      if (h->lean && lean_cfg(d, nw, kpw)) {
         h->tok_emb_fm = h->own((size_t)h->vocab_pad * d * e);
         frag_major(h->dt, h->tok_emb, h->vocab_pad, d, nw, kpw, h->tok_emb_fm, st);
       }
@@ -1583,6 +1592,7 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
 struct wcb_state {
   wcb_handle* h = nullptr;
   int B = 0, P = 1, T = 0, steps = 0, max_new = 0, min_new = 0, xmode = 1;
+  int fwd = 0;   // positions appended by wcb_forward_cached (a forward-cache state takes no decode steps)
   float lam = 0.f;
   uint64_t bias_id = 0;
 };
@@ -1645,6 +1655,7 @@ int wcb_decode_step(wcb_handle* h, wcb_state* st, const wcb_bias* bias, int32_t*
   return guarded(h, [&] {
     REQUIRE(h && st && st->h == h && h->step_state == st && next_ids, "bad argument (state of this handle, next_ids)");
     REQUIRE(st->steps < st->max_new, "max_target_positions reached");
+    REQUIRE(st->fwd == 0, "wcb_decode_step on a forward cache (wcb_forward_cached state)");
     const wcb_bias* bs = bias ? bias : h->empty_bias.get();
     REQUIRE(bs == h->empty_bias.get() || bs->owner == h, "bias automaton was created on another handle");
     REQUIRE(bs->vocab == h->d.vocab, "bias automaton built for another vocabulary");
@@ -1683,6 +1694,23 @@ int wcb_synchronize(wcb_handle* h) {
   });
 }
 
+// teacher forcing on decode context `buf` once its encoder-side buffer is ready (ev_xkv[buf] recorded
+// on the encoder stream): causal prefill of positions 0 .. T-1 of every row, logits of every position
+static void forward_decode(wcb_handle* h, int buf, int B, const int32_t* dec_ids, int T, float* logits) {
+  DecCtx& D = h->dc[buf];
+  HIPCHK(hipStreamWaitEvent(D.hs, h->ev_xkv[buf], 0));
+  int* ints = D.ints.as<int>();
+  HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 4 * B) * 4, D.hs));
+  for (int p0 = 0, np; p0 < T; p0 += np) {
+    np = std::min(prefill_chunk(B), T - p0);
+    StepCfg sc{B, T, 1, buf, true, false, logits + (size_t)p0 * h->d.vocab, (long)T * h->d.vocab, nullptr, 0.f,
+               0, nullptr, 0};
+    sc.xmode = h->xmode;
+    prefill_step(h, sc, np, dec_ids, T);
+  }
+  HIPCHK(hipEventRecord(h->ev_dec[buf], D.hs));
+}
+
 int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, int T, float* logits, void* enc_out,
                 void* stream) {
   return guarded(h, [&] {
@@ -1693,7 +1721,6 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
     ensure_enc_ws(h, B);
     ensure_dec_ws(h, B, B, T, 1, h->xmode, B * std::min(prefill_chunk(B), T));
     const int buf = h->gen_count++ % h->nctx;
-    DecCtx& D = h->dc[buf];
     sync_in(h, stream, h->he);
     HIPCHK(hipStreamWaitEvent(h->he, h->ev_dec[buf], 0));
     const size_t enc_bytes = (size_t)B * h->S() * h->d.d_model * esize(h->d.dtype);
@@ -1706,18 +1733,56 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
       cross_kv(h, B, buf, eo);
     }
     HIPCHK(hipEventRecord(h->ev_xkv[buf], h->he));
-    HIPCHK(hipStreamWaitEvent(D.hs, h->ev_xkv[buf], 0));
-    int* ints = D.ints.as<int>();
-    HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 4 * B) * 4, D.hs));
-    // teacher forcing = causal prefill of all T positions, logits of every position
+    forward_decode(h, buf, B, dec_ids, T, logits);
+    sync_out(h, stream, h->dc[buf].hs);
+  });
+}
+
+int wcb_forward_enc(wcb_handle* h, const void* enc, int B, const int32_t* dec_ids, int T, float* logits, void* stream) {
+  return guarded(h, [&] {
+    REQUIRE(h && enc && dec_ids && logits && B > 0 && T > 0, "bad argument");
+    if (!h->ready) throw WcbError(WCB_ERR_STATE, "weights not finalized");
+    REQUIRE(B <= 64, "batch > 64 per handle");
+    REQUIRE(T <= h->d.n_text_ctx, "decoder_input_ids longer than max_target_positions");
+    ensure_dec_ws(h, B, B, T, 1, h->xmode, B * std::min(prefill_chunk(B), T));
+    const int buf = h->gen_count++ % h->nctx;
+    sync_in(h, stream, h->he);
+    HIPCHK(hipStreamWaitEvent(h->he, h->ev_dec[buf], 0));
+    // the given encoder output takes the place of encode_impl's: the same buffer (encoder space) or the
+    // same cross-K/V GEMM over it (K/V formulation), so the logits equal wcb_forward's bit for bit
+    const size_t enc_bytes = (size_t)B * h->S() * h->d.d_model * esize(h->d.dtype);
+    if (h->xmode == 1) HIPCHK(hipMemcpyAsync(h->xkv2[buf].p, enc, enc_bytes, hipMemcpyDeviceToDevice, h->he));
+    else cross_kv(h, B, buf, enc);
+    HIPCHK(hipEventRecord(h->ev_xkv[buf], h->he));
+    forward_decode(h, buf, B, dec_ids, T, logits);
+    sync_out(h, stream, h->dc[buf].hs);
+  });
+}
+
+int wcb_forward_cached(wcb_handle* h, wcb_state* st, const int32_t* dec_ids, int T, float* logits, void* stream) {
+  return guarded(h, [&] {
+    REQUIRE(h && st && st->h == h && h->step_state == st && dec_ids && logits && T > 0,
+            "bad argument (state of this handle, dec_ids, logits, T > 0)");
+    REQUIRE(st->steps == 0, "wcb_forward_cached on a state that wcb_decode_step has advanced");
+    REQUIRE(st->P == 1, "wcb_forward_cached needs a state begun without a prefix");
+    REQUIRE(st->fwd + T <= st->T, "past_key_values + decoder_input_ids exceed max_target_positions");
+    const int ci = wcb_handle::kMaxCtx - 1, B = st->B;
+    ensure_dec_ws(h, B, B, st->T, st->max_new, st->xmode, B * std::min(prefill_chunk(B), T), ci, ci + 1);
+    DecCtx& D = h->dc[ci];
+    sync_in(h, stream, D.hs);
+    // the new ids at their absolute positions of the [B][T] forced buffer (prefill_ids reads src[b·T + pos])
+    if ((size_t)B * st->T * 4 > D.forced.bytes) { quiesce(h); D.forced.ensure((size_t)B * st->T * 4); }
+    HIPCHK(hipMemcpy2DAsync(D.forced.as<int>() + st->fwd, (size_t)st->T * 4, dec_ids, (size_t)T * 4, (size_t)T * 4, B,
+                            hipMemcpyDeviceToDevice, D.hs));
     for (int p0 = 0, np; p0 < T; p0 += np) {
       np = std::min(prefill_chunk(B), T - p0);
-      StepCfg sc{B, T, 1, buf, true, false, logits + (size_t)p0 * h->d.vocab, (long)T * h->d.vocab, nullptr, 0.f,
+      StepCfg sc{B, st->T, 1, ci, true, false, logits + (size_t)p0 * h->d.vocab, (long)T * h->d.vocab, nullptr, 0.f,
                  0, nullptr, 0};
-      sc.xmode = h->xmode;
-      prefill_step(h, sc, np, dec_ids, T);
+      sc.clips = B;
+      sc.xmode = st->xmode;
+      prefill_step(h, sc, np, D.forced.as<int>(), st->T);
     }
-    HIPCHK(hipEventRecord(h->ev_dec[buf], D.hs));
+    st->fwd += T;
     sync_out(h, stream, D.hs);
   });
 }
@@ -1979,12 +2044,14 @@ int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void*
     a.o = o; a.ldo = (long)H * 64; a.o_Sb = 1; a.B = B; a.H = H; a.nkeys = Sk;
     a.variant = variant;
     if (variant == 6 || variant == 7) a.kv_rows = Sk;   // the one-token self-attention kernel (speculative first keys)
-    static DevBuf nk_dev;
+    int* nk_dev = nullptr;
     if (variant == 7) {   // the key count read on the device (decode graphs): the lean self-attention kernel
-      nk_dev.ensure(4);
+      // per-call, stream-ordered scratch (a shared buffer would race between calls on different streams),
+      // written by a kernel whose argument carries the value (no pageable host source)
+      HIPCHK(hipMallocAsync(reinterpret_cast<void**>(&nk_dev), 4, (hipStream_t)stream));
       const int nk1 = Sk - 1;
-      HIPCHK(hipMemcpyAsync(nk_dev.p, &nk1, 4, hipMemcpyHostToDevice, (hipStream_t)stream));
-      a.nkeys_dev = nk_dev.as<int>(); a.nkeys_add = 1;
+      write_i32(nk_dev, &nk1, 1, (hipStream_t)stream);
+      a.nkeys_dev = nk_dev; a.nkeys_add = 1;
     }
     static DevBuf part, ticket;
     if (nsplit > 1) {
@@ -1995,6 +2062,7 @@ int wcb_op_attention_decode(int dtype, const void* q, const void* k, const void*
       a.ticket = ticket.as<int>();
     }
     attention_decode(DType(dtype), a, (hipStream_t)stream);
+    if (nk_dev) HIPCHK(hipFreeAsync(nk_dev, (hipStream_t)stream));
     HIPCHK(hipGetLastError());
   });
 }

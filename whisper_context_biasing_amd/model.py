@@ -52,10 +52,14 @@ class Seq2SeqLMOutput:
     loss: Optional[torch.Tensor]
     logits: torch.Tensor
     encoder_last_hidden_state: torch.Tensor
+    past_key_values: Optional["DecoderCache"] = None
+
+    def to_tuple(self):
+        return tuple(v for v in (self.loss, self.logits, self.past_key_values, self.encoder_last_hidden_state)
+                     if v is not None)
 
     def __getitem__(self, i):
-        return (self.logits, self.encoder_last_hidden_state)[i] if self.loss is None else \
-            (self.loss, self.logits, self.encoder_last_hidden_state)[i]
+        return self.to_tuple()[i]
 
 
 class BiasList:
@@ -110,6 +114,51 @@ class StepDecoder:
             pass
 
 
+class DecoderCache:
+    """`past_key_values` of `WhisperCB.forward(..., use_cache=True)` (models/whisper_medical.py:54-55, 89-110):
+    the decoder's self-attention KV cache and the encoder state, held on the device by a prefix-free step-wise
+    state (wcb_decode_begin); each forward(past_key_values=cache) appends its decoder_input_ids' positions
+    (wcb_forward_cached). One open cache (or StepDecoder) per model: a new use_cache=True forward closes the
+    previous cache, and close() frees it."""
+
+    def __init__(self, model: "WhisperCB", enc: torch.Tensor):
+        self.model, self.encoder_last_hidden_state, self.B = model, enc, enc.shape[0]
+        st = C.c_void_p()
+        _lib.check(model._lib.wcb_decode_begin(model._h, _ptr(enc), self.B, 1, None, 1, 0.0, 0, C.byref(st),
+                                               _stream(model.device)), model._h, "wcb_decode_begin")
+        self._st = st
+        self._seen = 0
+
+    def get_seq_length(self) -> int:   # the HF Cache accessor
+        return self._seen
+
+    def extend(self, ids: torch.Tensor) -> torch.Tensor:
+        m = self.model
+        if not self._st:
+            raise _lib.WcbError("past_key_values was closed (one open cache per model)")
+        if ids.shape[0] != self.B:
+            raise ValueError(f"decoder_input_ids has {ids.shape[0]} rows, the cache {self.B}")
+        T = ids.shape[1]
+        logits = torch.empty(self.B, T, m.dims.vocab, dtype=torch.float32, device=m.device)
+        _lib.check(m._lib.wcb_forward_cached(m._h, self._st, _ptr(ids), T, _ptr(logits), _stream(m.device)),
+                   m._h, "wcb_forward_cached")
+        self._seen += T
+        return logits
+
+    def close(self):
+        if self._st:
+            _lib.check(self.model._lib.wcb_decode_end(self.model._h, self._st), self.model._h, "wcb_decode_end")
+            self._st = None
+            if self.model._cache is self:
+                self.model._cache = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class WhisperCB:
     main_input_name = "input_features"
 
@@ -129,8 +178,6 @@ class WhisperCB:
         _lib.check(lib.wcb_create(C.byref(desc), device, C.byref(h)), None, "wcb_create")
         self._h = h
         self._lib = lib
-        for k, v in (options or {}).items():   # wcb_set_option: alternative formulations (tests)
-            _lib.check(lib.wcb_set_option(h, k.encode(), int(v)), h, f"wcb_set_option({k})")
         self.config = SimpleNamespace(use_cache=True, suppress_tokens=[], forced_decoder_ids=None,
                                       decoder_start_token_id=dims.decoder_start_token_id,
                                       pad_token_id=dims.pad_token_id, eos_token_id=dims.eos_token_id,
@@ -151,6 +198,10 @@ class WhisperCB:
         self._bias_retired: List[BiasList] = []
         self._word_start: Optional[np.ndarray] = None
         self._loaded = False
+        self._cache: Optional["DecoderCache"] = None   # the open forward(use_cache=True) state, if any
+        # options last: a rejected option raises with every attribute __del__ reads already set
+        for k, v in (options or {}).items():   # wcb_set_option: alternative formulations (tests)
+            _lib.check(lib.wcb_set_option(h, k.encode(), int(v)), h, f"wcb_set_option({k})")
 
     # ------------------------------------------------------------------ construction / weights
     @classmethod
@@ -202,9 +253,13 @@ class WhisperCB:
 
     def __del__(self):
         if getattr(self, "_h", None):
-            self._bias_cache.clear()
+            getattr(self, "_bias_cache", {}).clear()
             self._lib.wcb_destroy(self._h)
             self._h = None
+
+    def set_option(self, name: str, value: int) -> None:
+        """wcb_set_option on this handle (alternative formulations; include/wcb.h lists them)."""
+        _lib.check(self._lib.wcb_set_option(self._h, name.encode(), int(value)), self._h, f"wcb_set_option({name})")
 
     # reference-compatible no-ops (scripts/evaluation.py:181-183)
     def freeze_encoder(self):
@@ -385,16 +440,24 @@ class WhisperCB:
         """Step-wise greedy decoding from an encoder output [B, 1500, d] (this model's dtype, on its device):
         the streaming form of generate() (wcb_decode_begin). `prompt_ids` = one prompt for every row or
         a [B, P] array of per-row prompts (decoder_start_token_id is appended as generate() does)."""
-        enc = encoder_outputs.to(self.device, self.torch_dtype).contiguous()
+        enc = self._encoder_state(encoder_outputs)   # [B, 1500, d] checked: the library copies B·1500·d
         B = enc.shape[0]
+        if B > 64:
+            raise ValueError("decode_begin takes at most 64 clips")
         start = self.dims.decoder_start_token_id
         if prompt_ids is None:
             pre = None
         else:
             p = np.asarray(prompt_ids, dtype=np.int32)
-            p = np.broadcast_to(p, (B, p.shape[-1])) if p.ndim == 1 else p
+            if p.ndim == 1:
+                p = np.broadcast_to(p, (B, p.shape[-1]))
+            elif p.ndim != 2 or p.shape[0] != B:
+                raise ValueError(f"prompt_ids must be one prompt or a [{B}, P] array, got shape {p.shape}")
             pre = np.ascontiguousarray(np.concatenate([p, np.full((B, 1), start, np.int32)], axis=1))
-        bl = self.bias_list(bias_list) if (bias_list and bias_boost > 0) else None
+        if isinstance(bias_list, BiasList):   # a prebuilt automaton, as generate() accepts
+            bl = bias_list if bias_boost > 0 else None
+        else:
+            bl = self.bias_list(bias_list) if (bias_list and bias_boost > 0) else None
         st = C.c_void_p()
         _lib.check(self._lib.wcb_decode_begin(self._h, _ptr(enc), B, 1, pre.ctypes.data if pre is not None else None,
                                               pre.shape[1] if pre is not None else 1, float(bias_boost), int(min_new_tokens),
@@ -436,8 +499,36 @@ class WhisperCB:
         self._bias_retired.clear()
 
     # ------------------------------------------------------------------------------- forward
+    # forward() arguments of the reference signature (models/whisper_medical.py:45-65) that change nothing here:
+    # Whisper's encoder ignores attention_mask, and return_dict / output flags left at their defaults
+    _FORWARD_NOOP = {"attention_mask": None, "output_attentions": (None, False), "output_hidden_states": (None, False),
+                     "cache_position": None, "decoder_attention_mask": None}
+
+    def _encoder_state(self, encoder_outputs) -> torch.Tensor:
+        """encoder_outputs as HF accepts it: a BaseModelOutput, a tuple whose [0] is the last hidden state
+        ([tf] modeling_whisper.py WhisperModel.forward), or that tensor; [B, 1500, d], cast to the model dtype."""
+        e = getattr(encoder_outputs, "last_hidden_state", None)
+        if e is None:
+            e = encoder_outputs[0] if isinstance(encoder_outputs, (tuple, list)) else encoder_outputs
+        e = torch.as_tensor(e)
+        if e.dim() == 2:
+            e = e[None]
+        if tuple(e.shape[1:]) != (self.dims.n_audio_ctx, self.dims.d_model):
+            raise ValueError(f"encoder_outputs must be [B, {self.dims.n_audio_ctx}, {self.dims.d_model}], "
+                             f"got {tuple(e.shape)}")
+        return e.to(self.device, self.torch_dtype).contiguous()
+
     def forward(self, input_features=None, decoder_input_ids=None, labels=None, bias_spans=None,
-                encoder_outputs=None, return_dict: bool = True, **kwargs) -> Seq2SeqLMOutput:
+                encoder_outputs=None, past_key_values=None, use_cache=None, return_dict: bool = True,
+                **kwargs) -> Seq2SeqLMOutput:
+        """Teacher-forced decoder logits (models/whisper_medical.py:45-172): from `input_features` (encoded
+        here), from a given `encoder_outputs` (not re-encoded: bit-identical logits), or continuing a
+        `past_key_values` cache. `use_cache=True` returns the cache as `.past_key_values` (a DecoderCache:
+        one open per model); the default keeps none. The reference's weighted-CE `.loss` with `labels`."""
+        for k, v in kwargs.items():
+            ok = self._FORWARD_NOOP.get(k, "missing")
+            if ok == "missing" or (v is not None and not (isinstance(ok, tuple) and v in ok)):
+                raise NotImplementedError(f"forward(): argument {k}={v!r} is not supported by this path")
         if labels is not None:
             labels = torch.as_tensor(labels)
             if labels.shape[1] > self.dims.n_text_ctx:
@@ -450,27 +541,53 @@ class WhisperCB:
                 dec[:, 0] = self.dims.decoder_start_token_id
                 dec[dec == -100] = self.dims.pad_token_id
                 decoder_input_ids = dec
+        if decoder_input_ids is None:
+            raise ValueError("forward() needs decoder_input_ids (or labels)")
         ids = torch.as_tensor(decoder_input_ids).to(self.device, torch.int32).contiguous()
-        x = self._features(input_features)
-        if x.shape[0] > 64:   # 64 clips per library call: split, concatenate
-            outs = [self.forward(x[i:i + 64], decoder_input_ids=ids[i:i + 64]) for i in range(0, x.shape[0], 64)]
-            logits = torch.cat([o.logits for o in outs])
-            enc = torch.cat([o.encoder_last_hidden_state for o in outs])
+
+        def out(logits, enc, cache=None):
             loss = None
             if labels is not None:
                 from .loss import weighted_ce
                 loss = weighted_ce(logits, labels.to(self.device), bias_spans, self.bias_weight)
-            return Seq2SeqLMOutput(loss=loss, logits=logits, encoder_last_hidden_state=enc)
+            return Seq2SeqLMOutput(loss=loss, logits=logits, encoder_last_hidden_state=enc, past_key_values=cache)
+
+        if past_key_values is not None:   # continue a cache: logits of the new positions only
+            if not isinstance(past_key_values, DecoderCache) or past_key_values.model is not self:
+                raise TypeError("past_key_values must be the DecoderCache this model returned (use_cache=True)")
+            return out(past_key_values.extend(ids), past_key_values.encoder_last_hidden_state, past_key_values)
+        if input_features is None and encoder_outputs is None:
+            raise ValueError("You have to specify either input_features or encoder_outputs")
+        if use_cache:
+            enc = self._encoder_state(encoder_outputs) if encoder_outputs is not None else self.encode(input_features)
+            if enc.shape[0] > 64:
+                raise ValueError("use_cache=True takes at most 64 clips per cache")
+            if self._cache is not None:
+                self._cache.close()
+            self._cache = DecoderCache(self, enc)
+            return out(self._cache.extend(ids), enc, self._cache)
+        if encoder_outputs is not None:
+            enc = self._encoder_state(encoder_outputs)
+            B, T = ids.shape
+            if enc.shape[0] != B:
+                raise ValueError(f"encoder_outputs has {enc.shape[0]} clips, decoder_input_ids {B} rows")
+            logits = torch.empty(B, T, self.dims.vocab, dtype=torch.float32, device=self.device)
+            for i in range(0, B, 64):   # 64 clips per library call
+                n = min(64, B - i)
+                _lib.check(self._lib.wcb_forward_enc(self._h, _ptr(enc[i:i + n]), n, _ptr(ids[i:i + n]), T,
+                                                     _ptr(logits[i:i + n]), _stream(self.device)),
+                           self._h, "wcb_forward_enc")
+            return out(logits, enc)
+        x = self._features(input_features)
+        if x.shape[0] > 64:   # 64 clips per library call: split, concatenate
+            outs = [self.forward(x[i:i + 64], decoder_input_ids=ids[i:i + 64]) for i in range(0, x.shape[0], 64)]
+            return out(torch.cat([o.logits for o in outs]), torch.cat([o.encoder_last_hidden_state for o in outs]))
         B, T = ids.shape
         logits = torch.empty(B, T, self.dims.vocab, dtype=torch.float32, device=self.device)
         enc = torch.empty(B, self.dims.n_audio_ctx, self.dims.d_model, dtype=self.torch_dtype, device=self.device)
         _lib.check(self._lib.wcb_forward(self._h, _ptr(x), B, _ptr(ids), T, _ptr(logits), _ptr(enc),
                                          _stream(self.device)), self._h, "wcb_forward")
-        loss = None
-        if labels is not None:
-            from .loss import weighted_ce
-            loss = weighted_ce(logits, labels.to(self.device), bias_spans, self.bias_weight)
-        return Seq2SeqLMOutput(loss=loss, logits=logits, encoder_last_hidden_state=enc)
+        return out(logits, enc)
 
     __call__ = forward
 
