@@ -42,7 +42,7 @@ PEAK_F16_TFLOPS = 2500.0
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 ENC_GEMMS = ("enc_conv1", "enc_conv2", "enc_qkv", "enc_out", "enc_fc1", "enc_fc2")
-DEC_PROJ = ("dec_qkv", "dec_out", "dec_xq", "dec_kq", "dec_xqk", "dec_vg", "dec_xo", "dec_fc1", "dec_fc2", "lm_head")
+DEC_PROJ = ("dec_qkv", "dec_out", "dec_xq", "dec_kq", "dec_vg", "dec_xo", "dec_fc1", "dec_fc2", "lm_head")
 
 
 def log(*a):

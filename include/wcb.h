@@ -69,8 +69,10 @@ const char* wcb_last_error(const wcb_handle* h);
  *                      keeps W·diag(γ) copies of QKV / cross-q / fc1, ≈ +1/4 of the decoder weights), or its own
  *                      launch (0); before finalize
  *   "merge_v" 0/1      greedy encoder-space cross-attention: range merge and W_v fused (1) or two launches
- *   "xqk" 0/1          greedy encoder-space cross-attention query: LN + q_proj + W_k,hᵀ in one launch (1) or
- *                      two decode GEMMs (0, default: measured faster); bit-identical
+ *   "xq_kq" 0/1        greedy encoder-space cross-attention query (lean path): q'_h = W_k,hᵀ q_h computed inside
+ *                      the LN-fused q_proj launch (1, default) or as a launch of its own (0); bit-identical
+ *   "qkv_sa" 0/1       lean path, one position per row: the new token's self-attention inside the QKV launch
+ *                      (1, default) or as a launch of its own (0); bit-identical
  *   "lean" 0/1         decode projections of <= 64 rows (16-bit) on the lean single-tile kernel (1, default)
  *                      or the general decode GEMM (0); bit-identical. Before finalize: with it finalize keeps
  *                      fragment-major copies of the decoder projection weights and the token embedding (the

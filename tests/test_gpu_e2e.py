@@ -244,22 +244,24 @@ def test_broadcast_blob_views_load_without_host_copy():
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
-def test_fused_cross_query_is_bit_identical(dtype):
-    """Option xqk (1; default 0, measured slower): LN + q_proj + W_k,hᵀ as one launch (k_xenc.hip xq_kq_kernel) against the
-    two decode GEMMs it replaces (xqk 0): identical arithmetic, so identical ids even on the diverse
-    recipe, whose near-ties (gaps ~1e-3) flip on any rounding difference. 32 rows (one 32-row block)
-    and 13 rows (16-row blocks), 1000-phrase boost."""
+def test_fused_lean_launches_are_bit_identical(dtype):
+    """The lean decode path's in-launch fusions (gemm_impl.h dec_lean_kernel FZ): option xq_kq — q'_h =
+    W_k,hᵀ q_h inside the LN-fused q_proj launch — and option qkv_sa — the new token's self-attention inside
+    the QKV launch (common.h group_arrive_wait hand-offs) — against the separate launches they replace:
+    identical arithmetic, so identical ids even on the diverse recipe, whose near-ties (gaps ~1e-3) flip
+    on any rounding difference. 32 rows (32-row QKV blocks), 13 and 40 rows (16-row blocks, ragged),
+    1000-phrase boost."""
     dims = get_dims("small")
     sd = make_weights(dims, seed=0, recipe="diverse")
-    fused = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options={"xqk": 1})
-    plain = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options={"xqk": 0})
     phrases = synth_bias_list(1000, eot=dims.eos_token_id)
-    for B in (32, 13):
+    models = [WhisperCB.from_state_dict(dims, sd, dtype=dtype, options=o)
+              for o in ({"xq_kq": 1, "qkv_sa": 1}, {"xq_kq": 0, "qkv_sa": 0}, {"xq_kq": 1, "qkv_sa": 0})]
+    for B in (32, 13, 40):
         x = torch.from_numpy(W.log_mel(synth_batch(B, start=3), dims.n_mel))
         kw = dict(max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0)
-        a = fused.generate(x, **kw).cpu().numpy()
-        b = plain.generate(x, **kw).cpu().numpy()
-        np.testing.assert_array_equal(a, b)
+        out = [m.generate(x, **kw).cpu().numpy() for m in models]
+        for o in out[1:]:
+            np.testing.assert_array_equal(out[0], o)
 
 
 def test_bias_from_another_handle_is_rejected():

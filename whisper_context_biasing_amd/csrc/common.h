@@ -46,6 +46,56 @@ template <> struct DT<float> {
   WCB_DEV static float fromf(float f) { return f; }
 };
 
+// Cross-row lane exchanges without an LDS round trip: __shfl_xor(x, 16 | 32) lowers to
+// ds_bpermute_b32 (an LDS-unit instruction and an lgkmcnt wait); gfx950's v_permlane16_swap /
+// v_permlane32_swap swap rows in the VALU. (r[0], r[1]) at lane l = (x[l], x[l ^ 16]) in one order or
+// the other, and f32 add / max are commutative, so these equal x + __shfl_xor(x, 16) (etc.) bit for bit.
+WCB_DEV float xor16_add(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+WCB_DEV float xor32_add(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+WCB_DEV float xor16_max(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+WCB_DEV float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// In-launch hand-off between the workgroups of one group (MI355X_MICROARCH.md "Valid forms", row 1 of
+// the measured sc1 table; cdna_hip_programming.md §6 G16): the producers store the handed-off bytes
+// with sc1 (write-through) stores — st_sc1 — and call group_arrive_wait; it drains every wave's
+// stores (vmcnt(0)), joins the workgroup, lets one lane add to the group's counter (agent scope) and
+// poll it with sc1 loads until all n members of this generation arrived, then releases the other waves
+// at a second workgroup barrier. Readers load the bytes with sc1 loads only (ld_sc1). Counters are
+// monotonic (generation = the value an add returned / n) and zeroed between calls by the caller. The
+// spin is bounded (a co-residency failure cannot hang the GPU; results would then be wrong, which the
+// parity tests see).
+WCB_DEV void st_sc1(void* p, uint64_t v) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+WCB_DEV uint64_t ld_sc1(const void* p) {
+  return __hip_atomic_load(reinterpret_cast<uint64_t*>(const_cast<void*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+WCB_DEV void group_arrive_wait(int* cnt, int n) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int target = (old / n + 1) * n;
+    for (int spin = 0; spin < (1 << 22); ++spin) {
+      if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+
 // A8 bias boost (oracle/bias_ref.py): x + lam·units as one f32 product and one f32 add, never a
 // fused multiply-add, so every kernel rounds exactly like the oracle
 WCB_DEV float bias_bonus(float x, float lam, int units) { return __fadd_rn(x, __fmul_rn(lam, (float)units)); }
@@ -70,18 +120,33 @@ WCB_DEV typename DT<T>::frag load_frag(const T* p) {
 
 WCB_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
-WCB_DEV float wave_sum(float v) {
+WCB_DEV float wave_sum(float v) {   // xor 32, 16, 8, 4, 2, 1 (the row swaps in the VALU)
+  v = xor32_add(v);
+  v = xor16_add(v);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 WCB_DEV float wave_max(float v) {
+  v = xor32_max(v);
+  v = xor16_max(v);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
 
 // Store 8 consecutive f32 values as T.
+// load8f of bytes handed off inside the launch (group_arrive_wait): two 8-byte sc1 loads
+template <typename T> WCB_DEV void load8f_sc1(const T* src, float* v) {
+  static_assert(sizeof(T) == 2, "16-bit types");
+  const uint64_t w[2] = {ld_sc1(src), ld_sc1(src + 4)};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const unsigned short bits = (unsigned short)(w[j >> 2] >> (16 * (j & 3)));
+    if constexpr (__is_same(T, bf16_t)) v[j] = bf16_to_f(bits);
+    else v[j] = float(__builtin_bit_cast(f16_t, bits));
+  }
+}
 template <typename T> WCB_DEV void store8(T* dst, const float* v);
 template <> WCB_DEV void store8<bf16_t>(bf16_t* dst, const float* v) {
   s16x8 o;

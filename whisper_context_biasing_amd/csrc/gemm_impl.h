@@ -16,6 +16,7 @@
 #include <stdexcept>
 #include "common.h"
 #include "kernels.h"
+#include "self_attn.h"
 
 #include <algorithm>
 #include <cstdio>
@@ -884,8 +885,8 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
           s2 = fmaf(v, v, s2);
         }
       }
-      s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
-      s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
+      s1 = xor16_add(s1); s2 = xor16_add(s2);
+      s1 = xor32_add(s1); s2 = xor32_add(s2);
       if (lane < 16) rst[wave][i * 16 + lane] = float2{s1, s2};
     }
 #pragma unroll
@@ -1064,10 +1065,28 @@ template <typename T> struct DecLean {
   unsigned long long* stamp = nullptr;   // tools/dec_kernel_bench: per-workgroup phase stamps (null: off)
   int cfm_nw = 0, cfm_kpw = 0;           // EPI 0: out written fragment-major for a consumer with this split (0: rows)
   T* out2 = nullptr;                     // EPI 1: the 16-bit copy again, fragment-major with (cfm_nw, cfm_kpw)
+  // FZ 1 (EPI 2): the self-attention of the new token in the same launch — att [M][ld_att] (T) receives
+  // o_h; FZ 2 (EPI 0, the cross-attention query): q'_h = W_k,hᵀ q_h in the same launch — kq_w = W_kt's
+  // fragment-major copy ([H·D/16 tiles][2 waves][lane][8]), qp [M][ld_att] (T). sa_cnt: the arrival
+  // counters of the (row block, head) groups ([gridDim.y][kvH], monotonic)
+  T* att = nullptr; int ld_att = 0; int* sa_cnt = nullptr;
+  const T* kq_w = nullptr;
 };
 
-template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP, bool WFM = false, bool AFM = false>
+//   SA (EPI 2): the QKV launch also runs the self-attention of the new token. The 12 column tiles of a
+//   head (4 of q, 4 of k, 4 of v) store their tiles write-through (sc1), meet at the head's arrival
+//   counter (common.h group_arrive_wait: one dependent hand-off instead of a kernel boundary and a
+//   launch), and their waves then run self_attn_wave (self_attn.h, the stand-alone kernel's body, sc1
+//   loads) for one row each — bit-identical to the two launches.
+//   FZ 2 (EPI 0, LN: the cross-attention query q_h = LN(x) W_q,hᵀ + b_q): the 4 column tiles of a head store
+//   q_h write-through, meet at the head's counter, and each then computes a quarter of q'_h = W_k,hᵀ q_h
+//   (the grouped K = 64 product of the kq launch it replaces: the same two 32-deep MFMA halves summed in
+//   the same order, weights prefetched with the launch's first loads) — bit-identical to the two launches.
+template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP, bool WFM = false, bool AFM = false,
+          int FZ = 0>
 __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
+  constexpr bool SA = FZ == 1 && EPI == 2;
+  constexpr bool KQ = FZ == 2 && EPI == 0 && LN && !GELU && !GRP;
   using Frag = typename DT<T>::frag;
   constexpr int NT = NW * 64, K = NW * KPW * 32, R = MF * 16;
   static_assert(R * 4 <= NT, "epilogue: 4 columns per thread");
@@ -1124,6 +1143,21 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   if constexpr (EPI == 1) res4 = *reinterpret_cast<const f32x4*>(p.x + (long)erow * p.ldo + ecc);
   int pos = 0;
   if constexpr (EPI == 2) pos = __builtin_nontemporal_load(p.pos);
+  // KQ: this workgroup's share of q'_h = W_k,hᵀ q_h — K / 64 of the head's K / 16 column tiles, tile t of
+  // the share on wave t % NW — and their W_kt fragments (two 32-deep halves each), loaded with the burst
+  constexpr int KQT = KQ ? (K / 64 + NW - 1) / NW : 1;
+  Frag kqw[KQT][2];
+  if constexpr (KQ) {
+    const int hq = n0 >> 6, jq = (n0 >> 4) & 3;
+#pragma unroll
+    for (int t = 0; t < KQT; ++t) {
+      const int tt = min(wave + t * NW, K / 64 - 1);
+      const long ct = (long)hq * (K / 16) + jq * (K / 64) + tt;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+        kqw[t][kh] = __builtin_nontemporal_load(reinterpret_cast<const Frag*>(p.kq_w + ((ct * 2 + kh) * 64 + lane) * 8));
+    }
+  }
   __builtin_amdgcn_sched_barrier(0);
   unsigned long long t1 = 0, t2 = 0;
   if (p.stamp) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); t1 = stamp_now(); }
@@ -1145,8 +1179,8 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
           s2 = fmaf(v, v, s2);
         }
       }
-      s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
-      s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
+      s1 = xor16_add(s1); s2 = xor16_add(s2);
+      s1 = xor32_add(s1); s2 = xor32_add(s2);
       if (lane < 16) rst[wave][i * 16 + lane] = float2{s1, s2};
     }
     __syncthreads();
@@ -1180,9 +1214,10 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   __syncthreads();
   if (p.stamp) t2 = stamp_now();
   // ---------------- epilogue: 4 consecutive columns of one row per thread
-  if (er >= R) return;
   const int row = mb + er;
-  if (row >= p.M || ec >= p.N) return;
+  const bool live = er < R && row < p.M && ec < p.N;
+  if (!SA && !KQ && !live) return;   // (SA / KQ: every thread reaches the hand-off below)
+  if (live) {
   float v[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -1216,13 +1251,74 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
       const int n2 = ec - p.n_split, hh = n2 >> 6, dd = n2 & 63;
       const int kvs = hh / p.kvH, hd = hh % p.kvH;
       const long off = ((((long)kvs * p.kvB + row) * p.kvH + hd) * p.kvT + pos) * 64 + dd;
-      *reinterpret_cast<s4*>(p.kv + off) = hv;
+      if constexpr (SA) st_sc1(p.kv + off, __builtin_bit_cast(uint64_t, hv));
+      else *reinterpret_cast<s4*>(p.kv + off) = hv;
+    } else if (EPI == 2 && SA) {         // q of the new token, handed to the head's attention waves
+      st_sc1(p.out + (long)row * p.ldo + ec, __builtin_bit_cast(uint64_t, hv));
     } else if (EPI == 0 && p.cfm_nw) {   // fragment-major for the consumer's (waves, k-steps): 4 elements of one fragment
       const int kw = p.cfm_kpw * 32, w2 = ec / kw, ks2 = (ec % kw) >> 5, lg = (ec & 31) >> 3;
       const long off = ((((long)(row >> 4) * p.cfm_nw + w2) * p.cfm_kpw + ks2) * 64 + lg * 16 + (row & 15)) * 8 + (ec & 7);
       *reinterpret_cast<s4*>(p.out + off) = hv;
+    } else if constexpr (KQ) {           // q_h, handed to the head's W_k,hᵀ products
+      st_sc1(p.out + (long)row * p.ldo + ec, __builtin_bit_cast(uint64_t, hv));
     } else {
       *reinterpret_cast<s4*>(p.out + (long)row * p.ldo + ec) = hv;
+    }
+  }
+  }   // live
+  if constexpr (EPI == 2 && SA) {
+    // this tile's head and its index among the head's 12 tiles (q 0-3, k 4-7, v 8-11)
+    const int D = p.n_split;
+    int hg, j;
+    if (n0 < D) {
+      hg = n0 >> 6; j = (n0 >> 4) & 3;
+    } else {
+      const int hh = (n0 - D) >> 6;
+      hg = hh % p.kvH; j = 4 * (1 + hh / p.kvH) + (((n0 - D) >> 4) & 3);
+    }
+    group_arrive_wait(p.sa_cnt + blockIdx.y * p.kvH + hg, 12);
+    const int r = j * NW + wave;   // one row of the block per wave (12·NW >= R)
+    if (r < R && mb + r < p.M) {
+      const int b = mb + r;
+      const long kofs = (((long)b * p.kvH + hg) * p.kvT) * 64;
+      const long vofs = (long)p.kvB * p.kvH * p.kvT * 64;
+      self_attn_wave<T, true>(p.out + (long)b * p.ldo + hg * 64, p.kv + kofs, p.kv + vofs + kofs, p.kvT - 1,
+                              [&] { return pos + 1; }, p.att + (long)b * p.ld_att + hg * 64);
+    }
+  }
+  if constexpr (KQ) {
+    const int hq = n0 >> 6, jq = (n0 >> 4) & 3;
+    group_arrive_wait(p.sa_cnt + blockIdx.y * p.kvH + hq, 4);
+    // A = q_h rows of this block (lane: row lane & 15, k = 32·kh + 8·(lane >> 4)), sc1 loads
+    Frag qa[2];
+    {
+      const T* qr = p.out + (long)min(mb + (lane & 15), p.M - 1) * p.ldo + hq * 64 + 8 * (lane >> 4);
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const uint64_t w0 = ld_sc1(qr + kh * 32), w1 = ld_sc1(qr + kh * 32 + 4);
+        typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
+        qa[kh] = __builtin_bit_cast(Frag, u2{w0, w1});
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < KQT; ++t) {
+      const int tt = wave + t * NW;
+      if (tt < K / 64) {
+        const int c0 = jq * (K / 4) + tt * 16;   // first q'_h column of the tile
+        const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 a0 = mma16(qa[0], kqw[t][0], z), a1 = mma16(qa[1], kqw[t][1], z);
+        // C layout: lane holds rows 4·(lane >> 4) + e of column lane & 15; the kq launch's sum order
+        // ((0 + wave 0 half) + wave 1 half) + bias 0
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rr = mb + 4 * (lane >> 4) + e;
+          float sum = 0.f;
+          sum += a0[e];
+          sum += a1[e];
+          const float v = sum + 0.f;
+          if (rr < p.M) p.att[(long)rr * p.ld_att + hq * K + c0 + (lane & 15)] = DT<T>::fromf(v);
+        }
+      }
     }
   }
   if (p.stamp && tid == 0) {
@@ -1250,6 +1346,25 @@ static void launch_lean_k(const GemmArgs& g, hipStream_t s) {
   if (g.c_fm || g.out16_fm) lean_cfg(g.N, p.cfm_nw, p.cfm_kpw);   // the consumer's split of K = this N
   p.out2 = reinterpret_cast<T*>(g.out16_fm);
   const dim3 grid((g.N + 15) / 16, (g.M + MF * 16 - 1) / (MF * 16));
+  if constexpr (EPI == 2 && !GRP) {
+    if (g.sa_att) {   // QKV + the new token's self-attention in one launch (fragment-major weights)
+      if (!g.W_fm) throw std::runtime_error("internal error: fused QKV self-attention needs the fragment-major weights");
+      p.att = reinterpret_cast<T*>(g.sa_att); p.ld_att = g.sa_ld; p.sa_cnt = g.sa_cnt;
+      if (g.a_fm) WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, true, 1>), grid, dim3(NW * 64), 0, s, p);
+      else WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, false, 1>), grid, dim3(NW * 64), 0, s, p);
+      return;
+    }
+  }
+  if constexpr (EPI == 0 && LN && !GELU && !GRP) {
+    if (g.kq_w) {   // the cross-attention query and q'_h = W_k,hᵀ q_h in one launch (fragment-major weights)
+      if (!g.W_fm) throw std::runtime_error("internal error: fused cross-query needs the fragment-major weights");
+      p.att = reinterpret_cast<T*>(g.kq_out); p.ld_att = (int)g.kq_ld; p.sa_cnt = g.sa_cnt;
+      p.kq_w = reinterpret_cast<const T*>(g.kq_w); p.kvH = g.hs_H;
+      if (g.a_fm) WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, true, 2>), grid, dim3(NW * 64), 0, s, p);
+      else WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, false, 2>), grid, dim3(NW * 64), 0, s, p);
+      return;
+    }
+  }
   if (g.a_fm) {
     if constexpr (!GRP) WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, true>), grid, dim3(NW * 64), 0, s, p);
   } else if (g.W_fm) {
@@ -1344,8 +1459,8 @@ __global__ __launch_bounds__(NW * 64) void ln_rows_kernel(const T* __restrict__ 
       s2 = fmaf(v, v, s2);
     }
   }
-  s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
-  s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
+  s1 = xor16_add(s1); s2 = xor16_add(s2);
+  s1 = xor32_add(s1); s2 = xor32_add(s2);
   if (lane < 16) rst[wave][lane] = float2{s1, s2};
   __syncthreads();
   s1 = 0.f; s2 = 0.f;
@@ -1525,6 +1640,7 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
     // rows (measured C2: 1.074 vs 1.147 ms/token with 32-row workgroups); the LM head walks the
     // vocabulary persistently with 32-row workgroups, reading every weight tile once
     if (g.lean && launch_lean<T>(g, s)) return;
+    if (g.sa_att || g.kq_w) throw std::runtime_error("internal error: fused QKV self-attention / cross-query on a launch the lean kernel does not cover");
     if (g.a_fm || g.c_fm || g.out16_fm)   // the runtime pairs fragment-major operands only where the lean path takes both
       throw std::runtime_error("internal error: fragment-major operand on a launch the lean kernel does not cover");
     const bool mf1 = (g.M <= 64 && !(g.sel_val && g.M > 16)) || g.K >= 4096;

@@ -13,8 +13,11 @@
 //   decoder cross-attention over the precomputed encoder K/V, and the f32 "exact" encoder path).
 //   8 lanes per key (16 B of K and V each), one pass with an online softmax, optional split-KV
 //   over workgroups. HBM-bound on the K/V read.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
+#include "self_attn.h"
 
 namespace wcb {
 
@@ -76,8 +79,8 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(AttnArgs a) {
       mx = fmaxf(mx, sc[u]);
     }
     mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = xor16_max(mx);
+    mx = xor32_max(mx);
     const float mn = fmaxf(m, mx);           // finite: the first iteration has ≥ 1 valid key
     const float r = __expf(m - mn);          // 0 on the first iteration (m = −inf)
     m = mn;
@@ -94,13 +97,13 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(AttnArgs a) {
   }
   // reduce over the 8 lane groups (each group holds its own keys' p and p·v)
   l += __shfl_xor(l, 8, 64);
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
+  l = xor16_add(l);
+  l = xor32_add(l);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     o[e] += __shfl_xor(o[e], 8, 64);
-    o[e] += __shfl_xor(o[e], 16, 64);
-    o[e] += __shfl_xor(o[e], 32, 64);
+    o[e] = xor16_add(o[e]);
+    o[e] = xor32_add(o[e]);
   }
   if (kg == 0)
 #pragma unroll
@@ -254,8 +257,8 @@ __global__ __launch_bounds__(NW * 64) void attn_decode2p_kernel(AttnArgs a) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     o[e] += __shfl_xor(o[e], 8, 64);
-    o[e] += __shfl_xor(o[e], 16, 64);
-    o[e] += __shfl_xor(o[e], 32, 64);
+    o[e] = xor16_add(o[e]);
+    o[e] = xor32_add(o[e]);
   }
   __syncthreads();
   if (kg == 0)
@@ -401,8 +404,8 @@ __global__ __launch_bounds__(64) void attn_self_kernel(AttnArgs a) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     o[e] += __shfl_xor(o[e], 8, 64);
-    o[e] += __shfl_xor(o[e], 16, 64);
-    o[e] += __shfl_xor(o[e], 32, 64);
+    o[e] = xor16_add(o[e]);
+    o[e] = xor32_add(o[e]);
   }
   if (kg == 0) {
     float r[8];
@@ -428,68 +431,12 @@ template <typename T, int WPG = 1>
 __global__ __launch_bounds__(64 * WPG) void attn_self_lean_kernel(SelfLean a) {
   // WPG (row, head) pairs per workgroup, one per wave (pairs past the batch re-run the last one)
   const int pair = min(blockIdx.y * WPG + (int)(threadIdx.x >> 6), a.npairs - 1);
-  const int b = pair / a.H, h = pair % a.H, lane = threadIdx.x & 63;
-  const int seg = lane & 7, kg = lane >> 3;
-  const long base = (long)((a.row0 + b) / a.b_div) * a.k_sb + (long)h * a.k_sh + seg * 8;
-  const T* kb = reinterpret_cast<const T*>(a.k) + base;
-  const T* vb = reinterpret_cast<const T*>(a.v) + base;
-  const T* q = reinterpret_cast<const T*>(a.q) + (long)b * a.ldq + h * 64;
-  float qv[8], kv[8][8], vv[8][8];
-  load8f<T>(q + seg * 8, qv);
-#pragma unroll
-  for (int u = 0; u < 8; ++u) load8f<T>(kb + (long)min(u * 8 + kg, a.cap) * 64, kv[u]);
-#pragma unroll
-  for (int u = 0; u < 8; ++u) load8f<T>(vb + (long)min(u * 8 + kg, a.cap) * 64, vv[u]);
-  const int nk = __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(a.nkeys_dev)) + a.nkeys_add;
-  float m = -INFINITY, l = 0.f;
-  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int j0 = 0; j0 < nk; j0 += 64) {
-    if (j0) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) load8f<T>(kb + (long)min(min(j0 + u * 8 + kg, nk - 1), a.cap) * 64, kv[u]);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) load8f<T>(vb + (long)min(min(j0 + u * 8 + kg, nk - 1), a.cap) * 64, vv[u]);
-    }
-    float sc[8];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      float d = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) d = fmaf(qv[e], kv[u][e], d);
-#pragma unroll
-      for (int x = 1; x < 8; x <<= 1) d += __shfl_xor(d, x, 64);
-      sc[u] = (j0 + u * 8 + kg < nk) ? d : -INFINITY;
-      mx = fmaxf(mx, sc[u]);
-    }
-    const float mn = fmaxf(m, wave_max(mx));
-    const float r = __expf(m - mn);
-    l *= r;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] *= r;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const bool live = j0 + u * 8 + kg < nk;
-      const float p = live ? __expf(sc[u] - mn) : 0.f;
-      if (seg == 0) l += p;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = live ? fmaf(p, vv[u][e], o[e]) : o[e];
-    }
-    m = mn;
-  }
-  l = wave_sum(l);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    o[e] += __shfl_xor(o[e], 8, 64);
-    o[e] += __shfl_xor(o[e], 16, 64);
-    o[e] += __shfl_xor(o[e], 32, 64);
-  }
-  if (kg == 0) {
-    float r[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) r[e] = o[e] / l;
-    store8<T>(reinterpret_cast<T*>(a.o) + (long)b * a.ldo + h * 64 + seg * 8, r);
-  }
+  const int b = pair / a.H, h = pair % a.H;
+  const long base = (long)((a.row0 + b) / a.b_div) * a.k_sb + (long)h * a.k_sh;
+  self_attn_wave<T, false>(reinterpret_cast<const T*>(a.q) + (long)b * a.ldq + h * 64,
+                           reinterpret_cast<const T*>(a.k) + base, reinterpret_cast<const T*>(a.v) + base, a.cap,
+                           [&] { return __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(a.nkeys_dev)) + a.nkeys_add; },
+                           reinterpret_cast<T*>(a.o) + (long)b * a.ldo + h * 64);
 }
 
 template <typename T>
@@ -609,7 +556,11 @@ __global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnAr
   for (int p = 0; p < NS - 1; ++p)
     if (p < nt) stage(p, p);
   int st = 0;
-  for (int kt = 0; kt < nt; ++kt) {
+  // One K/V tile. TAIL: the tile reaches past the last key (only the very last tile can): its score
+  // masking lives in that instantiation alone — the compares and selects of a run-time `if` were
+  // hoisted by hipcc into every iteration (≈ 45 VALU / SALU instructions per query fragment per tile)
+  auto tile = [&](int kt, auto tail_tag) {
+    constexpr bool TAIL = decltype(tail_tag)::value;
     // tile kt landed (4 LDS-DMA per wave per tile; the younger tiles stay in flight), then the
     // barrier publishes every wave's part and frees the stage read in iteration kt - 1
     const int ahead = min(nt - 1 - kt, NS - 2);
@@ -631,7 +582,6 @@ __global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnAr
         kf[mf][ks] = *reinterpret_cast<const Frag*>(kt_l + swz(r, ks * 4 + (lane >> 4)));
       }
     const int kabs = (t_lo + kt) * 64;   // first key of this tile
-    const bool tail = kabs + 64 > S;
     // scores and softmax of every query fragment first, then P·V with the Vᵀ fragments of one
     // 16-row dd block live at a time (read once, used by every query fragment): 8 VGPRs of Vᵀ instead
     // of 32 keeps the kernel at 3 waves per SIMD
@@ -645,7 +595,7 @@ __global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnAr
         s[mf] = mma16(kf[mf][0], qf[qi][0], s[mf]);
         s[mf] = mma16(kf[mf][1], qf[qi][1], s[mf]);
       }
-      if (tail) {
+      if constexpr (TAIL) {
 #pragma unroll
         for (int mf = 0; mf < 4; ++mf)
 #pragma unroll
@@ -657,8 +607,8 @@ __global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnAr
       for (int mf = 0; mf < 4; ++mf)
 #pragma unroll
         for (int e = 0; e < 4; ++e) tmax = fmaxf(tmax, s[mf][e]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = xor16_max(tmax);
+      tmax = xor32_max(tmax);
       const float mnew = fmaxf(mrow[qi], tmax);
       const float alpha = __builtin_amdgcn_exp2f((mrow[qi] - mnew) * L2E);
       mrow[qi] = mnew;
@@ -686,13 +636,17 @@ __global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnAr
         o[qi][mf] = mma16(v1, pf[qi][1], o[qi][mf]);
       }
     }
-  }
+  };
+  // every tile but a partial last one without masking code, then that one (if any)
+  const int nt_full = nt > 0 && (t_lo + nt) * 64 > S ? nt - 1 : nt;   // (an empty key range: no tile)
+  for (int kt = 0; kt < nt_full; ++kt) tile(kt, std::false_type{});
+  if (nt_full < nt) tile(nt_full, std::true_type{});
   // epilogue: lane holds Oᵀ[dd = 16mf + 4(lane>>4) + e][q = lane&15]
 #pragma unroll
   for (int qi = 0; qi < QW; ++qi) {
     float l = lrow[qi];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    l = xor16_add(l);
+    l = xor32_add(l);
     const float inv = 1.f / l;
     const int qr = q0 + qi * 16 + (lane & 15);
     if (qr >= a.Sq) continue;
@@ -826,8 +780,8 @@ __global__ __launch_bounds__(NWV * 64) void attn_beam_kernel(AttnArgs a) {
     for (int mf = 0; mf < 4; ++mf)
 #pragma unroll
       for (int e = 0; e < 4; ++e) tmax = fmaxf(tmax, sc[mf][e]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    tmax = xor16_max(tmax);
+    tmax = xor32_max(tmax);
     const float mnew = fmaxf(mrow, tmax);
     const float alpha = __builtin_amdgcn_exp2f((mrow - mnew) * L2E);
     mrow = mnew;
@@ -850,8 +804,8 @@ __global__ __launch_bounds__(NWV * 64) void attn_beam_kernel(AttnArgs a) {
     }
   }
   // ---- merge the waves' partials (wave order): lane holds Oᵀ[dd = 16mf + 4(lane>>4) + e][q = lane&15]
-  lrow += __shfl_xor(lrow, 16, 64);
-  lrow += __shfl_xor(lrow, 32, 64);
+  lrow = xor16_add(lrow);
+  lrow = xor32_add(lrow);
   __syncthreads();                                     // every wave is done with its ring: reuse it
   f32x4* ob = reinterpret_cast<f32x4*>(lds_dyn);       // [NWV][4][64]
   float2* ml = reinterpret_cast<float2*>(lds_dyn + NWV * 4 * 64 * 16);   // [NWV][16]

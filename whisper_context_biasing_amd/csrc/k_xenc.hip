@@ -183,8 +183,8 @@ __global__ __launch_bounds__(512) void attn_xenc_kernel(XencArgs a) {
       }
     }
     float cm = fmaxf(fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s0[2], s0[3])), fmaxf(fmaxf(s1[0], s1[1]), fmaxf(s1[2], s1[3])));
-    cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
-    cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+    cm = xor16_max(cm);
+    cm = xor32_max(cm);
     const float mnew = fmaxf(m_run, cm);            // finite: every chunk holds >= 1 key of the range
     const float alpha = __builtin_amdgcn_exp2f((m_run - mnew) * L2E);
     m_run = mnew;
@@ -208,8 +208,8 @@ __global__ __launch_bounds__(512) void attn_xenc_kernel(XencArgs a) {
     }
   }
   // ---- range partials: lane holds Uᵀ[c0 + 4(lane>>4) + e][head lane&15]
-  l_run += __shfl_xor(l_run, 16, 64);
-  l_run += __shfl_xor(l_run, 32, 64);
+  l_run = xor16_add(l_run);
+  l_run = xor32_add(l_run);
   if (hq < a.H) {
     const long slot = ((long)b * a.nsplit + split) * a.H + hq;
     float* pp = a.part + slot * D + 4 * (lane >> 4);
@@ -328,8 +328,8 @@ __global__ __launch_bounds__((XregCfg<D, WNW>::NW * 64), ((NR == 2 && WNW == 4) 
       }
     }
     float cm = fmaxf(fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s0[2], s0[3])), fmaxf(fmaxf(s1[0], s1[1]), fmaxf(s1[2], s1[3])));
-    cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
-    cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+    cm = xor16_max(cm);
+    cm = xor32_max(cm);
     const float mnew = fmaxf(m_run, cm);
     const float alpha = __builtin_amdgcn_exp2f((m_run - mnew) * L2E);
     m_run = mnew;
@@ -378,8 +378,8 @@ __global__ __launch_bounds__((XregCfg<D, WNW>::NW * 64), ((NR == 2 && WNW == 4) 
     }
   }
   // ---- range partials: lane holds Uᵀ[cw0 + 16t + 4(lane>>4) + e][head lane&15]
-  l_run += __shfl_xor(l_run, 16, 64);
-  l_run += __shfl_xor(l_run, 32, 64);
+  l_run = xor16_add(l_run);
+  l_run = xor32_add(l_run);
   if (hq < a.H) {
     const long slot = ((long)b * a.nsplit + split) * a.H + hq;
     float* pp = a.part + slot * D + cw0 + 4 * (lane >> 4);
@@ -529,184 +529,6 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
       }
     }
   }
-}
-
-// xq_kq_kernel: workgroup = (column block cb of CB columns of q'_h, head h, row block of 16·MF rows),
-// 8 waves = 4 K slices x 2 column pairs. Phase 1 is the LN-fused q_proj decode GEMM of gemm_dec_kernel
-// (AM = 2) restricted to the head's 64 columns, with its exact arithmetic: the K range split into the
-// same 4 slices (KPW 32-deep steps each, the decode-GEMM table for K = D), row statistics from the
-// loaded 16-bit residual copy (per-slice partials summed in slice order), γ/β through LDS, slice
-// partials summed in slice order, + b_q, rounded to T. Phase 2 is the grouped W_k,hᵀ product of the
-// decode GEMM with K = 64 (two 32-deep MFMA steps summed after the fact, as its two waves do). Every
-// load of the launch (the head's W_q rows, the W_kt block, the residual rows, LN parameters, b_q) is
-// issued up front; the head's 98 KB of W_q rows are spread over 8 waves (loads in flight) and read by
-// the D/CB workgroups of that head (L2 / Infinity Cache after the first): redundant reads bought with
-// one dependent launch fewer per decoder layer.
-template <typename T, int D, int MF>
-__global__ __launch_bounds__(512) void xq_kq_kernel(XqkArgs a) {
-  using Frag = typename DT<T>::frag;
-  constexpr int NS = 4, KPW = D / 128, R = MF * 16, CB = 64, NT = 512;
-  __shared__ __attribute__((aligned(16))) float red[NS][R][65];
-  __shared__ __attribute__((aligned(16))) float lnp[2 * D];
-  __shared__ float2 rst[NS][R];
-  __shared__ __attribute__((aligned(16))) T qh[R][64 + 8];     // q_h rows (T), the phase-2 A operand
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ks_w = wave & 3, jp = wave >> 2;                     // K slice, column pair (frags 2jp, 2jp+1)
-  const int cb = blockIdx.x, h = blockIdx.y, mb = blockIdx.z * R;
-  const int kb = ks_w * (KPW * 32) + 8 * (lane >> 4);
-  // ---- every load of the launch
-  Frag w[2][KPW];                                   // W_q rows h·64 + 16(2jp + j) + (lane & 15)
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const T* W = reinterpret_cast<const T*>(a.wq) + (long)(h * 64 + (2 * jp + j) * 16 + (lane & 15)) * D + kb;
-#pragma unroll
-    for (int ks = 0; ks < KPW; ++ks) w[j][ks] = load_frag<T>(W + ks * 32);   // default policy: re-read by the head's D/64 workgroups
-  }
-  Frag wk[2];                                       // waves 0-3: W_kt[h][cb·CB + 16·wave + (lane & 15)][k]
-  {
-    const T* Wk = reinterpret_cast<const T*>(a.wkt) + ((long)h * D + cb * CB + ks_w * 16 + (lane & 15)) * 64 + 8 * (lane >> 4);
-    wk[0] = load_frag<T>(Wk);
-    wk[1] = load_frag<T>(Wk + 32);
-  }
-  Frag x[MF][KPW];
-#pragma unroll
-  for (int i = 0; i < MF; ++i) {
-    const int m = min(mb + i * 16 + (lane & 15), a.M - 1);
-    const T* xr = reinterpret_cast<const T*>(a.x16) + (long)m * D + kb;
-#pragma unroll
-    for (int ks = 0; ks < KPW; ++ks) x[i][ks] = load_frag<T>(xr + ks * 32);
-  }
-  constexpr int LQ = (2 * D / 4 + NT - 1) / NT;
-  f32x4 lq[LQ];
-#pragma unroll
-  for (int j = 0; j < LQ; ++j) {
-    const int c = (j * NT + tid) * 4;
-    lq[j] = c < 2 * D ? *reinterpret_cast<const f32x4*>((c < D ? a.ln_w : a.ln_b) + (c < D ? c : c - D))
-                      : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  constexpr int EP = (R * 64 + NT - 1) / NT;        // phase-1 outputs per thread
-  float pf_bias[EP];
-#pragma unroll
-  for (int it = 0; it < EP; ++it) pf_bias[it] = a.bq[h * 64 + ((it * NT + tid) & 63)];
-  __builtin_amdgcn_sched_barrier(0);
-  // ---- LayerNorm of the rows (gemm_dec_kernel AM = 2 arithmetic; slice partials from the jp = 0 waves)
-  auto xval = [&](int i, int ks, int e) -> float {
-    if constexpr (__is_same(T, bf16_t)) return bf16_to_f((bf16_t)x[i][ks][e]);
-    else return float(x[i][ks][e]);
-  };
-  if (jp == 0) {
-#pragma unroll
-    for (int i = 0; i < MF; ++i) {
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < KPW; ++ks)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float v = xval(i, ks, e);
-          s1 += v;
-          s2 = fmaf(v, v, s2);
-        }
-      s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
-      s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
-      if (lane < 16) rst[ks_w][i * 16 + lane] = float2{s1, s2};
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < LQ; ++j) {
-    const int c = (j * NT + tid) * 4;
-    if (c < 2 * D) *reinterpret_cast<f32x4*>(lnp + c) = lq[j];
-  }
-  __syncthreads();
-  f32x4 acc[MF][2];
-#pragma unroll
-  for (int i = 0; i < MF; ++i) {
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < NS; ++ww) { const float2 t = rst[ww][i * 16 + (lane & 15)]; s1 += t.x; s2 += t.y; }
-    const float mean = s1 / D;
-    const float rstd = rsqrtf(fmaxf(s2 / D - mean * mean, 0.f) + 1e-5f);
-    acc[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < KPW; ++ks) {
-      const f32x4 w0 = *reinterpret_cast<const f32x4*>(lnp + kb + ks * 32);
-      const f32x4 w1 = *reinterpret_cast<const f32x4*>(lnp + kb + ks * 32 + 4);
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(lnp + D + kb + ks * 32);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(lnp + D + kb + ks * 32 + 4);
-      Frag af;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float gw = e < 4 ? w0[e] : w1[e - 4], gb = e < 4 ? b0[e] : b1[e - 4];
-        const float v = (xval(i, ks, e) - mean) * rstd * gw + gb;
-        af[e] = __builtin_bit_cast(typename std::remove_reference<decltype(af[0])>::type, DT<T>::fromf(v));
-      }
-      acc[i][0] = mma16(af, w[0][ks], acc[i][0]);
-      acc[i][1] = mma16(af, w[1][ks], acc[i][1]);
-    }
-  }
-  // ---- slice partials → LDS, summed in slice order + b_q, rounded to T: q_h
-#pragma unroll
-  for (int i = 0; i < MF; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        red[ks_w][i * 16 + (lane >> 4) * 4 + e][(2 * jp + j) * 16 + (lane & 15)] = acc[i][j][e];
-  __syncthreads();
-#pragma unroll
-  for (int it = 0; it < EP; ++it) {
-    const int o = it * NT + tid;
-    if (o < R * 64) {
-      const int r = o >> 6, c = o & 63;
-      float v = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < NS; ++ww) v += red[ww][r][c];
-      qh[r][c] = DT<T>::fromf(v + pf_bias[it]);
-    }
-  }
-  __syncthreads();
-  if (wave >= 4) return;
-  // ---- phase 2: q'_h[m][c] = Σ_i q_h[m][i] W_kt[h][c][i], wave → 16 columns of the block
-#pragma unroll
-  for (int i = 0; i < MF; ++i) {
-    const Frag a0 = *reinterpret_cast<const Frag*>(&qh[i * 16 + (lane & 15)][8 * (lane >> 4)]);
-    const Frag a1 = *reinterpret_cast<const Frag*>(&qh[i * 16 + (lane & 15)][32 + 8 * (lane >> 4)]);
-    const f32x4 p0 = mma16(a0, wk[0], f32x4{0.f, 0.f, 0.f, 0.f});
-    const f32x4 p1 = mma16(a1, wk[1], f32x4{0.f, 0.f, 0.f, 0.f});
-    const int c = cb * CB + wave * 16 + (lane & 15);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int m = mb + i * 16 + (lane >> 4) * 4 + e;
-      if (m < a.M) reinterpret_cast<T*>(a.qp)[((long)m * a.H + h) * D + c] = DT<T>::fromf(p0[e] + p1[e]);
-    }
-  }
-}
-
-bool xqk_supported(DType t, int D) {
-  return (t == kBF16 || t == kF16) && (D == 384 || D == 512 || D == 768 || D == 1024);
-}
-
-template <typename T, int D>
-static void launch_xqk(const XqkArgs& a, hipStream_t s) {
-  // 16 rows per workgroup up to 16 rows, else 32 (more rows per W_q read; C2's 32 rows: one row block)
-  if (a.M <= 16) WCB_LAUNCH((xq_kq_kernel<T, D, 1>), dim3(D / 64, a.H, 1), dim3(512), 0, s, a);
-  else WCB_LAUNCH((xq_kq_kernel<T, D, 2>), dim3(D / 64, a.H, (a.M + 31) / 32), dim3(512), 0, s, a);
-}
-
-template <typename T>
-static void launch_xqk_t(const XqkArgs& a, hipStream_t s) {
-  switch (a.D) {
-    case 384: launch_xqk<T, 384>(a, s); break;
-    case 512: launch_xqk<T, 512>(a, s); break;
-    case 768: launch_xqk<T, 768>(a, s); break;
-    case 1024: launch_xqk<T, 1024>(a, s); break;
-    default: break;
-  }
-}
-
-void xq_kq(DType t, const XqkArgs& a, hipStream_t s) {
-  if (t == kBF16) launch_xqk_t<bf16_t>(a, s);
-  else if (t == kF16) launch_xqk_t<f16_t>(a, s);
 }
 
 bool xenc_supported(DType t, int D) {

@@ -106,6 +106,14 @@ struct GemmArgs {
   // LDS-ring tiles (encoder GEMMs): tile order in bands of `raster` row panels, column tiles outer
   // within a band (0: row-major tile order)
   int raster = 0;
+  // lean QKV (mode 2, one position per row): the new token's self-attention in the same launch
+  // (gemm_impl.h dec_lean_kernel SA): o_h → sa_att [M][sa_ld]; sa_cnt = the launch's arrival counters
+  // ([row blocks][hs_H] ints, zeroed once at allocation, monotonic). Set only where the lean kernel takes
+  // the launch (gemm() throws otherwise).
+  void* sa_att = nullptr; int sa_ld = 0; int* sa_cnt = nullptr;
+  // lean LN-fused cross-attention query (EPI 0): q'_h = W_k,hᵀ q_h in the same launch (kq_w = W_kt's
+  // fragment-major copy, kq_out [M][kq_ld] = [M][H·d], arrival counters in sa_cnt, heads in hs_H)
+  const void* kq_w = nullptr; void* kq_out = nullptr; long kq_ld = 0;
 };
 
 void gemm(DType t, const GemmArgs& g, hipStream_t s);
@@ -185,19 +193,6 @@ void xenc_attention(DType t, const XencArgs& a, hipStream_t s);
 void xenc_merge(DType t, const XencArgs& a, void* u, long ldu, hipStream_t s);
 // merge + value projection fused (D % 128 == 0): o[row][h·64 + j] = W_v,h·u_h + b_v, T
 void xenc_merge_v(DType t, const XencArgs& a, const void* wv, const float* bv, void* o, long ldo, hipStream_t s);
-// The cross-attention query of the encoder-space formulation in ONE launch (replaces the LN-fused
-// q_proj decode GEMM + the grouped W_k,hᵀ GEMM): q_h = LN(x) W_q,hᵀ + b_q,h rounded to T (bit-identical
-// to the two-launch path), then q'_h[c] = Σ_i W_kt[h][c][i] q_h[i] for this workgroup's block of c.
-struct XqkArgs {
-  const void* x16 = nullptr;                    // [M][D] T copy of the residual stream (LayerNorm input)
-  const float* ln_w = nullptr; const float* ln_b = nullptr;
-  const void* wq = nullptr; const float* bq = nullptr;   // [D][D] (pre-scaled q_proj), [D]
-  const void* wkt = nullptr;                    // [H][D][64]
-  void* qp = nullptr;                           // [M][H][D] T
-  int M = 0, H = 0, D = 0;
-};
-bool xqk_supported(DType t, int D);
-void xq_kq(DType t, const XqkArgs& a, hipStream_t s);
 
 // log-mel front end
 void logmel_power_mel(const float* pcm, long pcm_stride, int n_samples, int B, const float* dft,

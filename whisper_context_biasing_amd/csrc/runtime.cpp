@@ -128,6 +128,7 @@ struct DecCtx {
   int dec_B = 0, dec_T = 0;
   DevBuf kvself, dx, dx16, dx16fm, dh, dq, dqp, du, datt, dffn, dstats, drst, xpart, xml, xticket, logits, part_val, part_idx, ints,
       pids, outbuf, forced, beam;
+  DevBuf sa_cnt;   // arrival counters of the fused lean launches [L][kMaxSub][QKV+SA | xq+kq][4][H] (monotonic)
   int nchunk = 64;
   hipGraphExec_t gexec = nullptr;               // captured decode step
   hipGraphExec_t gexec_k = nullptr;             // steps_per_graph consecutive decode steps in one graph
@@ -179,9 +180,10 @@ struct wcb_handle {
   // greedy cross-attention (encoder space): range merge and W_v in one launch (option "merge_v";
   // C2 16,570 vs 16,259 audio-s/s for the two launches)
   int merge_v = 1;
-  // greedy cross-attention query (<= 64 rows, encoder space): LN + q_proj + W_k,hᵀ as one launch
-  // (option "xqk"; 0 = the two decode GEMMs, bit-identical)
-  int xqk = 0;   // measured slower fused (round 2, C2 decode alone); kept as a bit-identity check
+  // greedy cross-attention query (<= 64 rows, encoder space, lean path): q'_h = W_k,hᵀ q_h inside the
+  // LN-fused q_proj launch (option "xq_kq"; gemm_impl.h dec_lean_kernel FZ 2; 0 = two launches,
+  // bit-identical)
+  int xq_kq = 1;
   // decode rows > 64: 64-deep K sub-tiles per ring stage of the 64x32 / 32x32 tiles (option "ring_kt",
   // 1 or 2; C5 1,594 -> 1,644 audio-s/s)
   int ring_kt = 2;
@@ -215,6 +217,9 @@ struct wcb_handle {
   // lean path: the residual writers (embedding, out / xo / fc2 projections) also write the 16-bit rows
   // fragment-major for the LayerNorm-fused consumers (QKV, xq, fc1); option "lean_x"
   int lean_x = 1;
+  // lean path, one position per row: the new token's self-attention inside the QKV launch (option
+  // "qkv_sa"; gemm_impl.h dec_lean_kernel SA; bit-identical to the two launches)
+  int qkv_sa = 1;
   struct wcb_state* step_state = nullptr;   // the active step-wise decode (wcb_decode_begin), if any
   // encoder GEMM tile order (option "enc_raster"): bands of n row panels with the column tiles outer
   // (GemmArgs::raster; 0 = row-major). 8 measured best with the round-3 ring kernel (whisper-small:
@@ -499,7 +504,7 @@ void wcb_destroy(wcb_handle* h) {
     if (D.gexec) (void)hipGraphExecDestroy(D.gexec);
     if (D.gexec_k) (void)hipGraphExecDestroy(D.gexec_k);
     for (DevBuf* b : {&D.kvself, &D.dx, &D.dx16, &D.dx16fm, &D.dh, &D.dq, &D.dqp, &D.du, &D.datt, &D.dffn, &D.dstats, &D.drst, &D.xpart, &D.xml, &D.xticket,
-                      &D.logits, &D.part_val, &D.part_idx, &D.ints, &D.outbuf, &D.forced, &D.beam})
+                      &D.logits, &D.part_val, &D.part_idx, &D.ints, &D.outbuf, &D.forced, &D.beam, &D.sa_cnt})
       b->release();
     if (D.ev_fork) (void)hipEventDestroy(D.ev_fork);
     for (hipEvent_t e : D.ev_poll)
@@ -565,8 +570,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "ring_kt") {
       REQUIRE(value == 1 || value == 2, "option ring_kt: 1 or 2");
       h->ring_kt = value;
-    } else if (n == "xqk") {
-      h->xqk = value != 0;
+    } else if (n == "xq_kq") {
+      h->xq_kq = value != 0;
     } else if (n == "enc_raster") {
       REQUIRE(value >= 0 && value <= 64, "option enc_raster: 0..64");
       h->enc_raster = value;
@@ -576,6 +581,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       h->lean = value != 0;
     } else if (n == "lean_x") {
       h->lean_x = value != 0;
+    } else if (n == "qkv_sa") {
+      h->qkv_sa = value != 0;
     } else if (n == "merge_v") {
       h->merge_v = value != 0;
     } else if (n == "ln_fold") {
@@ -996,6 +1003,7 @@ void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode
     D.dqp.ensure((size_t)rows * h->H() * d * e);
     D.du.ensure((size_t)rows * h->H() * d * e);
     D.xticket.ensure((size_t)rows * h->H() * 4);     // zeroed on allocation; combiners reset their slot
+    D.sa_cnt.ensure((size_t)L * DecCtx::kMaxSub * 2 * 4 * h->H() * 4);   // zeroed on allocation, monotonic
     D.pids.ensure((size_t)rows * 4);
     D.logits.ensure((size_t)B * h->vocab_pad * 4);
     D.nchunk = lm_head_partials(h->dt, (int)d, h->d.vocab);   // argmax partials per row of the LM head
@@ -1126,6 +1134,14 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
     q.kv_rps = rps; q.ln_u = w.ln1_u; q.ln_c = w.ln1_c; q.ln_wg = w.qkv_wg; q.W_fm = w.qkv_fm;
     if (x16fm) { q.ln_a16 = x16fm; q.a_fm = 1; }
+    // the new token's self-attention in the QKV launch: one position per row on the lean kernel with
+    // the fragment-major weights (the conditions under which launch_lean takes this launch)
+    const bool sa = h->qkv_sa && h->lean && fm_ok && rps == 1 && w.qkv_fm && !c.phys &&
+                    (d == 512 || d == 768 || d == 1024 || d == 1280);   // launch_lean's LayerNorm table
+    if (sa) {
+      q.sa_att = datt; q.sa_ld = d;
+      q.sa_cnt = D.sa_cnt.as<int>() + (((size_t)l * DecCtx::kMaxSub + chain) * 2 + 0) * 4 * H;
+    }
     proj("dec_qkv", q);
     AttnArgs a;
     a.q = dq; a.ldq = d; a.q_Sb = rps; a.Sq = rps; a.causal = rps > 1;
@@ -1135,7 +1151,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     a.row0 = b0; a.phys = c.phys; a.phys_ld = T;
     a.o = datt; a.ldo = d; a.o_Sb = rps; a.B = nb; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1;
     a.kv_rows = rps == 1 ? T : 0;
-    {
+    if (!sa) {
       const double t_keys = c.host_pos >= 0 ? c.host_pos + 1 : 0;   // keys this step (eager pass)
       h->timed("dec_self_attn", 4.0 * nb * H * t_keys * 64, nb * H * t_keys * 128.0 * e, st_,
                [&] { attention_decode(h->dt, a, st_); });
@@ -1148,19 +1164,18 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       // cross attention in encoder space: q'_h = W_k,hᵀ q_h (block-diagonal GEMM, K = 64), one pass
       // over the encoder output per layer for all heads, range combine + W_v,h + b_v
       char* dqp = (char*)D.dqp.p + (size_t)r0 * H * d * e;
-      if (!tiled && lna && h->xqk && xqk_supported(h->dt, d)) {
-        // LN + q_proj + W_k,hᵀ in one launch (bit-identical to the two decode GEMMs below)
-        XqkArgs qa;
-        qa.x16 = lna; qa.ln_w = w.lnx_w; qa.ln_b = w.lnx_b; qa.wq = w.xq_w; qa.bq = w.xq_b; qa.wkt = w.xkt_w;
-        qa.qp = dqp; qa.M = M; qa.H = H; qa.D = d;
-        h->timed("dec_xqk", 2.0 * M * d * d * 2, (2.0 * d * d * 2 + (double)M * d * (1 + H)) * e, st_,
-                 [&] { xq_kq(h->dt, qa, st_); });
-      } else {
-        GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
-        xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
-        xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg; xq.W_fm = w.xq_fm;
-        if (x16fm) { xq.ln_a16 = x16fm; xq.a_fm = 1; }
-        proj("dec_xq", xq);
+      GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
+      xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
+      xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg; xq.W_fm = w.xq_fm;
+      if (x16fm) { xq.ln_a16 = x16fm; xq.a_fm = 1; }
+      // q'_h = W_k,hᵀ q_h in the q_proj launch: the lean LN table's widths, both fragment-major copies
+      const bool kqf = h->xq_kq && h->lean && fm_ok && w.xq_fm && w.xkt_fm && (d == 512 || d == 768 || d == 1024 || d == 1280);
+      if (kqf) {
+        xq.kq_w = w.xkt_fm; xq.kq_out = dqp; xq.kq_ld = (long)H * d; xq.hs_H = H;
+        xq.sa_cnt = D.sa_cnt.as<int>() + (((size_t)l * DecCtx::kMaxSub + chain) * 2 + 1) * 4 * H;
+      }
+      proj("dec_xq", xq);
+      if (!kqf) {
         GemmArgs kq = drow(dq, d, w.xkt_w, M, H * d, 64, dqp, (long)H * d);
         kq.a_grp_n = d; kq.a_grp_off = 64; kq.W_fm = w.xkt_fm;
         proj("dec_kq", kq);
