@@ -30,7 +30,12 @@ def main():
     ap.add_argument("--concurrent", type=int, default=0,
                     help="also time this many overlapping async calls of --long tokens (decode contexts in flight)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE", help="wcb_set_option")
+    ap.add_argument("--side-stream", action="store_true",
+                    help="issue every call from a non-default torch stream (CU-masked decode streams are "
+                         "blocking streams: work on the legacy null stream would serialise them)")
     a = ap.parse_args()
+    if a.side_stream:
+        torch.cuda.set_stream(torch.cuda.Stream())
     dims = get_dims(a.model)
     opts = {k: int(v) for k, v in (o.split("=", 1) for o in a.opt)}
     m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=0), dtype=a.dtype, options=opts or None)

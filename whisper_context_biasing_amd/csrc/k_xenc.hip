@@ -26,6 +26,7 @@
 // xenc_merge_kernel: workgroup = (head, row): merges the ranges (fixed order: deterministic) and
 //   normalises: u[row][h] = Σ_j p_j,h e_j in the model dtype. W_v,h and b_v are then one block-diagonal
 //   skinny GEMM (gemm_impl.h, grouped A), whose output feeds the out-projection GEMM.
+#include <algorithm>
 #include <type_traits>
 
 #include "common.h"
@@ -249,7 +250,9 @@ template <int D, int WNW = 4> struct XregCfg {
 };
 
 // NR = chunks in flight per wave (register ring depth): 2 (two workgroups per CU) or 3 (one).
-template <typename T, int D, int NR, int WNW = 4>
+// FM: the encoder output in the fragment-major chunk layout of xenc_fm_kernel (below): every load
+// wave-instruction reads 1 KiB contiguous, where the row layout touches 16 key rows x 64 B.
+template <typename T, int D, int NR, int WNW = 4, bool FM = false>
 __global__ __launch_bounds__((XregCfg<D, WNW>::NW * 64), ((NR == 2 && WNW == 4) ? 2 : 1)) void attn_xenc_reg_kernel(XencArgs a) {
   using Frag = typename DT<T>::frag;
   using C = XregCfg<D, WNW>;
@@ -274,13 +277,24 @@ __global__ __launch_bounds__((XregCfg<D, WNW>::NW * 64), ((NR == 2 && WNW == 4) 
     for (int i = 0; i < KSW; ++i) qf[i] = hq < a.H ? load_frag<T>(qrow + i * 32) : Frag{};
   }
   auto load_chunk = [&](Frag (&f)[2][KSW], int c) {
-    const int key0 = k_lo + c * CK + (lane & 15);   // past the range: re-read its last key (L2)
-    const T* r0 = E + (long)min(key0, k_hi - 1) * D;
-    const T* r1 = E + (long)min(key0 + 16, k_hi - 1) * D;
+    if constexpr (FM) {   // chunk g of the clip: [g][wave][half][ks][lane][8] (past the range: its last chunk)
+      const int g = min((k_lo + c * CK) / CK, (k_hi - 1) / CK);
+      const T* cb = reinterpret_cast<const T*>(a.enc) + (long)((a.row0 + b) / a.rows_per_enc) * a.enc_sb +
+                    (((long)g * NW + wave) * 2 * KSW * 64 + lane) * 8;
 #pragma unroll
-    for (int ks = 0; ks < KSW; ++ks) {
-      f[0][ks] = load_frag<T>(r0 + ks * 32);
-      f[1][ks] = load_frag<T>(r1 + ks * 32);
+      for (int ks = 0; ks < KSW; ++ks) {
+        f[0][ks] = load_frag<T>(cb + ks * 512);
+        f[1][ks] = load_frag<T>(cb + (KSW + ks) * 512);
+      }
+    } else {
+      const int key0 = k_lo + c * CK + (lane & 15);   // past the range: re-read its last key (L2)
+      const T* r0 = E + (long)min(key0, k_hi - 1) * D;
+      const T* r1 = E + (long)min(key0 + 16, k_hi - 1) * D;
+#pragma unroll
+      for (int ks = 0; ks < KSW; ++ks) {
+        f[0][ks] = load_frag<T>(r0 + ks * 32);
+        f[1][ks] = load_frag<T>(r1 + ks * 32);
+      }
     }
   };
 
@@ -531,6 +545,47 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
   }
 }
 
+// The encoder output [B][S][D] → the fragment-major chunk layout of attn_xenc_reg_kernel<.., FM>:
+// [B][ceil(S/32) chunks][NW waves][2 halves][KSW k-steps][64 lanes][8], element (lane, e) of (chunk g,
+// wave w, half h, k-step ks) = enc[b][32g + 16h + (lane & 15)][w·CW + 32ks + 8(lane >> 4) + e] (zero
+// past S): the lane layout of the kernel's row loads, stored so one wave-instruction reads 1 KiB.
+template <typename T, int D>
+__global__ __launch_bounds__(256) void xenc_fm_kernel(const T* __restrict__ src, T* __restrict__ dst, int S, long n16) {
+  using C = XregCfg<D>;
+  constexpr int NW = C::NW, KSW = C::KSW, CW = C::CW;
+  const int nchunk = (S + kXencCK - 1) / kXencCK;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (long)gridDim.x * blockDim.x) {
+    long r = i;
+    const int lane = (int)(r % 64); r /= 64;
+    const int ks = (int)(r % KSW); r /= KSW;
+    const int hf = (int)(r % 2); r /= 2;
+    const int w = (int)(r % NW); r /= NW;
+    const int g = (int)(r % nchunk);
+    const long clip = r / nchunk;
+    const int key = g * kXencCK + hf * 16 + (lane & 15);
+    const int col = w * CW + 8 * (lane >> 4) + 32 * ks;
+    s16x8 v = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (key < S) v = *reinterpret_cast<const s16x8*>(src + (clip * S + key) * D + col);
+    *reinterpret_cast<s16x8*>(dst + i * 8) = v;
+  }
+}
+
+long xenc_fm_elems(int B, int S, int D) { return (long)B * ((S + kXencCK - 1) / kXencCK) * kXencCK * D; }
+
+template <typename T>
+static void launch_fm_t(const void* src, void* dst, int B, int S, int D, hipStream_t s) {
+  const long n16 = xenc_fm_elems(B, S, D) / 8;
+  const dim3 grid((unsigned)std::min<long>((n16 + 255) / 256, 4096));
+#define WCB_FM(DD) case DD: WCB_LAUNCH((xenc_fm_kernel<T, DD>), grid, dim3(256), 0, s, (const T*)src, (T*)dst, S, n16); break;
+  switch (D) { WCB_FM(64) WCB_FM(128) WCB_FM(256) WCB_FM(384) WCB_FM(512) WCB_FM(768) WCB_FM(1024) default: break; }
+#undef WCB_FM
+}
+
+void xenc_to_fm(DType t, const void* src, void* dst, int B, int S, int D, hipStream_t s) {
+  if (t == kBF16) launch_fm_t<bf16_t>(src, dst, B, S, D, s);
+  else if (t == kF16) launch_fm_t<f16_t>(src, dst, B, S, D, s);
+}
+
 bool xenc_supported(DType t, int D) {
   return (t == kBF16 || t == kF16) && (D == 384 || D == 768 || D == 1024 || D == 64 || D == 128 || D == 256 || D == 512);
 }
@@ -545,7 +600,18 @@ static void launch_xenc(const XencArgs& a, hipStream_t s) {
                               XregCfg<D>::LDS);
     (void)hipFuncSetAttribute((const void*)attn_xenc_reg_kernel<T, D, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               XregCfg<D>::LDS);
+    (void)hipFuncSetAttribute((const void*)attn_xenc_reg_kernel<T, D, 2, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              XregCfg<D>::LDS);
+    (void)hipFuncSetAttribute((const void*)attn_xenc_reg_kernel<T, D, 3, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              XregCfg<D>::LDS);
     attr_set = true;
+  }
+  if (a.fm) {   // the fragment-major chunk layout (register-ring variants 1 and 2 only)
+    if (a.variant == 2)
+      WCB_LAUNCH((attn_xenc_reg_kernel<T, D, 3, 4, true>), dim3(a.nsplit, a.rows), dim3(XregCfg<D>::NW * 64), XregCfg<D>::LDS, s, a);
+    else
+      WCB_LAUNCH((attn_xenc_reg_kernel<T, D, 2, 4, true>), dim3(a.nsplit, a.rows), dim3(XregCfg<D>::NW * 64), XregCfg<D>::LDS, s, a);
+    return;
   }
   if constexpr (D % (8 * 32) == 0 && D >= 512) {
     static bool attr8 = false;

@@ -186,8 +186,13 @@ struct XencArgs {
   Stamp stamp;
   int variant = 1;                              // 1 register chunk ring, 0 LDS-DMA chunk ring
   int row0 = 0, rows_per_enc = 1;               // row b reads encoder output (row0 + b) / rows_per_enc
+  int fm = 0;                                   // enc in the fragment-major chunk layout (xenc_to_fm; variants 1, 2)
 };
 bool xenc_supported(DType t, int D);
+// enc [B][S][D] → the fragment-major chunk layout of the register-ring kernel (xenc_fm_elems(B, S, D)
+// elements: S rounded up to whole 32-key chunks, zero rows past S)
+void xenc_to_fm(DType t, const void* src, void* dst, int B, int S, int D, hipStream_t s);
+long xenc_fm_elems(int B, int S, int D);
 void xenc_attention(DType t, const XencArgs& a, hipStream_t s);
 // u[r][h·D + c] = (Σ_s w_s part[r][s][h][c]) / L  (model dtype; ldu elements per row)
 void xenc_merge(DType t, const XencArgs& a, void* u, long ldu, hipStream_t s);

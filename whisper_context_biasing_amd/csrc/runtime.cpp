@@ -204,13 +204,17 @@ struct wcb_handle {
   // parallel streams (measured: C3 1814 -> 2215, C5 864 -> 983 audio-s/s; profiles/r01c_sweep_grp_*)
   int group_rows = 512;
   int xenc_split = 8;   // key ranges per row of the encoder-space kernel (rows x ranges workgroups)
+  // the decode's copy of the encoder output in the fragment-major chunk layout (k_xenc.hip
+  // xenc_fm_kernel): 1 KiB contiguous per load wave-instruction of the register-ring kernel, where the
+  // row layout touches 16 rows x 64 B (option "xenc_fm"; variants 1 and 2; bit-identical)
+  int xenc_fm = 1;
   int xenc_variant = 1; // attn_xenc kernel variant (k_xenc.hip)
   // decoder LayerNorm input of the fused LN projections: 1 = the T-typed copy of the residual stream
   // the producers write beside the f32 rows (half the bytes per projection workgroup; C2 decode 1.066
   // vs 1.110 ms/token), 0 = the f32 rows (f32 mode). WCB_LN16 overrides.
   int ln16 = 1;
   int vocab_pad = 0;    // LM-head rows padded to a multiple of 128 (zero rows): the MFMA tile path's N
-  int steps_per_graph = 8;   // decode steps captured per replayed graph (WCB_STEPS_PER_GRAPH)
+  int steps_per_graph = 8;   // decode steps captured per replayed graph (option "steps_per_graph")
   // decode projections of <= 64 rows on dec_lean_kernel (gemm_impl.h; bit-identical to
   // gemm_dec_kernel, one kernel-argument round trip and one load burst per launch; option "lean")
   int lean = 1;
@@ -570,6 +574,36 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "ring_kt") {
       REQUIRE(value == 1 || value == 2, "option ring_kt: 1 or 2");
       h->ring_kt = value;
+    } else if (n == "decode_cu_split") {
+      // decode context k's stream on half k % 2 of the CUs (alternate CU bits), so two overlapping decode
+      // chains never share a CU; 0: every CU, high priority (the default). Re-creates the decode streams.
+      REQUIRE(value == 0 || value == 1, "option decode_cu_split: 0 or 1");
+      REQUIRE(!h->step_state, "option decode_cu_split: a step-wise decode is active");
+      quiesce(h);
+      drop_graphs(h);
+      int ncu = 0;
+      HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
+      const int words = (ncu + 31) / 32;
+      int prio_lo = 0, prio_hi = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+      for (int ci = 0; ci < wcb_handle::kMaxCtx; ++ci) {
+        DecCtx& D = h->dc[ci];
+        if (D.hs) HIPCHK(hipStreamDestroy(D.hs));
+        D.hs = nullptr;
+        if (value) {
+          std::vector<uint32_t> mask(words, 0u);
+          for (int cu = 0; cu < ncu; ++cu)
+            if (cu % 2 == ci % 2) mask[cu / 32] |= 1u << (cu % 32);
+          HIPCHK(hipExtStreamCreateWithCUMask(&D.hs, (uint32_t)words, mask.data()));
+        } else {
+          HIPCHK(hipStreamCreateWithPriority(&D.hs, hipStreamNonBlocking, prio_hi));
+        }
+      }
+    } else if (n == "steps_per_graph") {
+      REQUIRE(value >= 1 && value <= 64, "option steps_per_graph: 1..64");
+      h->steps_per_graph = value;
+    } else if (n == "xenc_fm") {
+      h->xenc_fm = value != 0;
     } else if (n == "xq_kq") {
       h->xq_kq = value != 0;
     } else if (n == "enc_raster") {
@@ -972,7 +1006,7 @@ void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode
   rows = std::max(rows, B);
   const size_t e = esize(h->d.dtype), d = h->d.d_model, L = h->d.n_layers, S = h->S();
   const DecCtx& D0 = h->dc[c1 - 1];   // every context of the range is sized together
-  const size_t xbuf = xmode ? (size_t)clips * S * d * e : 2 * L * (size_t)clips * S * d * e;
+  const size_t xbuf = xmode ? (size_t)xenc_fm_elems(clips, (int)S, (int)d) * e : 2 * L * (size_t)clips * S * d * e;
   const size_t need[] = {xbuf, 2 * L * (size_t)B * T * d * e, (size_t)rows * d * 4,
                          (size_t)rows * h->d.ffn * e, (size_t)B * h->vocab_pad * 4, (size_t)(I_NEXT + 4 * B + 16) * 4,
                          (size_t)B * out_ld * 4};
@@ -1021,6 +1055,20 @@ void cross_kv(wcb_handle* h, int B, int buf, const void* enc) {
   GemmArgs g = rowgemm(enc, d, h->xkv_w, B * S, 2 * L * d, d, h->xkv2[buf].p, 0);
   g.bias = h->xkv_b; g.mode = 1; g.hs_S = S; g.hs_H = h->H(); g.hs_B = B;
   run_gemm(h, "xkv_gemm", g);
+}
+
+// the encoder-space decode's encoder output (xmode 1) in decode buffer `buf` from the row layout
+// [B][S][d] (fragment-major chunk layout when xenc_fm applies: the layout the register-ring kernel
+// streams), on stream st
+bool xenc_fm_on(const wcb_handle* h) { return h->xenc_fm && (h->xenc_variant == 1 || h->xenc_variant == 2); }
+void fill_xenc(wcb_handle* h, int buf, const void* src, int B, hipStream_t st) {
+  if (xenc_fm_on(h)) {
+    h->timed("xenc_layout", 0, 2.0 * B * h->S() * h->d.d_model * esize(h->d.dtype), st,
+             [&] { xenc_to_fm(h->dt, src, h->xkv2[buf].p, B, h->S(), h->d.d_model, st); });
+  } else if (src != h->xkv2[buf].p) {
+    HIPCHK(hipMemcpyAsync(h->xkv2[buf].p, src, (size_t)B * h->S() * h->d.d_model * esize(h->d.dtype),
+                          hipMemcpyDeviceToDevice, st));
+  }
 }
 
 struct StepCfg {
@@ -1181,7 +1229,8 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
         proj("dec_kq", kq);
       }
       XencArgs xa;
-      xa.enc = h->xkv2[c.buf].p; xa.enc_sb = (long)S * d;
+      xa.fm = xenc_fm_on(h);
+      xa.enc = h->xkv2[c.buf].p; xa.enc_sb = xa.fm ? xenc_fm_elems(1, S, d) : (long)S * d;
       xa.row0 = r0; xa.rows_per_enc = c.nb * rps;   // beams (and prefill positions) of a clip share its encoder output
       xa.qp = dqp; xa.rows = M; xa.H = H; xa.D = d; xa.S = S; xa.nsplit = h->xenc_split;
       xa.variant = h->xenc_variant;
@@ -1450,8 +1499,9 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     //      last read that buffer has finished. It overlaps the previous call's decode.
     sync_in(h, stream, h->he);
     HIPCHK(hipStreamWaitEvent(h->he, h->ev_dec[buf], 0));
-    if (xm == 1) {
-      encode_impl(h, mel, B, h->xkv2[buf].p);   // the decode reads the encoder output itself
+    if (xm == 1) {   // the decode reads the encoder output itself (re-laid out for the stream when xenc_fm)
+      encode_impl(h, mel, B, xenc_fm_on(h) ? nullptr : h->xkv2[buf].p);
+      if (xenc_fm_on(h)) fill_xenc(h, buf, h->encout.p, B, h->he);
     } else {
       encode_impl(h, mel, B, nullptr);
       h->timed_wall("xkv_gemm_total", h->he, [&] { cross_kv(h, B, buf, h->encout.p); });
@@ -1630,9 +1680,8 @@ int wcb_decode_begin(wcb_handle* h, const void* enc, int B, int num_beams, const
     DecCtx& D = h->dc[ci];
     sync_in(h, stream, D.hs);
     // the caller's encoder output [B][1500][d] (model dtype) is copied / projected into owned buffers
-    const size_t e = esize(h->d.dtype);
     if (xm == 1) {
-      HIPCHK(hipMemcpyAsync(h->xkv2[ci].p, enc, (size_t)B * h->S() * h->d.d_model * e, hipMemcpyDeviceToDevice, D.hs));
+      fill_xenc(h, ci, enc, B, D.hs);
     } else {
       sync_in(h, stream, h->he);
       cross_kv(h, B, ci, enc);                        // on the encoder stream
@@ -1738,10 +1787,10 @@ int wcb_forward(wcb_handle* h, const float* mel, int B, const int32_t* dec_ids, 
     const int buf = h->gen_count++ % h->nctx;
     sync_in(h, stream, h->he);
     HIPCHK(hipStreamWaitEvent(h->he, h->ev_dec[buf], 0));
-    const size_t enc_bytes = (size_t)B * h->S() * h->d.d_model * esize(h->d.dtype);
     if (h->xmode == 1) {
-      encode_impl(h, mel, B, h->xkv2[buf].p);
-      if (enc_out) HIPCHK(hipMemcpyAsync(enc_out, h->xkv2[buf].p, enc_bytes, hipMemcpyDeviceToDevice, h->he));
+      void* eo = enc_out ? enc_out : h->encout.p;
+      encode_impl(h, mel, B, eo);
+      fill_xenc(h, buf, eo, B, h->he);
     } else {
       void* eo = enc_out ? enc_out : h->encout.p;
       encode_impl(h, mel, B, eo);
@@ -1765,8 +1814,7 @@ int wcb_forward_enc(wcb_handle* h, const void* enc, int B, const int32_t* dec_id
     HIPCHK(hipStreamWaitEvent(h->he, h->ev_dec[buf], 0));
     // the given encoder output takes the place of encode_impl's: the same buffer (encoder space) or the
     // same cross-K/V GEMM over it (K/V formulation), so the logits equal wcb_forward's bit for bit
-    const size_t enc_bytes = (size_t)B * h->S() * h->d.d_model * esize(h->d.dtype);
-    if (h->xmode == 1) HIPCHK(hipMemcpyAsync(h->xkv2[buf].p, enc, enc_bytes, hipMemcpyDeviceToDevice, h->he));
+    if (h->xmode == 1) fill_xenc(h, buf, enc, B, h->he);
     else cross_kv(h, B, buf, enc);
     HIPCHK(hipEventRecord(h->ev_xkv[buf], h->he));
     forward_decode(h, buf, B, dec_ids, T, logits);
