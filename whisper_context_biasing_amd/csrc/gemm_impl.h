@@ -816,9 +816,16 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
     }
   };
   // ---------------- every load of the launch is issued here
-  Frag wc[KPW], wn[P ? KPW : 1];
+  // P (column walk): PD tiles of weights in flight ahead of the one being multiplied (a one-tile
+  // lookahead left each walker waiting a memory round trip per tile)
+  constexpr int PD = P ? 3 : 1;
+  Frag wc[KPW], wn[PD][KPW];
   int ct = blockIdx.x;
   load_w(wc, ct);
+  if constexpr (P) {
+#pragma unroll
+    for (int d = 0; d < PD - 1; ++d) load_w(wn[d], min(ct + (d + 1) * (int)gridDim.x, ntile - 1));
+  }
   Frag a[MF][KPW];
   f32x4 xf[AM == 1 ? MF : 1][AM == 1 ? KPW : 1][2];
   if constexpr (AM == 0 || AM == 2) {
@@ -930,12 +937,12 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
   int buf = 0;
   for (; ct < ntile; ct += gridDim.x) {
     const int n0 = ct * 16;
-    // P (persistent column walk): the next tile's weights are in flight behind this tile (clamped:
-    // an unconditional load keeps hipcc from draining the queue at the loop head)
+    // P (persistent column walk): the tile PD - 1 walker steps ahead goes in flight behind this one
+    // (clamped: an unconditional load keeps hipcc from draining the queue at the loop head); the next
+    // tile's boost bits one step ahead
     if constexpr (P) {
-      const int cn = min(ct + (int)gridDim.x, ntile - 1);
-      load_w(wn, cn);
-      if (boost) rbn = g.sel_root_bits[(cn * 16) >> 5];
+      load_w(wn[PD - 1], min(ct + PD * (int)gridDim.x, ntile - 1));
+      if (boost) rbn = g.sel_root_bits[(min(ct + (int)gridDim.x, ntile - 1) * 16) >> 5];
     }
     if constexpr (AM == 3) {
       const T* A = reinterpret_cast<const T*>(g.A) + (long)(n0 / g.a_grp_n) * g.a_grp_off;
@@ -1022,7 +1029,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
     buf ^= 1;
     if constexpr (P) {
 #pragma unroll
-      for (int ks = 0; ks < KPW; ++ks) wc[ks] = wn[ks];
+      for (int ks = 0; ks < KPW; ++ks) wc[ks] = wn[0][ks];
+#pragma unroll
+      for (int d = 0; d < PD - 1; ++d)
+#pragma unroll
+        for (int ks = 0; ks < KPW; ++ks) wn[d][ks] = wn[d + 1][ks];
       rbw = rbn;
     } else {
       break;

@@ -358,9 +358,10 @@ __global__ __launch_bounds__(256) void beam_step_kernel(BeamArgs a) {
     for (int k = 0; k < K; ++k) allhit &= hit[k] != 0;
     __hip_atomic_store(a.flags + 2 * b, (unsat_old && any) ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(a.flags + 2 * b + 1, allhit ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __threadfence();
+    // the flags went out write-through (sc1); drained before the ticket, read back with sc1 loads by the
+    // utterance whose add returns last (MI355X_MICROARCH.md "Valid forms", row 1): no fences
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (atomicAdd(a.ticket, 1) == a.B - 1) {    // every utterance has arrived
-      __threadfence();
       bool any_unsat = false, all_hit = true;
       for (int u = 0; u < a.B; ++u) {
         any_unsat |= __hip_atomic_load(a.flags + 2 * u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
@@ -370,7 +371,6 @@ __global__ __launch_bounds__(256) void beam_step_kernel(BeamArgs a) {
       *a.pos = *a.pos + 1;
       if ((!any_unsat || all_hit) && *a.all_done == 0) *a.all_done = step + 1;
       *a.ticket = 0;
-      __threadfence();
     }
   }
 }

@@ -109,17 +109,16 @@ __global__ __launch_bounds__(64) void select_finalize_kernel(SelectArgs a) {
     if (a.out_score) a.out_score[m] = fin ? 0.f : bv;
     const bool nf = fin || tok == a.eos;
     a.finished[m] = nf ? 1 : 0;
-    if (!nf) atomicAdd(a.unfinished, 1);
-    __threadfence();
-    if (atomicAdd(a.ticket, 1) == a.M - 1) {       // every row has arrived
-      __threadfence();
-      const int nun = atomicAdd(a.unfinished, 0);
+    // one 64-bit counter: arrivals in the low word, unfinished rows in the high word, so the row that
+    // arrives last reads the complete count from the value its own add returns — no fence (the other
+    // rows' stores are read only by later launches, behind the kernel boundary)
+    const unsigned long long old = atomicAdd(a.ticket_unfin, 1ull + (nf ? 0ull : (1ull << 32)));
+    if ((unsigned)(old & 0xffffffffull) == (unsigned)(a.M - 1)) {   // every row has arrived
+      const int nun = (int)(old >> 32) + (nf ? 0 : 1);
       *a.step = step + 1;
       *a.pos = *a.pos + 1;
       if (nun == 0 && *a.all_done == 0) *a.all_done = step + 1;
-      *a.unfinished = 0;
-      *a.ticket = 0;
-      __threadfence();
+      *a.ticket_unfin = 0ull;
     }
   }
 }

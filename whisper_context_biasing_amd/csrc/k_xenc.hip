@@ -35,6 +35,18 @@
 namespace wcb {
 
 constexpr int kXencCK = 32;   // keys per chunk
+
+// tools/xattn_probe.hip builds this file with WCB_XENC_PROBE: the register-ring kernel then writes
+// s_memtime stamps of its phases (wave 0) to a.stamp.base[workgroup][16] instead of the launch stamps
+#ifdef WCB_XENC_PROBE
+#define XPROBE(k)                                                                                        \
+  do {                                                                                                   \
+    if (threadIdx.x == 0)                                                                                \
+      a.stamp.base[(blockIdx.y * gridDim.x + blockIdx.x) * 16 + (k)] = __builtin_amdgcn_s_memtime();     \
+  } while (0)
+#else
+#define XPROBE(k) do {} while (0)
+#endif
 constexpr int kXencNW = 8;    // waves per workgroup
 
 template <int D> struct XencCfg {
@@ -263,6 +275,7 @@ __global__ __launch_bounds__((XregCfg<D, WNW>::NW * 64), ((NR == 2 && WNW == 4) 
   f32x4* red = reinterpret_cast<f32x4*>(lds + NW * C::TILE);
   const int split = blockIdx.x, b = blockIdx.y;
   const unsigned long long t_start = a.stamp.base ? stamp_now() : 0;
+  XPROBE(0);
   const int per = ((a.S + a.nsplit - 1) / a.nsplit + CK - 1) / CK * CK;
   const int k_lo = split * per, k_hi = min(a.S, k_lo + per);
   const int nch = k_hi > k_lo ? (k_hi - k_lo + CK - 1) / CK : 0;
@@ -367,6 +380,7 @@ __global__ __launch_bounds__((XregCfg<D, WNW>::NW * 64), ((NR == 2 && WNW == 4) 
       const Frag ef = tr_frag<T>(tile + (c0 >> 6) * PANEL, 0, ((c0 & 63) >> 4) * 2, lane);
       acc[t] = mma16(ef, pf, acc[t]);
     }
+    XPROBE(2 + min(c, 7));
   };
 
   if (nch > 0) {
@@ -375,6 +389,7 @@ __global__ __launch_bounds__((XregCfg<D, WNW>::NW * 64), ((NR == 2 && WNW == 4) 
       Frag fa[2][KSW], fb[2][KSW];
       load_chunk(fa, 0);
       load_chunk(fb, 1);
+      XPROBE(1);
       for (int c = 0; c < nch; c += 2) {
         body(fa, c);
         body(fb, c + 1);
@@ -394,6 +409,7 @@ __global__ __launch_bounds__((XregCfg<D, WNW>::NW * 64), ((NR == 2 && WNW == 4) 
   // ---- range partials: lane holds Uᵀ[cw0 + 16t + 4(lane>>4) + e][head lane&15]
   l_run = xor16_add(l_run);
   l_run = xor32_add(l_run);
+  XPROBE(10);
   if (hq < a.H) {
     const long slot = ((long)b * a.nsplit + split) * a.H + hq;
     float* pp = a.part + slot * D + cw0 + 4 * (lane >> 4);
@@ -401,10 +417,15 @@ __global__ __launch_bounds__((XregCfg<D, WNW>::NW * 64), ((NR == 2 && WNW == 4) 
     for (int t = 0; t < CTW; ++t) *reinterpret_cast<f32x4*>(pp + t * 16) = acc[t];
     if (wave == 0 && lane < 16) *reinterpret_cast<float2*>(a.ml + slot * 2) = float2{m_run, l_run};
   }
+#ifdef WCB_XENC_PROBE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  XPROBE(11);
+#else
   if (a.stamp.base) {
     __syncthreads();
     if (tid == 0) stamp_commit(a.stamp, t_start);
   }
+#endif
 }
 
 template <typename T, int D>

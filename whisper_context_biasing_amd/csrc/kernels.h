@@ -222,7 +222,7 @@ struct SelectArgs {
   int* next_ids = nullptr; int* out_ids = nullptr; int out_ld = 0;
   float* part_val = nullptr; int* part_idx = nullptr; int nchunk = 0;
   int* all_done = nullptr;
-  int* ticket = nullptr; int* unfinished = nullptr;   // zero between steps (reset by the last row)
+  unsigned long long* ticket_unfin = nullptr;   // arrivals | unfinished << 32, zero between steps (reset by the last row)
   float* out_score = nullptr;        // optional: the chosen token's (boosted) logit per row (0 for finished rows)
 };
 void select_greedy(const SelectArgs& a, hipStream_t s);          // vocabulary pass + finalize

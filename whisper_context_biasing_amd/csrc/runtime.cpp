@@ -982,7 +982,8 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
   h->timed("layernorm", 0, M * d * (4.0 + e), h->he, [&] { layernorm(h->dt, h->x.as<float>(), h->enc_ln_w, h->enc_ln_b, dst, (int)M, d, h->he); });
 }
 
-enum { I_STEP = 0, I_POS = 1, I_DONE = 2, I_TICKET = 3, I_UNFIN = 4, I_NEXT = 16 };
+// device ints of a decode context: I_TU = the greedy select's 64-bit arrival | unfinished counter (8-byte aligned)
+enum { I_STEP = 0, I_POS = 1, I_DONE = 2, I_TICKET = 3, I_UNFIN = 4, I_TU = 6, I_NEXT = 16 };
 
 void drop_graphs(wcb_handle* h) {
   for (DecCtx& D : h->dc) {
@@ -1393,7 +1394,7 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     s.out_ids = D.outbuf.as<int>(); s.out_ld = c.out_ld;
     s.part_val = D.part_val.as<float>(); s.part_idx = D.part_idx.as<int>(); s.nchunk = D.nchunk;
     s.all_done = ints + I_DONE;
-    s.ticket = ints + I_TICKET; s.unfinished = ints + I_UNFIN;
+    s.ticket_unfin = reinterpret_cast<unsigned long long*>(ints + I_TU);
     s.out_score = c.score_out;
     h->timed("dec_select", 0, (double)B * D.nchunk * 8, D.hs, [&] { select_finalize(s, D.hs); });
   } else {
