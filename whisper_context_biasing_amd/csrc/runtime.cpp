@@ -222,8 +222,10 @@ struct wcb_handle {
   // fragment-major for the LayerNorm-fused consumers (QKV, xq, fc1); option "lean_x"
   int lean_x = 1;
   // lean path, one position per row: the new token's self-attention inside the QKV launch (option
-  // "qkv_sa"; gemm_impl.h dec_lean_kernel SA; bit-identical to the two launches)
-  int qkv_sa = 1;
+  // "qkv_sa"; gemm_impl.h dec_lean_kernel SA; bit-identical to the two launches). Off by default:
+  // measured slower than the two launches (rocprofv3, C2 decode: 13.2 µs fused against 5.3 + 5.1 µs;
+  // the attention's K/V reads must bypass the caches (sc1) behind the in-launch hand-off)
+  int qkv_sa = 0;
   struct wcb_state* step_state = nullptr;   // the active step-wise decode (wcb_decode_begin), if any
   // encoder GEMM tile order (option "enc_raster"): bands of n row panels with the column tiles outer
   // (GemmArgs::raster; 0 = row-major). 8 measured best with the round-3 ring kernel (whisper-small:
