@@ -87,7 +87,9 @@ const char* wcb_last_error(const wcb_handle* h);
  *                      layout (1, default; 1 KiB contiguous per load wave-instruction) or the row layout (0)
  *   "ring_kt" 1/2      decode rows > 64: 64-deep K sub-tiles per LDS-ring stage of the projection tiles
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)
- *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave), 4 (64 queries, default)
+ *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave), 4 (64 queries, default),
+ *                      5 (64 queries, P·V per query fragment; bit-identical to 4), 6 (64 queries, q
+ *                      pre-scaled by log2 e in the QKV epilogue, scores relative to the running max)
  *   "enc_raster" n     encoder GEMM tile order: bands of n row panels, column tiles outer (8, default;
  *                      0: row-major); bit-identical */
 int wcb_set_option(wcb_handle* h, const char* name, int value);
@@ -211,6 +213,12 @@ int wcb_debug_copy(wcb_handle* h, const char* name, void* dst, int64_t bytes, in
 /* out[M][N] = act(A[M][K] · W[N][K]ᵀ + bias) (+ resid), row-major, dtype of A/W = dtype */
 int wcb_op_gemm(int dtype, const void* A, const void* W, int M, int N, int K, const float* bias, int act,
                 const float* resid, void* out, int out_f32, void* stream);
+/* the same with the encoder-GEMM kernel chosen: kernel 1 = the ping-pong kernel where it covers the shape
+ * and is the faster one (16-bit, N % 256 == 0, K % 64 == 0, K >= 128, M >= 256, no residual epilogue; the
+ * runtime's default, option "enc_gemm"), 2 = the ping-pong kernel for every shape it covers (residual
+ * epilogue included), 0 = the LDS-ring / tile kernels */
+int wcb_op_gemm_kernel(int dtype, const void* A, const void* W, int M, int N, int K, const float* bias, int act,
+                       const float* resid, void* out, int out_f32, int kernel, void* stream);
 /* decode-step fused form: out[M][N] = act(LN(X) · W[N][K]ᵀ + bias), X f32 [M][K] (M <= 64), with the
  * LayerNorm row statistics taken from stats[M][K/16][2] = per-16-column (Σx, Σx²) partials */
 int wcb_op_gemm_ln(int dtype, const float* X, const float* ln_w, const float* ln_b, const float* stats,
@@ -221,7 +229,8 @@ int wcb_op_layernorm(int dtype, const float* x, const float* w, const float* b, 
                      void* stream);
 /* o[B][Sq][H*64] = softmax(q kᵀ) v per head (q pre-scaled), k/v [B][Sk][H*64];
  * flash=1 selects the MFMA kernel (16-bit dtypes; Sq <= 16: the few-query form of beam search), 100 the
- * MFMA kernel with 64 queries per wave, 200 / 201 / 202 (Sq <= 16) the beam kernel (the keys of a (set,
+ * MFMA kernel with 64 queries per wave, 101 the same with P·V per query fragment, 102 the same with q
+ * given pre-scaled by log2(e) (softmax in base 2), 200 / 201 / 202 (Sq <= 16) the beam kernel (the keys of a (set,
  * head) split over its waves, merged in the workgroup: 4 waves x 2 LDS stages, 2 x 4, 2 x 5), -n (Sq <= 16)
  * the MFMA kernel over n key ranges merged in
  * fixed order; 0 the decode kernel; n >= 2 the decode kernel with n split-KV key chunks combined by the

@@ -120,8 +120,15 @@ def test_flash_attention(dt, S):
     # P is rounded to the 16-bit type before P·V: |err| ≲ 2^-8 relative for bf16
     tol = 1e-2 if dt == "bf16" else 2e-3
     assert (o.double() - ref).abs().max().item() < tol
-    o4 = _attn(dt, q, k, v, 100)   # 64 queries per wave (encoder option enc_flash_qw = 4)
+    o4 = _attn(dt, q, k, v, 100)   # 64 queries per wave (encoder option enc_flash = 4)
     assert (o4.double() - ref).abs().max().item() < tol
+    o5 = _attn(dt, q, k, v, 101)   # the same, P·V per query fragment (enc_flash = 5): bit-identical
+    assert torch.equal(o5, o4)
+    # enc_flash = 6: q pre-scaled by log2(e) (the QKV epilogue's one rounding), base-2 softmax
+    q2 = (q.float() * 1.4426950408889634).to(DT[dt][0])
+    o6 = _attn(dt, q2, k, v, 102)
+    ref2 = _attn_ref(q2.double() / 1.4426950408889634, k, v)
+    assert (o6.double() - ref2).abs().max().item() < tol
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
@@ -278,6 +285,55 @@ def test_gemm_ring_encoder_shapes(dt, M, N, K, act, resid):
     tol = 1e-4 if resid else (8e-3 if dt == "bf16" else 1e-3)
     err = ((out.double() - ref).abs() - tol * ref.abs()).max().item()
     assert err < 2e-4, err
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("M,N,K,act,resid,bias,f32", [
+    (4096, 768, 768, 0, False, True, False), (6000, 2304, 768, 0, False, True, False),
+    (5000, 768, 3072, 0, True, True, True), (4100, 3072, 768, 1, False, True, False),
+    (300, 256, 64, 0, False, True, False),      # one K tile (the LDS-ring kernel takes it)
+    (511, 512, 128, 1, False, False, False),    # two K tiles, no bias
+    (257, 256, 192, 0, True, True, True),       # three K tiles, one row past a tile
+    (1000, 1024, 320, 0, False, False, True),   # f32 out without a residual
+    # more tiles than workgroups (256): each workgroup streams several tiles' K tiles back to back
+    (8200, 2304, 128, 0, False, True, False), (16500, 1024, 192, 1, False, True, False),
+    (48000, 768, 768, 0, True, True, True), (33000, 2304, 768, 0, False, True, False)])
+def test_gemm_pingpong_kernel(dt, M, N, K, act, resid, bias, f32):
+    """The ping-pong encoder GEMM (gemm_pp_kernel: 256x256 tiles, staggered wave halves, counted LDS-DMA
+    waits, persistent K-tile stream) through wcb_op_gemm_kernel(kernel=2), every K-tile count of its piece schedule's tail (1, 2, 3,
+    many), ragged M, each epilogue, vs fp64 and against the LDS-ring kernel (kernel=0)."""
+    lib = _lib.load()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + 1)
+    A = torch.randn(M, K, generator=g).to(DT[dt][0]).cuda()
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(DT[dt][0]).cuda()
+    b = torch.randn(N, generator=g).float().cuda() if bias else None
+    R = torch.randn(M, N, generator=g).float().cuda() if resid else None
+
+    def run(kernel):
+        out = torch.full((M, N), float("nan"), device="cuda", dtype=torch.float32 if f32 else A.dtype)
+        if resid:
+            out.copy_(R)   # in place, as the encoder's residual stream
+        _lib.check(lib.wcb_op_gemm_kernel(DT[dt][1], A.data_ptr(), W.data_ptr(), M, N, K,
+                                          b.data_ptr() if bias else None, act,
+                                          out.data_ptr() if resid else None, out.data_ptr(), int(f32), kernel,
+                                          _s()), None, "gemm")
+        torch.cuda.synchronize()
+        return out
+    out = run(2)
+    ref = A.double() @ W.double().T
+    if bias:
+        ref = ref + b.double()
+    if act:
+        ref = torch.nn.functional.gelu(ref)
+    if resid:
+        ref = ref + R.double()
+    tol = 1e-4 if f32 else (8e-3 if dt == "bf16" else 1e-3)
+    err = ((out.double() - ref).abs() - tol * ref.abs()).max().item()
+    assert err < 2e-4, err
+    assert torch.equal(run(2), out)   # deterministic
+    other = run(0)
+    err0 = ((other.double() - ref).abs() - tol * ref.abs()).max().item()
+    assert err0 < 2e-4, err0
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f32"])

@@ -30,9 +30,22 @@ def xenc_case(rows=32, nsplit=8, variant=1):
 
 if __name__ == "__main__":
     torch.manual_seed(0)
-    attn_case(32, 12, 1500, 1500, 100)
-    attn_case(32, 12, 1500, 1500, 1)
-    for (M, N, K) in [(48000, 2304, 768), (48000, 768, 768), (48000, 3072, 768), (48000, 768, 3072)]:
-        gemm_case(M, N, K)
-    ln_case(48000, 768)
-    xenc_case()
+    only = sys.argv[1] if len(sys.argv) > 1 else ""
+    if only in ("", "attn"):
+        attn_case(32, 12, 1500, 1500, 100)
+        attn_case(32, 12, 1500, 1500, 101)
+        attn_case(32, 12, 1500, 1500, 102)
+        attn_case(32, 12, 1500, 1500, 1)
+    shapes = [(48000, 2304, 768, 0, False), (48000, 768, 768, 0, True),
+              (48000, 3072, 768, 1, False), (48000, 768, 3072, 0, True)]
+    if only == "gemm-medium":   # C3: whisper-medium, 64 clips
+        shapes = [(96000, 3072, 1024, 0, False), (96000, 1024, 1024, 0, True),
+                  (96000, 4096, 1024, 1, False), (96000, 1024, 4096, 0, True)]
+        only = "gemm"
+    for (M, N, K, act, resid) in shapes:
+        if only in ("", "gemm"):
+            for kernel in (0, 2):
+                gemm_case(M, N, K, kernel=kernel, act=act, resid=resid)
+    if only == "":
+        ln_case(48000, 768)
+        xenc_case()

@@ -36,18 +36,25 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-def gemm_case(M, N, K, dt=torch.bfloat16):
+def gemm_case(M, N, K, dt=torch.bfloat16, kernel=1, act=0, resid=False):
+    """kernel 1: the runtime's encoder-GEMM choice (ping-pong kernel where it is the faster one), 2: the
+    ping-pong kernel wherever it covers the shape, 0: the LDS-ring / tile kernels; act 1 = bias + GELU, resid = bias + residual into f32 (the encoder epilogues)"""
     A = torch.randn(M, K, device="cuda").to(dt)
     W = torch.randn(N, K, device="cuda").to(dt)
-    out = torch.empty(M, N, device="cuda", dtype=dt)
+    bias = torch.randn(N, device="cuda")
+    out = torch.zeros(M, N, device="cuda", dtype=torch.float32 if resid else dt)
     code = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2}[dt]
 
     def fn():
-        lib.wcb_op_gemm(code, A.data_ptr(), W.data_ptr(), M, N, K, None, 0, None, out.data_ptr(), 0, stream())
+        assert lib.wcb_op_gemm_kernel(code, A.data_ptr(), W.data_ptr(), M, N, K, bias.data_ptr(), act,
+                                      out.data_ptr() if resid else None, out.data_ptr(), int(resid), kernel,
+                                      stream()) == 0
     us = per_launch_us(fn, reps=20 if M > 64 else 50)
     flops = 2.0 * M * N * K
     byts = (M * K + N * K + M * N) * A.element_size()
-    print(f"gemm M={M:6d} N={N:6d} K={K:5d}: {us:9.2f} us  {flops / us / 1e6:8.1f} TFLOP/s  {byts / us / 1e3:8.1f} GB/s")
+    print(f"gemm M={M:6d} N={N:6d} K={K:5d} kernel={kernel} act={act} resid={int(resid)}: {us:9.2f} us  "
+          f"{flops / us / 1e6:8.1f} TFLOP/s  {byts / us / 1e3:8.1f} GB/s", flush=True)
+    return us
 
 
 def gemm_ln_case(M, N, K):

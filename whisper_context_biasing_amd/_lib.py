@@ -62,6 +62,8 @@ SIGNATURES = {
     "wcb_profile_kernel": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_int64)]),
     "wcb_op_gemm": (C.c_int, [C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P, _P,
                               C.c_int, _P]),
+    "wcb_op_gemm_kernel": (C.c_int, [C.c_int, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P, _P,
+                                     C.c_int, C.c_int, _P]),
     "wcb_op_gemm_ln": (C.c_int, [C.c_int, _P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int, _P, C.c_int, _P,
                                  C.c_int, _P]),
     "wcb_op_weighted_ce": (C.c_int, [_P, C.c_long, C.c_int, C.c_int, C.c_int, _P, _P, _P, C.c_int, C.c_int,

@@ -139,6 +139,7 @@ WCB_DEV float epi_store1(const GemmArgs& g, int m, int n, float v) {
 template <typename T, int EPI = E_RUNTIME>
 WCB_DEV float epi_pointwise(const GemmArgs& g, int m, int n, float v) {
   if (has<EPI>(g, E_BIAS)) v += g.bias[n];
+  if (n < g.col_scale_n) v *= g.col_scale;
   if (has<EPI>(g, E_GELU)) v = gelu_t<T>(v);
   if (has<EPI>(g, E_ADDROW)) v += g.addrow[(long)(g.c_Mb ? m % g.c_Mb : m) * g.N + n];
   return v;
@@ -491,6 +492,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {   // epi_pointwise's order: + bias, GELU, + row table
         if (has<EPI>(g, E_BIAS)) v[e] += b8[e];
+        if (n < g.col_scale_n) v[e] *= g.col_scale;
         if (has<EPI>(g, E_GELU)) v[e] = gelu_t<T>(v[e]);
         if (has<EPI>(g, E_ADDROW))
           v[e] += g.addrow[(long)(g.c_Mb ? min(m, g.M - 1) % g.c_Mb : min(m, g.M - 1)) * g.N + min(n + e, g.N - 1)];
@@ -542,6 +544,319 @@ static void launch_ring(const GemmArgs& g, hipStream_t s) {
       launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_GELU | E_F32 | E_ADDROW, false, 1, BKB, PRIO>(g, s); break;
     case E_BIAS | E_HEAD: launch_ring_e<T, BM, BN, WM, WN, NS, E_BIAS | E_HEAD, false, 1, BKB, PRIO>(g, s); break;
     default: launch_ring_e<T, BM, BN, WM, WN, NS, E_RUNTIME, false, 1, BKB, PRIO>(g, s); break;
+  }
+}
+
+// ---- Encoder GEMM, ping-pong form (gemm_pp_kernel): 256 x 256 output tiles, 64-deep K tiles, 8 waves
+// as 2 (row halves) x 4 (64-column quarters), one persistent workgroup per CU (128 KiB of LDS: two
+// K-tile buffers, each A [256][64] + W [256][64] in 128-byte rows, 16-byte chunk c of row r at slot
+// c ^ ((r >> 1) & 7), the swizzle applied to the DMA source address) walking tiles blockIdx.x,
+// blockIdx.x + gridDim.x, ... as ONE stream of K tiles: the LDS-DMA for the next tile's first K tiles is
+// issued during the current tile's last ones, and its epilogue stores drain behind the next tile's
+// multiplies (measured before: a 12-K-tile tile spent 9k of its 54k cycles filling the pipe and 10k
+// draining its stores, tools/gemm_probe).
+// Waves 4-7 run one barrier behind waves 0-3, and each SIMD holds one wave of each half, so in every
+// barrier interval one wave of a SIMD multiplies while its partner reads its next fragments from LDS
+// and issues LDS-DMA for later K tiles (MI355X_MICROARCH.md "Two waves per SIMD";
+// cdna_hip_programming.md "The 256² 8-phase template").
+// A K tile is 4 phases; phase p multiplies the wave's rows [32p, 32p + 32) (2 row fragments) with its
+// 64 columns (4 weight fragments, read in phase 0 and kept) over 2 k-steps: 16 MFMAs.
+// LDS-DMA pieces (one 16-byte load per thread each): "A quarter" q = the 64 tile rows phase q reads
+// (rows 32q.. of both halves), one piece; the weight halves (128 rows), two pieces each. K tile t of the
+// stream: W left + A q0 in phase 2 and W right + A q1 in phase 3 of K tile t - 2, A q2 / A q3 in phases
+// 0 / 1 of K tile t - 1: every piece is issued >= 3 phases before its first read and restaged >= 2
+// phases after its last read (the distance the one-barrier stagger needs for WAR). Waits are counted
+// s_waitcnt vmcnt; a tile's epilogue issues exactly S vector-memory operations (rows past M are
+// stored to a scratch slot, not skipped), counted into the waits they sit behind.
+// The weight fragment is the MFMA's A operand, so a lane's accumulator holds 4 consecutive columns
+// of one output row: the epilogue (bias, GELU, residual, store) runs from registers, no LDS pass.
+// tools/gemm_probe.hip builds this header with WCB_GEMM_PROBE: wave 0 of every workgroup then stamps
+// s_memtime at its phases into wcb_gemm_probe[workgroup][8] (its first tile)
+#ifdef WCB_GEMM_PROBE
+__device__ unsigned long long* wcb_gemm_probe;
+#define GPROBE(k)                                                                              \
+  do {                                                                                         \
+    if (threadIdx.x == 0) wcb_gemm_probe[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define GPROBE(k) do {} while (0)
+#endif
+__device__ float wcb_pp_zeros[8192];            // the bias of a launch without one
+__device__ __attribute__((aligned(16))) char wcb_pp_scratch[64 * 16];   // stores of rows past M
+
+template <int N> WCB_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N < 63 ? N : 63) : "memory"); }
+
+template <typename T, int EPI>
+__global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
+  using Frag = typename DT<T>::frag;
+  constexpr int BUF = 65536, WOFF = 32768;
+  // vector-memory operations a tile's epilogue issues: 32 stores (+ 32 residual loads). (Wave 0 also
+  // moves the tile's 256 bias values into LDS by one more DMA in phase 0 of its first K tile: every
+  // count below then over-waits by one for that wave, which is safe.)
+  constexpr int S = 32 + ((EPI & E_RESID) ? 32 : 0);
+  constexpr int BIAS_LDS = 2 * BUF;   // [tile parity][256] f32
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  GPROBE(0);
+  const int tiles_n = g.N >> 8, tiles_m = (g.M + 255) >> 8, ntiles = tiles_m * tiles_n;
+  const int nk = g.K >> 6;
+  const int my = (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;   // tiles of this workgroup
+  const int total = my * nk;                                             // K tiles of its stream
+  auto origin = [&](int it, int& m0, int& n0) {
+    const int wg = xcd_remap((int)blockIdx.x + it * (int)gridDim.x, ntiles);
+    if (g.raster > 0) {   // bands of `raster` row panels, column tiles outer within a band
+      const int band = g.raster * tiles_n;
+      const int fm = (wg / band) * g.raster, gm = min(tiles_m - fm, g.raster), r = wg % band;
+      m0 = (fm + r % gm) * 256;
+      n0 = (r / gm) * 256;
+    } else {
+      m0 = (wg / tiles_n) * 256;
+      n0 = (wg % tiles_n) * 256;
+    }
+  };
+  auto swzr = [](int r) { return (r >> 1) & 7; };
+  const T* A = reinterpret_cast<const T*>(g.A);
+  const T* W = reinterpret_cast<const T*>(g.W);
+  // DMA geometry of this lane: A piece p → tile row ar[p] (element offset aoff[p] from the tile's first
+  // row), W piece t → tile row 64t + i8 (boff[t])
+  const int i8 = 8 * wave + (lane >> 3), ch = lane & 7;
+  // the last row panel (m0 = m_last) re-reads row M - 1 for the rows past M: aoff_last
+  const int m_last = (tiles_m - 1) * 256;
+  int aoff[4], aoff_last[4], boff[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int ar = i8 < 32 ? 32 * p + i8 : 96 + 32 * p + i8;
+    const int cs = (ch ^ swzr(ar)) << 3;
+    aoff[p] = ar * (int)g.lda + cs;
+    aoff_last[p] = (min(m_last + ar, g.M - 1) - m_last) * (int)g.lda + cs;
+    boff[p] = (64 * p + i8) * (int)g.ldw + ((ch ^ swzr(64 * p + i8)) << 3);
+  }
+  // stream cursors: tile iteration, K tile, tile origin, and the tile's A / W panel pointers advanced to
+  // the K tile (scalar: a DMA adds only the lane's offset)
+  struct Cur { int it, kt, m0, n0; const T* a; const T* b; bool last; };
+  auto set_tile = [&](Cur& c) {
+    origin(c.it, c.m0, c.n0);
+    c.a = A + (long)c.m0 * g.lda;
+    c.b = W + (long)c.n0 * g.ldw;
+    c.last = c.m0 == m_last;
+  };
+  auto advance = [&](Cur& c) {
+    c.a += 64;
+    c.b += 64;
+    if (++c.kt == nk) {
+      c.kt = 0;
+      if (++c.it < my) set_tile(c);
+    }
+  };
+  auto dma_a = [&](int p, const Cur& c, int gk) {
+    glds16(c.a + (c.last ? aoff_last[p] : aoff[p]),
+           smem + (gk & 1) * BUF + (wave < 4 ? 32 * p + 8 * wave : 96 + 32 * p + 8 * wave) * 128);
+  };
+  auto dma_b = [&](int t, const Cur& c, int gk) {
+    glds16(c.b + boff[t], smem + (gk & 1) * BUF + WOFF + (64 * t + 8 * wave) * 128);
+  };
+  auto barrier = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Cur cc;   // the K tile being multiplied
+  cc.it = 0; cc.kt = 0;
+  set_tile(cc);
+  Cur c1 = cc, c2 = cc;   // the K tiles one and two ahead (their DMA)
+  advance(c1);
+  advance(c2);
+  advance(c2);
+  // K tiles 0 and 1 in the steady-state piece order
+  dma_b(0, cc, 0); dma_b(1, cc, 0); dma_a(0, cc, 0); dma_b(2, cc, 0); dma_b(3, cc, 0); dma_a(1, cc, 0);
+  dma_a(2, cc, 0); dma_a(3, cc, 0);
+  if (total > 1) { dma_b(0, c1, 1); dma_b(1, c1, 1); dma_a(0, c1, 1); dma_b(2, c1, 1); dma_b(3, c1, 1); dma_a(1, c1, 1); }
+  GPROBE(1);
+  if (total > 1) vm_wait<9>();   // W(0) and A q0(0) landed
+  else vm_wait<3>();
+  GPROBE(2);
+  barrier();
+  if (wr == 1) barrier();   // the stagger: waves 4-7 one barrier behind
+
+  const int c0 = lane >> 4;
+  const float* bias = g.bias ? g.bias : wcb_pp_zeros;
+  // one K tile of the stream. ST (steady): K tile >= 2 of its tile with two more after it in the stream —
+  // the waits are the plain counts and every DMA is issued, no run-time branch in its phases (the
+  // general form's branches cost ≈ 600 cycles per K tile, tools/gemm_probe)
+  // fragment reads: the swizzle term of row base + (lane & 15) is ((lane >> 1) & 7) for every 16-aligned
+  // base, so a read address is a per-lane constant (one per k-step) plus a compile-time offset
+  const int sl = (lane >> 1) & 7;
+  const int lo0 = (lane & 15) * 128 + ((c0 ^ sl) << 4), lo1 = (lane & 15) * 128 + (((4 + c0) ^ sl) << 4);
+  const int wb0 = WOFF + 64 * wc * 128 + lo0, wb1 = WOFF + 64 * wc * 128 + lo1;   // this wave's W rows
+  const int ab0 = 128 * wr * 128 + lo0, ab1 = 128 * wr * 128 + lo1;                 // this wave's A rows
+  auto ktile = [&](int gk, auto steady_tag) {
+    constexpr bool ST = decltype(steady_tag)::value;
+    const char* buf = smem + (gk & 1) * BUF;
+    const bool n1 = ST || gk + 1 < total, n2 = ST || gk + 2 < total;
+    // the previous tile's epilogue operations sit between this phase's piece and the younger ones
+    const bool e0 = !ST && cc.kt == 0 && cc.it > 0, e1 = !ST && cc.kt == 1 && cc.it > 0;
+    // the plain counts (one scalar branch per phase; the general cases below run on <= 3 K tiles a tile)
+    const bool plain = ST || (n2 && !e0 && !e1);
+    Frag bw[4][2];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      // retire the piece the NEXT phase reads (this phase's own pieces were retired one phase ago)
+      if (plain) {
+        if (p < 3) vm_wait<8>();
+        else vm_wait<6>();
+      } else if (p == 0) {
+        if (n1) { if (e0 || e1) vm_wait<8 + S>(); else vm_wait<8>(); }
+        else { if (e0 || e1) vm_wait<2 + S>(); else vm_wait<2>(); }
+      } else if (p == 1) {
+        if (n1) { if (e0) vm_wait<8 + S>(); else vm_wait<8>(); }
+        else { if (e0) vm_wait<1 + S>(); else vm_wait<1>(); }
+      } else if (p == 2) {
+        if (n1) { if (e0) vm_wait<8 + S>(); else vm_wait<8>(); }
+        else { if (e0) vm_wait<S>(); else vm_wait<0>(); }
+      } else if (n1) {
+        if (n2) { if (e0) vm_wait<6 + S>(); else vm_wait<6>(); }
+        else { if (e0) vm_wait<3 + S>(); else vm_wait<3>(); }
+      }
+      if (p == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bw[j][0] = *reinterpret_cast<const Frag*>(buf + wb0 + j * 16 * 128);
+          bw[j][1] = *reinterpret_cast<const Frag*>(buf + wb1 + j * 16 * 128);
+        }
+      }
+      if (!ST && p == 0 && cc.kt == 0 && wave == 0)   // this tile's bias into LDS (a global load in the
+                                                      // epilogue would make hipcc wait for every DMA piece)
+        glds16(bias + cc.n0 + 4 * lane, smem + BIAS_LDS + (cc.it & 1) * 1024);
+      Frag af[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        af[i][0] = *reinterpret_cast<const Frag*>(buf + ab0 + (32 * p + 16 * i) * 128);
+        af[i][1] = *reinterpret_cast<const Frag*>(buf + ab1 + (32 * p + 16 * i) * 128);
+      }
+      if (p == 0 && n1) dma_a(2, c1, gk + 1);
+      if (p == 1 && n1) dma_a(3, c1, gk + 1);
+      if (p == 2 && n2) { dma_b(0, c2, gk + 2); dma_b(1, c2, gk + 2); dma_a(0, c2, gk + 2); }
+      if (p == 3 && n2) { dma_b(2, c2, gk + 2); dma_b(3, c2, gk + 2); dma_a(1, c2, gk + 2); }
+      barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[2 * p + i][j] = mma16(bw[j][ks], af[i][ks], acc[2 * p + i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+    }
+  };
+  for (int gk = 0; gk < total; ++gk) {
+    ktile(gk, std::false_type{});
+    if (gk == 0) GPROBE(3);
+    if (gk == nk / 2) GPROBE(4);
+    if (gk == 2 * nk - 1) GPROBE(7);   // the second tile's last K tile done
+    if (cc.kt == nk - 1) {
+      // epilogue of tile cc.it: lane → row m0 + 128·wr + 16·mi + (lane & 15), columns
+      // n0 + 64·wc + 16·j + 4·(lane >> 4) + e; exactly S vector-memory operations per wave
+      if (cc.it == 0) GPROBE(5);
+      const int rb = cc.m0 + 128 * wr + (lane & 15);
+      const int cb = cc.n0 + 64 * wc + 4 * c0;
+      const float cs = cc.n0 < g.col_scale_n ? g.col_scale : 1.f;   // (col_scale_n % 256 == 0)
+      f32x4 b4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b4[j] = *reinterpret_cast<const f32x4*>(smem + BIAS_LDS + (cc.it & 1) * 1024 + (64 * wc + 4 * c0 + 16 * j) * 4);
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        const int m = rb + 16 * mi;
+        const long off = (long)min(m, g.M - 1) * g.ldc + cb;
+        f32x4 r4[4];
+        if constexpr ((EPI & E_RESID) != 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r4[j] = *reinterpret_cast<const f32x4*>(g.resid + off + 16 * j);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x4 v = acc[mi][j] + b4[j];
+          if (g.col_scale_n) v *= cs;
+          acc[mi][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr ((EPI & E_GELU) != 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gelu_t<T>(v[e]);
+          }
+          if constexpr ((EPI & E_RESID) != 0) v += r4[j];
+          if constexpr ((EPI & E_F32) != 0) {
+            float* dst = m < g.M ? reinterpret_cast<float*>(g.out) + off + 16 * j
+                                 : reinterpret_cast<float*>(wcb_pp_scratch + lane * 16);
+            *reinterpret_cast<f32x4*>(dst) = v;
+          } else {
+            typedef short s4 __attribute__((ext_vector_type(4)));
+            s4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = __builtin_bit_cast(short, DT<T>::fromf(v[e]));
+            T* dst = m < g.M ? reinterpret_cast<T*>(g.out) + off + 16 * j : reinterpret_cast<T*>(wcb_pp_scratch + lane * 16);
+            *reinterpret_cast<s4*>(dst) = o;
+          }
+        }
+      }
+      if (cc.it == 0) GPROBE(6);   // (issued, not drained)
+    }
+    cc = c1;
+    c1 = c2;
+    advance(c2);
+  }
+  if (wr == 0) barrier();   // balance the stagger
+}
+
+template <typename T, int EPI>
+static void launch_pp_e(const GemmArgs& g, hipStream_t s) {
+  constexpr int kLds = 2 * 65536 + 2048;   // two K-tile buffers + two tiles' bias
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<T, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+    attr_set = true;
+  }
+  const int tiles = ((g.M + 255) / 256) * (g.N / 256);
+  // one persistent workgroup per CU (LDS-bound); pp 3 (tools/gemm_probe): one tile per workgroup
+  const dim3 grid((unsigned)(g.pp == 3 ? tiles : std::min(tiles, 256)));
+  WCB_LAUNCH((gemm_pp_kernel<T, EPI>), grid, dim3(512), kLds, s, g);
+}
+
+// the ping-pong kernel where it covers the launch: 16-bit, N % 256 == 0, K % 64 == 0 (>= 128), plain
+// rows, epilogue (bias) / (bias) + GELU / (bias) + residual, f32 or T out, no clamp. g.pp 1 (runtime
+// default): where it measured at least as fast as the LDS-ring kernel; 2: every covered shape (tests,
+// microbenchmarks). tools/enc_bench.py: C2 (small) QKV 875 vs 868 TFLOP/s, fc1 880 vs 797; C3 (medium)
+// QKV 1007 vs 1008, out 697 vs 614, fc1 949 vs 888, fc2 1064 vs 1002
+template <typename T>
+static bool launch_pp(const GemmArgs& g, hipStream_t s) {
+  if constexpr (sizeof(T) != 2) {
+    return false;
+  } else {
+    if (g.N % 256 != 0 || g.N > 8192 || g.K % 64 != 0 || g.K < 128 || g.a_Mb || g.c_Mb || g.addrow || g.mode != 0 || g.clamp != 0.f ||
+        g.rst_out || g.out16 || g.M < 256 || (g.resid && !g.out_f32) || (g.resid && g.act) || g.col_scale_n % 256)
+      return false;
+    if (g.pp == 1) {   // where the LDS-ring kernel takes 256x192 tiles (d-wide N = 768: fewer tile rounds), it
+                       // measured faster (C2 out 99 vs 104 µs, fc2 271 vs 277 µs)
+      const long tm = (g.M + 255) / 256;
+      const long r256 = (tm * ((g.N + 255) / 256) + 255) / 256, r192 = (tm * ((g.N + 191) / 192) + 255) / 256;
+      if (g.N % 192 == 0 && r192 * 192 * 10 < r256 * 256 * 9) return false;
+    }
+    const int bits = (g.act == 1 ? E_GELU : 0) | (g.resid ? E_RESID : 0) | (g.out_f32 ? E_F32 : 0);
+    switch (bits) {
+      case 0: launch_pp_e<T, 0>(g, s); return true;
+      case E_GELU: launch_pp_e<T, E_GELU>(g, s); return true;
+      case E_F32: launch_pp_e<T, E_F32>(g, s); return true;
+      case E_RESID | E_F32: launch_pp_e<T, E_RESID | E_F32>(g, s); return true;
+      default: return false;
+    }
   }
 }
 
@@ -1684,6 +1999,7 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
   // d-wide out / fc2 (M = 48000, N = 768: 564 tiles = 2.2 rounds against 752 = 2.9), 12 % / 10 %
   // faster (tools/enc_gemm_bench.hip); QKV / fc1 keep 256x256 (192 measured 9 / 15 % slower)
   if constexpr (sizeof(T) == 2) {
+    if (g.pp && launch_pp<T>(g, s)) return;
     if (g.N % 128 == 0 && g.M >= 4096) {
       const long tm = (g.M + 255) / 256;
       const long r256 = (tm * ((g.N + 255) / 256) + 255) / 256, r192 = (tm * ((g.N + 191) / 192) + 255) / 256;

@@ -106,6 +106,11 @@ struct GemmArgs {
   // LDS-ring tiles (encoder GEMMs): tile order in bands of `raster` row panels, column tiles outer
   // within a band (0: row-major tile order)
   int raster = 0;
+  // 16-bit encoder GEMMs: the ping-pong kernel (gemm_impl.h gemm_pp_kernel) where it covers the launch
+  int pp = 0;
+  // output columns [0, col_scale_n) scaled by col_scale after the bias (the encoder's q pre-scaled by
+  // log2 e for the flash kernel's exp2 softmax); 0 = off
+  int col_scale_n = 0; float col_scale = 1.f;
   // lean QKV (mode 2, one position per row): the new token's self-attention in the same launch
   // (gemm_impl.h dec_lean_kernel SA): o_h → sa_att [M][sa_ld]; sa_cnt = the launch's arrival counters
   // ([row blocks][hs_H] ints, zeroed once at allocation, monotonic). Set only where the lean kernel takes
@@ -164,6 +169,7 @@ struct AttnArgs {
   int row0 = 0, b_div = 1;
   const int* phys = nullptr; long phys_ld = 0;
   int causal = 0;    // decode kernels, Sq > 1 (prefill): query i sees the first nkeys(+dev) + i keys
+  int q_log2 = 0;    // flash (encoder variant 6): q is pre-scaled by log2(e)
   int xcd_nqb = 0;   // flash, > 0: 1-D grid, the xcd_nqb query blocks of one (set, head) on one XCD
                      // (they share its K/V through that XCD's L2); requires B·H % 8 == 0
   int kv_rows = 0;   // > 0: K/V rows allocated per (row, head) — the one-token self-attention kernel

@@ -231,6 +231,9 @@ struct wcb_handle {
   // (GemmArgs::raster; 0 = row-major). 8 measured best with the round-3 ring kernel (whisper-small:
   // QKV 185 -> 177, fc1 297 -> 281, out 118 -> 116 us, fc2 within noise; profiles/r03f_enc_gemm_bench.txt)
   int enc_raster = 8;
+  // encoder GEMMs: the ping-pong kernel (option "enc_gemm" 1; gemm_impl.h gemm_pp_kernel) or the LDS-ring
+  // kernel (0)
+  int enc_gemm = 1;
   // decode projections on gemm_dec_kernel (K supported): the LayerNorm consumers compute their row
   // statistics from the rows they load, so the producers publish no per-16-column partial sums
   bool dec_gemm = false;
@@ -567,7 +570,7 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       REQUIRE(value >= 0 && value <= 3, "option xenc_variant: 0..3");
       h->xenc_variant = value;
     } else if (n == "enc_flash") {
-      REQUIRE(value == 2 || value == 4, "option enc_flash: 2 or 4");
+      REQUIRE(value == 2 || value == 4 || value == 5 || value == 6, "option enc_flash: 2, 4, 5 or 6");
       h->enc_flash_qw = value;
     } else if (n == "xenc_split") {
       REQUIRE(!h->ready, "option xenc_split: set before the weights are finalized");
@@ -608,6 +611,9 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       h->xenc_fm = value != 0;
     } else if (n == "xq_kq") {
       h->xq_kq = value != 0;
+    } else if (n == "enc_gemm") {
+      REQUIRE(value == 0 || value == 1, "option enc_gemm: 0 or 1");
+      h->enc_gemm = value;
     } else if (n == "enc_raster") {
       REQUIRE(value >= 0 && value <= 64, "option enc_raster: 0..64");
       h->enc_raster = value;
@@ -927,6 +933,7 @@ void dgemm(wcb_handle* h, const char* cls, const GemmArgs& g, hipStream_t st) {
 void run_gemm(wcb_handle* h, const char* cls, const GemmArgs& g0) {
   GemmArgs g = g0;
   g.raster = h->enc_raster;
+  g.pp = h->enc_gemm;
   h->timed(cls, 2.0 * g.M * g.N * g.K, 0.0, h->he, [&] { gemm(h->dt, g, h->he); });
 }
 
@@ -959,12 +966,17 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
     h->timed("layernorm", 0, M * d * (4.0 + e), h->he, [&] { layernorm(h->dt, h->x.as<float>(), w.ln1_w, w.ln1_b, h->h.p, (int)M, d, h->he); });
     GemmArgs q = rowgemm(h->h.p, d, w.qkv_w, (int)M, 3 * d, d, h->qkv.p, 3 * d);
     q.bias = w.qkv_b;
+    // enc_flash 6: q leaves the projection scaled by log2(e) (one rounding, in the epilogue) for the
+    // flash kernel's exp2 softmax
+    const bool ql2 = h->enc_flash_qw == 6 && h->dt != kF32;
+    if (ql2) { q.col_scale_n = d; q.col_scale = 1.4426950408889634f; }
     run_gemm(h, "enc_qkv", q);
     AttnArgs a;
     a.q = h->qkv.p; a.ldq = 3 * d; a.q_Sb = S; a.Sq = S;
     a.k = (char*)h->qkv.p + d * e; a.v = (char*)h->qkv.p + 2 * d * e;
     a.k_sb = (long)S * 3 * d; a.k_sh = 64; a.k_sk = 3 * d;
-    a.o = h->att.p; a.ldo = d; a.o_Sb = S; a.B = B; a.H = H; a.nkeys = S; a.variant = h->enc_flash_qw;
+    a.o = h->att.p; a.ldo = d; a.o_Sb = S; a.B = B; a.H = H; a.nkeys = S;
+    a.variant = h->dt == kF32 ? 4 : h->enc_flash_qw;   // (f32: the VALU kernel below)
     h->timed("enc_attn", 4.0 * B * H * (double)S * S * 64, 0, h->he, [&] {
       if (!attention_flash(h->dt, a, h->he)) attention_decode(h->dt, a, h->he);
     });
@@ -2067,17 +2079,25 @@ int wcb_profile_kernel(wcb_handle* h, int i, char* name, int cap, int64_t* grid)
 }
 
 // ------------------------------------------------------------------------------ kernel-level ops
-int wcb_op_gemm(int dtype, const void* A, const void* W, int M, int N, int K, const float* bias, int act,
-                const float* resid, void* out, int out_f32, void* stream) {
+int wcb_op_gemm_kernel(int dtype, const void* A, const void* W, int M, int N, int K, const float* bias, int act,
+                       const float* resid, void* out, int out_f32, int kernel, void* stream) {
   return guarded(nullptr, [&] {
     REQUIRE(A && W && out && M > 0 && N > 0 && K > 0, "bad argument");
     REQUIRE(N % 8 == 0, "N must be a multiple of 8");
     REQUIRE(K % (dtype == WCB_F32 ? 32 : 64) == 0, "K must be a multiple of the 128-byte K tile");
+    REQUIRE(kernel >= 0 && kernel <= 2, "kernel: 0, 1 or 2");
     GemmArgs g = rowgemm(A, K, W, M, N, K, out, N);
     g.bias = bias; g.act = act; g.resid = resid; g.out_f32 = out_f32;
+    g.raster = 8;
+    g.pp = kernel;
     gemm(DType(dtype), g, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
   });
+}
+
+int wcb_op_gemm(int dtype, const void* A, const void* W, int M, int N, int K, const float* bias, int act,
+                const float* resid, void* out, int out_f32, void* stream) {
+  return wcb_op_gemm_kernel(dtype, A, W, M, N, K, bias, act, resid, out, out_f32, 1, stream);
 }
 
 int wcb_op_gemm_ln(int dtype, const float* X, const float* ln_w, const float* ln_b, const float* stats,
@@ -2192,10 +2212,11 @@ int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, voi
     a.k = k; a.v = v; a.k_sb = (long)Sk * ld; a.k_sh = 64; a.k_sk = ld;
     a.o = o; a.ldo = ld; a.o_Sb = Sq; a.B = B; a.H = H; a.nkeys = Sk;
     const bool beam = flash >= 200 && flash <= 202;
-    if (flash == 1 || flash == 100 || beam || flash < 0) {
-      // 100: 64 queries per wave; 200 / 201 / 202: the beam kernel (keys split over the waves, Sq <= 16;
-      // 4 waves x 2 stages, 2 x 4, 2 x 5); -n: n key ranges + merge (Sq <= 16)
-      a.variant = flash == 100 ? 4 : beam ? 7 + (flash - 200) : 1;
+    if (flash == 1 || (flash >= 100 && flash <= 102) || beam || flash < 0) {
+      // 100: 64 queries per wave; 101: the same with P·V per query fragment (enc_flash 5); 102: q given
+      // pre-scaled by log2(e) (enc_flash 6); 200 / 201 / 202: the beam kernel (keys split over the waves,
+      // Sq <= 16; 4 waves x 2 stages, 2 x 4, 2 x 5); -n: n key ranges + merge (Sq <= 16)
+      a.variant = flash == 100 ? 4 : flash == 101 ? 5 : flash == 102 ? 6 : beam ? 7 + (flash - 200) : 1;
       REQUIRE(!beam || Sq <= 16, "the beam kernel takes at most 16 query rows per set");
       REQUIRE(dtype != WCB_F32, "flash attention needs a 16-bit dtype");
       static DevBuf fpart;
