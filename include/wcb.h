@@ -88,8 +88,8 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "ring_kt" 1/2      decode rows > 64: 64-deep K sub-tiles per LDS-ring stage of the projection tiles
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)
  *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave), 4 (64 queries, default),
- *                      5 (64 queries, P·V per query fragment; bit-identical to 4), 6 (64 queries, q
- *                      pre-scaled by log2 e in the QKV epilogue, scores relative to the running max)
+ *                      6 (64 queries, q pre-scaled by log2 e in the QKV epilogue, scores relative to the
+ *                      running max)
  *   "enc_raster" n     encoder GEMM tile order: bands of n row panels, column tiles outer (8, default;
  *                      0: row-major); bit-identical */
 int wcb_set_option(wcb_handle* h, const char* name, int value);
@@ -229,8 +229,8 @@ int wcb_op_layernorm(int dtype, const float* x, const float* w, const float* b, 
                      void* stream);
 /* o[B][Sq][H*64] = softmax(q kᵀ) v per head (q pre-scaled), k/v [B][Sk][H*64];
  * flash=1 selects the MFMA kernel (16-bit dtypes; Sq <= 16: the few-query form of beam search), 100 the
- * MFMA kernel with 64 queries per wave, 101 the same with P·V per query fragment, 102 the same with q
- * given pre-scaled by log2(e) (softmax in base 2), 200 / 201 / 202 (Sq <= 16) the beam kernel (the keys of a (set,
+ * MFMA kernel with 64 queries per wave, 102 the same with q given pre-scaled by log2(e) (softmax in
+ * base 2), 200 / 201 / 202 (Sq <= 16) the beam kernel (the keys of a (set,
  * head) split over its waves, merged in the workgroup: 4 waves x 2 LDS stages, 2 x 4, 2 x 5), -n (Sq <= 16)
  * the MFMA kernel over n key ranges merged in
  * fixed order; 0 the decode kernel; n >= 2 the decode kernel with n split-KV key chunks combined by the

@@ -492,17 +492,12 @@ void attention_decode(DType t, const AttnArgs& a, hipStream_t s) {
 // the arguments are ≤ 0 here and results below 2^-126 contribute nothing.
 // NS LDS stages (NS - 1 K/V tiles in flight behind the one being multiplied). 2 everywhere: a
 // third stage measured 3.6 % slower on the beam cross-attention (C3: 90.9 vs 87.7 µs per launch).
-// PIPE (encoder variant 5): every Vᵀ fragment of the tile is read up front and each query fragment's
-// P·V follows its own softmax, so the scores of query fragment i + 1 (MFMA) can issue beside the
-// softmax of fragment i (VALU): the two-phase form runs all 32 score MFMAs, then ~700 VALU
-// instructions with no MFMA beside them, then all 32 P·V MFMAs. Same MFMAs in the same order per
-// accumulator (bit-identical).
 // QL2 (encoder variant 6): q arrives pre-scaled by log2(e) (the QKV GEMM epilogue, GemmArgs::col_scale), and
 // the score accumulators start at -m (the running max of the query, log2 units), so the MFMA leaves
 // s - m and the softmax is exp2 straight off the accumulator (no per-score multiply-add). When a tile
 // raises some query's max (and always on a range's first tile) the wave subtracts the increase and
 // rescales, as the plain form does on every tile.
-template <typename T, int QW, int NS, bool PIPE = false, bool QL2 = false>
+template <typename T, int QW, int NS, bool QL2 = false>
 __global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnArgs a) {
   using Frag = typename DT<T>::frag;
   constexpr int QB = 4 * QW * 16;     // query rows per workgroup
@@ -594,15 +589,7 @@ __global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnAr
     const int kabs = (t_lo + kt) * 64;   // first key of this tile
     // scores and softmax of every query fragment first, then P·V with the Vᵀ fragments of one
     // 16-row dd block live at a time (read once, used by every query fragment): 8 VGPRs of Vᵀ instead
-    // of 32 keeps the kernel at 3 waves per SIMD. PIPE: all Vᵀ fragments now, P·V per query fragment.
-    Frag vf[PIPE ? 4 : 1][2];
-    if constexpr (PIPE) {
-#pragma unroll
-      for (int mf = 0; mf < 4; ++mf) {
-        vf[mf][0] = tr_frag<T>(vt_l, 0, mf * 2, lane);
-        vf[mf][1] = tr_frag<T>(vt_l, 32, mf * 2, lane);
-      }
-    }
+    // of 32 keeps the kernel at 3 waves per SIMD
     Frag pf[QW][2];
 #pragma unroll
     for (int qi = 0; qi < QW; ++qi) {
@@ -668,24 +655,15 @@ __global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnAr
       }
       pf[qi][0] = pack_p<T>(s[0], s[1]);
       pf[qi][1] = pack_p<T>(s[2], s[3]);
-      if constexpr (PIPE) {
-#pragma unroll
-        for (int mf = 0; mf < 4; ++mf) {
-          o[qi][mf] = mma16(vf[mf][0], pf[qi][0], o[qi][mf]);
-          o[qi][mf] = mma16(vf[mf][1], pf[qi][1], o[qi][mf]);
-        }
-      }
     }
-    if constexpr (!PIPE) {
-      // Vᵀ fragments (A operand of Oᵀ): rows = dd 16mf + (lane&15), k = keys (permuted)
+    // Vᵀ fragments (A operand of Oᵀ): rows = dd 16mf + (lane&15), k = keys (permuted)
 #pragma unroll
-      for (int mf = 0; mf < 4; ++mf) {
-        const Frag v0 = tr_frag<T>(vt_l, 0, mf * 2, lane), v1 = tr_frag<T>(vt_l, 32, mf * 2, lane);
+    for (int mf = 0; mf < 4; ++mf) {
+      const Frag v0 = tr_frag<T>(vt_l, 0, mf * 2, lane), v1 = tr_frag<T>(vt_l, 32, mf * 2, lane);
 #pragma unroll
-        for (int qi = 0; qi < QW; ++qi) {
-          o[qi][mf] = mma16(v0, pf[qi][0], o[qi][mf]);
-          o[qi][mf] = mma16(v1, pf[qi][1], o[qi][mf]);
-        }
+      for (int qi = 0; qi < QW; ++qi) {
+        o[qi][mf] = mma16(v0, pf[qi][0], o[qi][mf]);
+        o[qi][mf] = mma16(v1, pf[qi][1], o[qi][mf]);
       }
     }
   };
@@ -922,14 +900,13 @@ static void launch_flash(const AttnArgs& a, hipStream_t s) {
   } else {   // one key range (the key split is the few-query form only); XCD-grouped query blocks
     AttnArgs b = a;
     b.nsplit = 1;
-    const int qb = a.variant >= 4 && a.variant <= 6 ? 256 : 128, nqb = (a.Sq + qb - 1) / qb, BH = a.B * a.H;
+    const int qb = a.variant == 4 || a.variant == 6 ? 256 : 128, nqb = (a.Sq + qb - 1) / qb, BH = a.B * a.H;
     const bool xg = nqb > 1 && BH % 8 == 0;
     b.xcd_nqb = xg ? nqb : 0;
     const dim3 grid = xg ? dim3(nqb * BH) : dim3(nqb, BH);
     // encoder tilings (option enc_flash): 64 queries per wave (4, default) or 32 (2)
     if (a.variant == 4) WCB_LAUNCH((attn_flash_kernel<T, 4, 2>), grid, dim3(256), 0, s, b);
-    else if (a.variant == 5) WCB_LAUNCH((attn_flash_kernel<T, 4, 2, true>), grid, dim3(256), 0, s, b);
-    else if (a.variant == 6) WCB_LAUNCH((attn_flash_kernel<T, 4, 2, false, true>), grid, dim3(256), 0, s, b);
+    else if (a.variant == 6) WCB_LAUNCH((attn_flash_kernel<T, 4, 2, true>), grid, dim3(256), 0, s, b);
     else WCB_LAUNCH((attn_flash_kernel<T, 2, 2>), grid, dim3(256), 0, s, b);
   }
 }

@@ -570,7 +570,7 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       REQUIRE(value >= 0 && value <= 3, "option xenc_variant: 0..3");
       h->xenc_variant = value;
     } else if (n == "enc_flash") {
-      REQUIRE(value == 2 || value == 4 || value == 5 || value == 6, "option enc_flash: 2, 4, 5 or 6");
+      REQUIRE(value == 2 || value == 4 || value == 6, "option enc_flash: 2, 4 or 6");
       h->enc_flash_qw = value;
     } else if (n == "xenc_split") {
       REQUIRE(!h->ready, "option xenc_split: set before the weights are finalized");
@@ -2212,11 +2212,11 @@ int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, voi
     a.k = k; a.v = v; a.k_sb = (long)Sk * ld; a.k_sh = 64; a.k_sk = ld;
     a.o = o; a.ldo = ld; a.o_Sb = Sq; a.B = B; a.H = H; a.nkeys = Sk;
     const bool beam = flash >= 200 && flash <= 202;
-    if (flash == 1 || (flash >= 100 && flash <= 102) || beam || flash < 0) {
-      // 100: 64 queries per wave; 101: the same with P·V per query fragment (enc_flash 5); 102: q given
-      // pre-scaled by log2(e) (enc_flash 6); 200 / 201 / 202: the beam kernel (keys split over the waves,
-      // Sq <= 16; 4 waves x 2 stages, 2 x 4, 2 x 5); -n: n key ranges + merge (Sq <= 16)
-      a.variant = flash == 100 ? 4 : flash == 101 ? 5 : flash == 102 ? 6 : beam ? 7 + (flash - 200) : 1;
+    if (flash == 1 || flash == 100 || flash == 102 || beam || flash < 0) {
+      // 100: 64 queries per wave; 102: the same with q given pre-scaled by log2(e) (enc_flash 6);
+      // 200 / 201 / 202: the beam kernel (keys split over the waves, Sq <= 16; 4 waves x 2 stages, 2 x 4,
+      // 2 x 5); -n: n key ranges + merge (Sq <= 16)
+      a.variant = flash == 100 ? 4 : flash == 102 ? 6 : beam ? 7 + (flash - 200) : 1;
       REQUIRE(!beam || Sq <= 16, "the beam kernel takes at most 16 query rows per set");
       REQUIRE(dtype != WCB_F32, "flash attention needs a 16-bit dtype");
       static DevBuf fpart;
