@@ -27,29 +27,34 @@ __global__ void fill_bf16(bf* p, long n, unsigned seed, float scale) {
 }
 
 int main(int argc, char** argv) {
-  const int M = 48000;
   struct Shape { const char* name; int N, K, act; bool resid; };
-  const Shape shapes[] = {{"qkv", 2304, 768, 0, false}, {"out", 768, 768, 0, true}, {"fc1", 3072, 768, 1, false},
-                          {"fc2", 768, 3072, 0, true}};
+  const bool medium = argc > 3 && atoi(argv[3]) == 1;   // C3's whisper-medium encoder (64 clips)
+  const int M = medium ? 96000 : 48000;
+  const Shape small_shapes[] = {{"qkv", 2304, 768, 0, false}, {"out", 768, 768, 0, true}, {"fc1", 3072, 768, 1, false},
+                                {"fc2", 768, 3072, 0, true}};
+  const Shape medium_shapes[] = {{"qkv", 3072, 1024, 0, false}, {"out", 1024, 1024, 0, true},
+                                 {"fc1", 4096, 1024, 1, false}, {"fc2", 1024, 4096, 0, true}};
+  const Shape* shapes = medium ? medium_shapes : small_shapes;
   const int raster = argc > 1 ? atoi(argv[1]) : 8;
   const int pp = argc > 2 ? atoi(argv[2]) : 2;   // 2: persistent grid, 3: one tile per workgroup
   bf *A, *W;
   float *bias, *out;
-  CHK(hipMalloc(&A, (long)M * 3072 * 2));
-  CHK(hipMalloc(&W, 3072L * 3072 * 2));
-  CHK(hipMalloc(&bias, 3072 * 4));
-  CHK(hipMalloc(&out, (long)M * 3072 * 4));
-  CHK(hipMemset(bias, 0, 3072 * 4));
-  CHK(hipMemset(out, 0, (long)M * 3072 * 4));
-  fill_bf16<<<2048, 256>>>(A, (long)M * 3072, 1u, 1.f);
-  fill_bf16<<<2048, 256>>>(W, 3072L * 3072, 2u, 0.03f);
+  CHK(hipMalloc(&A, (long)M * 4096 * 2));
+  CHK(hipMalloc(&W, 4096L * 4096 * 2));
+  CHK(hipMalloc(&bias, 4096 * 4));
+  CHK(hipMalloc(&out, (long)M * 4096 * 4));
+  CHK(hipMemset(bias, 0, 4096 * 4));
+  CHK(hipMemset(out, 0, (long)M * 4096 * 4));
+  fill_bf16<<<2048, 256>>>(A, (long)M * 4096, 1u, 1.f);
+  fill_bf16<<<2048, 256>>>(W, 4096L * 4096, 2u, 0.03f);
   unsigned long long* probe;
   const int maxwg = 4096;
   CHK(hipMalloc(&probe, maxwg * 8 * 8));
   CHK(hipMemcpyToSymbol(HIP_SYMBOL(wcb_gemm_probe), &probe, sizeof(probe)));
   hipStream_t s;
   CHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  for (const Shape& sh : shapes) {
+  for (int si = 0; si < 4; ++si) {
+    const Shape& sh = shapes[si];
     GemmArgs g;
     g.A = A; g.lda = sh.K; g.W = W; g.ldw = sh.K; g.M = M; g.N = sh.N; g.K = sh.K;
     g.bias = bias; g.act = sh.act; g.out = out; g.ldc = sh.N; g.out_f32 = sh.resid ? 1 : 0;
@@ -76,6 +81,7 @@ int main(int argc, char** argv) {
       best = std::min(best, ms);
     }
     const int nwg = pp == 3 ? ((M + 255) / 256) * (sh.N / 256) : 256;
+    if (nwg * 8 > maxwg * 8) { printf("too many workgroups for the probe buffer\n"); continue; }
     std::vector<unsigned long long> h((size_t)nwg * 8);
     CHK(hipMemcpy(h.data(), probe, h.size() * 8, hipMemcpyDeviceToHost));
     const double us = best * 1e3 / 10;
