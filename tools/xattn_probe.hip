@@ -93,6 +93,50 @@ int main() {
     printf("  workgroup starts spread %llu cycles; first start -> last end %llu cycles\n", mx - mn, mx_end - mn);
     CHK(hipGraphExecDestroy(ge));
     CHK(hipGraphDestroy(g));
+    if (fm) {   // the range merge + W_v behind the fragment-major xattn (the runtime's pair)
+      unsigned short* wv;
+      float* bv;
+      unsigned short* o;
+      unsigned long long* mp;
+      CHK(hipMalloc(&wv, (long)D * D * 2));
+      CHK(hipMalloc(&bv, D * 4));
+      CHK(hipMalloc(&o, (long)rows * D * 2));
+      CHK(hipMalloc(&mp, 4096 * 8 * 8));
+      CHK(hipMemset(bv, 0, D * 4));
+      fill_rand<<<1024, 256>>>(wv, (long)D * D, 11u, 0.05f);
+      CHK(hipMemcpyToSymbol(HIP_SYMBOL(wcb_merge_probe), &mp, sizeof(mp)));
+      hipGraph_t g2;
+      hipGraphExec_t ge2;
+      CHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      for (int i = 0; i < 48; ++i) { xenc_attention(kBF16, a, s); xenc_merge_v(kBF16, a, wv, bv, o, D, s); }
+      CHK(hipStreamEndCapture(s, &g2));
+      CHK(hipGraphInstantiate(&ge2, g2, nullptr, nullptr, 0));
+      CHK(hipGraphLaunch(ge2, s));
+      CHK(hipStreamSynchronize(s));
+      float best2 = 1e30f;
+      for (int r = 0; r < 5; ++r) {
+        CHK(hipEventRecord(e0, s));
+        CHK(hipGraphLaunch(ge2, s));
+        CHK(hipEventRecord(e1, s));
+        CHK(hipEventSynchronize(e1));
+        float ms;
+        CHK(hipEventElapsedTime(&ms, e0, e1));
+        best2 = std::min(best2, ms);
+      }
+      const int nm = H * rows / 2;
+      std::vector<unsigned long long> hm((size_t)nm * 8);
+      CHK(hipMemcpy(hm.data(), mp, hm.size() * 8, hipMemcpyDeviceToHost));
+      printf("xattn + merge_v: %.2f us per pair (48 in a graph)\n", best2 * 1e3 / 48);
+      for (int k = 1; k <= 4; ++k) {
+        std::vector<long> d;
+        for (int w = 0; w < nm; ++w) d.push_back((long)(hm[w * 8 + k] - hm[w * 8 + k - 1]));
+        std::sort(d.begin(), d.end());
+        printf("  merge phase %d-%d: median %6ld p90 %6ld cycles\n", k - 1, k, d[d.size() / 2], d[d.size() * 9 / 10]);
+      }
+      unsigned long long mn = ~0ull, mx = 0;
+      for (int w = 0; w < nm; ++w) { mn = std::min(mn, hm[w * 8]); mx = std::max(mx, hm[w * 8 + 4]); }
+      printf("  merge: first start -> last end %llu cycles over %d workgroups\n", mx - mn, nm);
+    }
   }
   return 0;
 }

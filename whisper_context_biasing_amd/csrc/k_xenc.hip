@@ -44,8 +44,17 @@ constexpr int kXencCK = 32;   // keys per chunk
     if (threadIdx.x == 0)                                                                                \
       a.stamp.base[(blockIdx.y * gridDim.x + blockIdx.x) * 16 + (k)] = __builtin_amdgcn_s_memtime();     \
   } while (0)
+// ... and xenc_merge_v_kernel stamps (wave 0) into wcb_merge_probe[workgroup][8]: start (0), loads issued
+// (1), partials landed (2), range merge done (3), outputs stored (4)
+__device__ unsigned long long* wcb_merge_probe;
+#define MPROBE(k)                                                                                        \
+  do {                                                                                                   \
+    if (threadIdx.x == 0)                                                                                \
+      wcb_merge_probe[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (k)] = __builtin_amdgcn_s_memtime();   \
+  } while (0)
 #else
 #define XPROBE(k) do {} while (0)
+#define MPROBE(k) do {} while (0)
 #endif
 constexpr int kXencNW = 8;    // waves per workgroup
 
@@ -485,6 +494,7 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
   const int ns = a.nsplit;
   __shared__ float2 sv[RPW][MS];
   __shared__ __attribute__((aligned(16))) float us[RPW][D];
+  MPROBE(0);
   // weights first: pass p, output j = 16p + 4·wave + (lane >> 4), chunks (k·16 + (lane & 15))
   Frag wf[4][CPL];
 #pragma unroll
@@ -510,7 +520,9 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
     const float2 mlv = *reinterpret_cast<const float2*>(a.ml + (((long)b * ns + min(tid, ns - 1)) * a.H + h) * 2);
     if (tid < MS) sv[r][tid] = tid < ns ? mlv : float2{0.f, 0.f};
   }
+  MPROBE(1);
   __syncthreads();
+  MPROBE(2);
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     float2 v[MS];
@@ -537,6 +549,7 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
     if (tid * 4 < D) *reinterpret_cast<f32x4*>(&us[r][c]) = acc;
   }
   __syncthreads();
+  MPROBE(3);
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     const int b = blockIdx.y * RPW + r;
@@ -564,6 +577,10 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
       }
     }
   }
+#ifdef WCB_XENC_PROBE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  MPROBE(4);
+#endif
 }
 
 // The encoder output [B][S][D] → the fragment-major chunk layout of attn_xenc_reg_kernel<.., FM>:
