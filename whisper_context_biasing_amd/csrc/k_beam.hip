@@ -3,7 +3,7 @@
 // ([tf] utils.py:3388-3389). Oracle: oracle/beam_np.py.
 //
 // Rows r = b·nb + i (utterance b, running beam i). Per decode step:
-//   beam_topk_kernel  one workgroup per row over the f32 logits row: log_softmax (max, Σexp), the
+//   beam_topk_kernel  one workgroup (4-16 waves) per row over the f32 logits row: log_softmax (max, Σexp), the
 //                     boost (lam·(k - d + root bit) on the vocabulary, the exact lam·n(s, v) on the
 //                     tokens of trans(state), which an LDS bitmap excludes from the vocabulary
 //                     pass; oracle/bias_ref.py) and EOS mask, plus the
@@ -20,6 +20,8 @@
 // elements per row; the self-attention kernel reads each key through the map.
 #include "common.h"
 #include "kernels.h"
+
+#include <type_traits>
 
 namespace wcb {
 
@@ -38,19 +40,25 @@ WCB_DEV int ac_delta(const BeamArgs& a, int s, int tok) {
   return c >= 0 ? c : 0;
 }
 
-WCB_DEV float block_max4(float v, float* red) {
+template <int NW>
+WCB_DEV float block_max(float v, float* red) {
   v = wave_max(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  const float r = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float r = red[0];
+#pragma unroll
+  for (int q = 1; q < NW; ++q) r = fmaxf(r, red[q]);
   __syncthreads();
   return r;
 }
-WCB_DEV float block_sum4(float v, float* red) {
+template <int NW>
+WCB_DEV float block_sum(float v, float* red) {
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  const float r = (red[0] + red[1]) + (red[2] + red[3]);
+  float r = red[0];
+#pragma unroll
+  for (int q = 1; q < NW; ++q) r += red[q];
   __syncthreads();
   return r;
 }
@@ -74,22 +82,24 @@ __global__ __launch_bounds__(256) void beam_init_kernel(BeamArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
+// NT threads per row (16 waves when the rows leave CUs idle: one wave per SIMD cannot hide the
+// serial compare-exchange chain of a list insert, which every element of a wave pays when any lane
+// inserts), KL = the per-thread list length (K rounded up: the chain is KL steps long)
+template <int NT, int KL>
+__global__ __launch_bounds__(NT) void beam_topk_kernel(BeamArgs a) {
+  constexpr int NW = NT / 64;
   if (*a.all_done) return;                    // frozen once the search has stopped
   __shared__ uint32_t bits[kBitWords];
   __shared__ uint32_t tbits[kBitWords];       // tokens of trans(state): scored in their own pass
-  __shared__ float red[4];
-  __shared__ float cv[256][kTopK + 1];
-  __shared__ int ci[256][kTopK + 1];
-  __shared__ float wv[4];
-  __shared__ int wi[4], wt[4];
+  __shared__ float red[NW];
+  __shared__ float wv[NW];
+  __shared__ int wi[NW], wt[NW];
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float* row = a.logits + (long)r * a.ld;
-  // the row as float4 (a.ld is a multiple of 4: the padded vocabulary), UB loads in flight per lane:
-  // a plain strided loop keeps one load per lane in flight and pays the cache latency per element
+  // the row as float4 (a.ld is a multiple of 4: the padded vocabulary), UB loads in flight per lane
   const f32x4* row4 = reinterpret_cast<const f32x4*>(row);
   const int V4 = a.V >> 2;
-  constexpr int UB = 8;
+  constexpr int UB = 4;
   auto load4 = [&](int i) -> f32x4 {   // float4 i of the row, -inf past the vocabulary
     if (i < V4) return row4[i];
     f32x4 x;
@@ -98,37 +108,34 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
     return x;
   };
   const int n4 = (a.V + 3) >> 2;
-  // one pass for max and Σexp (per lane: a running max, the sum rescaled when a batch raises it);
-  // UB2 float4 loads in flight per lane: one workgroup per row, so the row's read is latency-bound
-  // on the loads each lane keeps in flight (C5: 80 rows = 80 workgroups)
-  constexpr int UB2 = 8;
+  // one pass for max and Σexp (per lane: a running max, the sum rescaled when a batch raises it)
   float m = -INFINITY, s = 0.f;
-  for (int i0 = tid; i0 < n4; i0 += 256 * UB2) {
-    f32x4 x[UB2];
+  for (int i0 = tid; i0 < n4; i0 += NT * UB) {
+    f32x4 x[UB];
 #pragma unroll
-    for (int u = 0; u < UB2; ++u) x[u] = i0 + u * 256 < n4 ? load4(i0 + u * 256) : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int u = 0; u < UB; ++u) x[u] = i0 + u * NT < n4 ? load4(i0 + u * NT) : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     float bm = m;
 #pragma unroll
-    for (int u = 0; u < UB2; ++u) bm = fmaxf(bm, fmaxf(fmaxf(x[u][0], x[u][1]), fmaxf(x[u][2], x[u][3])));
+    for (int u = 0; u < UB; ++u) bm = fmaxf(bm, fmaxf(fmaxf(x[u][0], x[u][1]), fmaxf(x[u][2], x[u][3])));
     if (bm > m) { s = m == -INFINITY ? 0.f : s * expf(m - bm); m = bm; }
     if (m == -INFINITY) continue;
 #pragma unroll
-    for (int u = 0; u < UB2; ++u)
+    for (int u = 0; u < UB; ++u)
 #pragma unroll
       for (int e = 0; e < 4; ++e) s += expf(x[u][e] - m);
   }
-  const float mrow = block_max4(m, red);
+  const float mrow = block_max<NW>(m, red);
   s = m == -INFINITY ? 0.f : s * expf(m - mrow);   // lane sums onto the row max
   m = mrow;
-  const float lsum = logf(block_sum4(s, red));
+  const float lsum = logf(block_sum<NW>(s, red));
   const bool boost = a.lam != 0.f;
   const int st = a.state[r];
   int rb = 0, sd = 0, sk = 0;
   if (boost) {
     const int nw = (a.V + 31) >> 5;
-    for (int k = tid; k < nw; k += 256) { bits[k] = a.root_bits[k]; tbits[k] = 0u; }
+    for (int k = tid; k < nw; k += NT) { bits[k] = a.root_bits[k]; tbits[k] = 0u; }
     __syncthreads();
-    for (int t = a.trans_off[st] + tid; t < a.trans_off[st + 1]; t += 256) {
+    for (int t = a.trans_off[st] + tid; t < a.trans_off[st + 1]; t += NT) {
       const int v = a.trans_tok[t];
       atomicOr(&tbits[v >> 5], 1u << (v & 31));
     }
@@ -139,16 +146,16 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
   }
   const bool mask_eos = *a.step < a.min_new;
   const float rsc = a.run_sc[r];
-  float lv[kTopK];
-  int li[kTopK];
+  float lv[KL];
+  int li[KL];
 #pragma unroll
-  for (int k = 0; k < kTopK; ++k) { lv[k] = -INFINITY; li[k] = 0x7fffffff; }
+  for (int k = 0; k < KL; ++k) { lv[k] = -INFINITY; li[k] = 0x7fffffff; }
   auto insert = [&](float x, int v) {
-    if (beam_better(x, v, lv[kTopK - 1], li[kTopK - 1])) {
+    if (beam_better(x, v, lv[KL - 1], li[KL - 1])) {
       float pv = x;
       int pi = v;
 #pragma unroll
-      for (int k = 0; k < kTopK; ++k) {
+      for (int k = 0; k < KL; ++k) {
         if (beam_better(pv, pi, lv[k], li[k])) {
           const float tv = lv[k];
           const int ti = li[k];
@@ -157,15 +164,15 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
       }
     }
   };
-  for (int i0 = tid; i0 < n4; i0 += 256 * UB) {
+  for (int i0 = tid; i0 < n4; i0 += NT * UB) {
     f32x4 xs[UB];
 #pragma unroll
-    for (int u = 0; u < UB; ++u) xs[u] = i0 + u * 256 < n4 ? load4(i0 + u * 256) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < UB; ++u) xs[u] = i0 + u * NT < n4 ? load4(i0 + u * NT) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < UB; ++u)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int v = 4 * (i0 + u * 256) + e;
+        const int v = 4 * (i0 + u * NT) + e;
         if (v >= a.V) continue;
         float x = (xs[u][e] - m) - lsum;                               // log_softmax
         if (boost) {                                                   // bias boost processor
@@ -177,7 +184,7 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
       }
   }
   if (boost) {   // trans(state): the exact n(s, v) = d' - d + min(k, d + 1 - d')
-    for (int t = a.trans_off[st] + tid; t < a.trans_off[st + 1]; t += 256) {
+    for (int t = a.trans_off[st] + tid; t < a.trans_off[st + 1]; t += NT) {
       const int v = a.trans_tok[t];
       const int d2 = a.st_depth[a.trans_dst[t]];
       float x = bias_bonus((row[v] - m) - lsum, a.lam, d2 - sd + min(sk, sd + 1 - d2));
@@ -185,13 +192,13 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
       insert(x + rsc, v);
     }
   }
-#pragma unroll
-  for (int k = 0; k < kTopK; ++k) { cv[tid][k] = lv[k]; ci[tid][k] = li[k]; }
   int head = 0;
-  __syncthreads();
   for (int k = 0; k < a.K; ++k) {   // K rounds: block argmax over the threads' list heads
-    float hv = head < kTopK ? cv[tid][head] : -INFINITY;
-    int hi = head < kTopK ? ci[tid][head] : 0x7fffffff;
+    float hv = -INFINITY;
+    int hi = 0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < KL; ++q)
+      if (q == head) { hv = lv[q]; hi = li[q]; }
     int ht = tid;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -204,7 +211,7 @@ __global__ __launch_bounds__(256) void beam_topk_kernel(BeamArgs a) {
     float bv = wv[0];
     int bi = wi[0], bt = wt[0];
 #pragma unroll
-    for (int q = 1; q < 4; ++q)
+    for (int q = 1; q < NW; ++q)
       if (beam_better(wv[q], wi[q], bv, bi)) { bv = wv[q]; bi = wi[q]; bt = wt[q]; }
     if (tid == bt) ++head;
     // an all-NaN row leaves bi = INT_MAX: keep the candidate index inside the vocabulary
@@ -389,7 +396,18 @@ void beam_init(const BeamArgs& a, hipStream_t s) {
   WCB_LAUNCH(beam_init_kernel, dim3(a.B * a.nb), dim3(256), 0, s, a);
 }
 void beam_select(const BeamArgs& a, hipStream_t s) {
-  WCB_LAUNCH(beam_topk_kernel, dim3(a.B * a.nb), dim3(256), 0, s, a);
+  // 16 waves per row while the rows fit one per CU (C5: 80 rows), 8 up to two per CU (C3: 320)
+  const int rows = a.B * a.nb;
+  auto topk = [&](auto kl) {
+    constexpr int KL = decltype(kl)::value;
+    if (rows <= 256) WCB_LAUNCH((beam_topk_kernel<1024, KL>), dim3(rows), dim3(1024), 0, s, a);
+    else if (rows <= 1024) WCB_LAUNCH((beam_topk_kernel<512, KL>), dim3(rows), dim3(512), 0, s, a);
+    else WCB_LAUNCH((beam_topk_kernel<256, KL>), dim3(rows), dim3(256), 0, s, a);
+  };
+  if (a.K <= 4) topk(std::integral_constant<int, 4>{});
+  else if (a.K <= 8) topk(std::integral_constant<int, 8>{});
+  else if (a.K <= 12) topk(std::integral_constant<int, 12>{});
+  else topk(std::integral_constant<int, 16>{});
   WCB_LAUNCH(beam_step_kernel, dim3(a.B), dim3(256), 0, s, a);
 }
 void beam_output(const BeamArgs& a, hipStream_t s) {
