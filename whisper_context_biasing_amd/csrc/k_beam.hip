@@ -94,6 +94,8 @@ __global__ __launch_bounds__(NT) void beam_topk_kernel(BeamArgs a) {
   __shared__ float red[NW];
   __shared__ float wv[NW];
   __shared__ int wi[NW], wt[NW];
+  __shared__ float thr_v;
+  __shared__ int thr_i;
   const int r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float* row = a.logits + (long)r * a.ld;
   // the row as float4 (a.ld is a multiple of 4: the padded vocabulary), UB loads in flight per lane
@@ -164,34 +166,67 @@ __global__ __launch_bounds__(NT) void beam_topk_kernel(BeamArgs a) {
       }
     }
   };
-  for (int i0 = tid; i0 < n4; i0 += NT * UB) {
-    f32x4 xs[UB];
+  // the row's scores, f(score, token) per element: the vocabulary pass, then trans(state)
+  auto scan = [&](auto&& f) {
+    for (int i0 = tid; i0 < n4; i0 += NT * UB) {
+      f32x4 xs[UB];
 #pragma unroll
-    for (int u = 0; u < UB; ++u) xs[u] = i0 + u * NT < n4 ? load4(i0 + u * NT) : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int u = 0; u < UB; ++u) xs[u] = i0 + u * NT < n4 ? load4(i0 + u * NT) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < UB; ++u)
+      for (int u = 0; u < UB; ++u)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int v = 4 * (i0 + u * NT) + e;
-        if (v >= a.V) continue;
-        float x = (xs[u][e] - m) - lsum;                               // log_softmax
-        if (boost) {                                                   // bias boost processor
-          if ((tbits[v >> 5] >> (v & 31)) & 1u) continue;              // scored below
-          x = bias_bonus(x, a.lam, rb + (int)((bits[v >> 5] >> (v & 31)) & 1u));
+        for (int e = 0; e < 4; ++e) {
+          const int v = 4 * (i0 + u * NT) + e;
+          if (v >= a.V) continue;
+          float x = (xs[u][e] - m) - lsum;                               // log_softmax
+          if (boost) {                                                   // bias boost processor
+            if ((tbits[v >> 5] >> (v & 31)) & 1u) continue;              // scored below
+            x = bias_bonus(x, a.lam, rb + (int)((bits[v >> 5] >> (v & 31)) & 1u));
+          }
+          if (mask_eos && v == a.eos) x = -INFINITY;                     // MinNewTokens processor
+          f(x + rsc, v);                                                 // + running beam score
         }
-        if (mask_eos && v == a.eos) x = -INFINITY;                     // MinNewTokens processor
-        insert(x + rsc, v);                                            // + running beam score
-      }
-  }
-  if (boost) {   // trans(state): the exact n(s, v) = d' - d + min(k, d + 1 - d')
-    for (int t = a.trans_off[st] + tid; t < a.trans_off[st + 1]; t += NT) {
-      const int v = a.trans_tok[t];
-      const int d2 = a.st_depth[a.trans_dst[t]];
-      float x = bias_bonus((row[v] - m) - lsum, a.lam, d2 - sd + min(sk, sd + 1 - d2));
-      if (mask_eos && v == a.eos) x = -INFINITY;
-      insert(x + rsc, v);
     }
+    if (boost) {   // trans(state): the exact n(s, v) = d' - d + min(k, d + 1 - d')
+      for (int t = a.trans_off[st] + tid; t < a.trans_off[st + 1]; t += NT) {
+        const int v = a.trans_tok[t];
+        const int d2 = a.st_depth[a.trans_dst[t]];
+        float x = bias_bonus((row[v] - m) - lsum, a.lam, d2 - sd + min(sk, sd + 1 - d2));
+        if (mask_eos && v == a.eos) x = -INFINITY;
+        f(x + rsc, v);
+      }
+    }
+  };
+  // Threshold (when K <= NW): the K-th best of the NW wave maxima. They are K distinct elements at or
+  // above it, so the row's top-K is too, and the list pass inserts only elements at or above it: a
+  // few per wave instead of a serial insert chain on nearly every element. The top-K is unchanged.
+  float tv = -INFINITY;
+  int ti = 0x7fffffff;
+  if (NW >= 8 && a.K <= NW) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    scan([&](float x, int v) { if (beam_better(x, v, bv, bi)) { bv = x; bi = v; } });
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (beam_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) { wv[w] = bv; wi[w] = bi; }
+    if (tid == 0) { thr_v = -INFINITY; thr_i = 0x7fffffff; }
+    __syncthreads();
+    if (tid < NW) {   // the wave maximum of rank K - 1 (NaN-free maxima are distinct elements)
+      bv = wv[tid];
+      bi = wi[tid];
+      int rank = 0;
+      for (int j = 0; j < NW; ++j) rank += beam_better(wv[j], wi[j], bv, bi) ? 1 : 0;
+      if (rank == a.K - 1) { thr_v = bv; thr_i = bi; }
+    }
+    __syncthreads();
+    tv = thr_v;
+    ti = thr_i;
   }
+  scan([&](float x, int v) { if (!beam_better(tv, ti, x, v)) insert(x, v); });
   int head = 0;
   for (int k = 0; k < a.K; ++k) {   // K rounds: block argmax over the threads' list heads
     float hv = -INFINITY;
