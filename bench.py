@@ -7,10 +7,16 @@ SURVEY.md §8(d) benchmark mode) with the fused bias-list boost (1000 phrases, l
 Default workload = config C2: whisper-small, batch 32 per GPU, bf16 (random-init weights of that
 architecture; no checkpoint offline).
 
-Multi-GPU (`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`): one process
-per GPU, utterances sharded (weak scaling: 32 clips per GPU), weights generated on rank 0 and
-broadcast once over RCCL/xGMI (`dist.broadcast`), no collective in the timed region besides the
-barriers; time = max over ranks.
+Multi-GPU: one process per GPU, utterances sharded (weak scaling: 32 clips per GPU), weights
+generated on rank 0 and broadcast once over RCCL/xGMI (`dist.broadcast`), no collective in the
+timed region besides the barriers; time = max over ranks. Two ways in:
+  * `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N` (WORLD_SIZE set: this
+    process is one rank);
+  * `python bench.py --gpus N` (WORLD_SIZE unset): this process is only a launcher — it starts N
+    rank processes of itself before anything touches the GPU (it never initialises HIP), forwards
+    rank 0's JSON line and exits non-zero when any rank fails (the others are then stopped).
+`--backend nccl` (default: RCCL, rank r on GPU r) or `gloo` (ranks may share a GPU: rank r on GPU
+r mod the device count — how the N>1 path is exercised on a one-GPU box).
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus `roofline` (dominant kernel:
 the kernel symbol with the most device time per step, grouped as rocprofv3 --stats groups them, from
@@ -162,9 +168,73 @@ def _config_tag(args, world):
     return ("C4" if world > 1 else "C2") if args.model == "small" else "greedy"
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(cmd, n, env_extra=None, grace_s=15.0, poll_s=0.2):
+    """Run `n` rank processes of `cmd` (one per GPU) and wait for them. Each gets RANK / LOCAL_RANK /
+    WORLD_SIZE / LOCAL_WORLD_SIZE and a 127.0.0.1 rendezvous (MASTER_ADDR / MASTER_PORT), as
+    torch.distributed.run would set them. Rank 0's stdout is forwarded line by line and its last
+    JSON line kept; the other ranks inherit stdout / stderr. When a rank exits non-zero the others
+    are terminated (SIGTERM, SIGKILL after `grace_s`) — by the PIDs started here, never by pattern.
+    Returns (exit code, rank 0's last JSON line or None): 0 only when every rank exited 0 and rank 0
+    printed a JSON line. This process starts no GPU work of its own."""
+    import subprocess
+    import threading
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+                WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), **(env_extra or {}))
+    procs, last_json = [], [None]
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else None, text=True))
+
+    def pump():   # rank 0's stdout → ours
+        for line in procs[0].stdout:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+            s = line.strip()
+            if s.startswith("{") and s.endswith("}"):
+                last_json[0] = s
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            log(f"launcher: a rank exited with {rc}; stopping the others")
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            t_end = time.time() + grace_s
+            for p in procs:
+                try:
+                    p.wait(timeout=max(0.1, t_end - time.time()))
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(poll_s)
+    th.join(timeout=5.0)
+    if rc == 0 and last_json[0] is None:
+        log("launcher: rank 0 printed no JSON line")
+        rc = 1
+    return (rc if rc >= 0 else 128 - rc), last_json[0]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process group for N > 1 ranks: nccl (RCCL over xGMI, one GPU per rank) or gloo "
+                         "(ranks may share a GPU: rank r on GPU r mod the device count)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="small")
@@ -187,6 +257,12 @@ def main():
     ap.add_argument("--no-overlap", action="store_true",
                     help="serialise batches (default: batch i+1's front end + encoder overlap batch i's decode)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launcher: N fresh rank processes of this script, started before anything here touches the GPU
+        rc, _ = launch_ranks([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], args.gpus)
+        sys.exit(rc)
     if args.reference_mode:
         args.new_tokens, args.boost, args.no_overlap, args.no_cpu_baseline = 225, 0.0, True, True
     min_new = 0 if args.reference_mode else args.new_tokens   # benchmark mode: EOS masked, fixed length
@@ -203,10 +279,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    if args.backend == "nccl" and world > 1 and local >= ndev:
+        raise SystemExit(f"bench.py: rank {rank} (local {local}) needs GPU {local} but {ndev} are visible; "
+                         f"nccl takes one GPU per rank (--backend gloo lets ranks share one)")
+    gpu = local % ndev
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    devices_used = min(world, ndev)
 
     dims = get_dims(args.model)
     # ---- weights: rank 0 generates, one RCCL broadcast of the packed bf16 blob over xGMI
@@ -216,7 +303,7 @@ def main():
         torch.cuda.synchronize()
         log(f"rank {rank}: weights broadcast in {time.perf_counter() - t0:.3f} s")
     opts = {k: int(v) for k, v in (o.split("=", 1) for o in args.opt)}
-    model = WhisperCB.from_state_dict(dims, sd, dtype=args.dtype, device=local, options=opts or None)
+    model = WhisperCB.from_state_dict(dims, sd, dtype=args.dtype, device=gpu, options=opts or None)
     del sd
 
     B = args.batch
@@ -462,6 +549,7 @@ def main():
                                     f"greedy decode to natural EOS, max_length=225, no boost "
                                     f"(scripts/evaluation.py:173-179); batches serialised"),
                        "num_beams": args.num_beams, "global_batch": world * B, "parallelism": f"utterance-dp{world}",
+                       "collective_backend": args.backend if world > 1 else None, "devices_used": devices_used,
                        "hipgraph_decode": use_graph, "batches_in_flight": 3 if overlap else 1},
             "rtf": round(1.0 / (value / world), 6),
             "roofline": roof,

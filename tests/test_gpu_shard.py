@@ -54,6 +54,26 @@ def _worker(rank, world, port, outdir, name):
     dist.destroy_process_group()
 
 
+def test_bench_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with no torch.distributed.run: the launcher starts two ranks (gloo,
+    both on this box's GPU), each decodes its 32 clips, rank 0 prints the whole-job line."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "-u", os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2",
+                        "--warmup", "1", "--no-cpu-baseline", "--no-profile", "--backend", "gloo"],
+                       capture_output=True, text=True, timeout=900, env=env)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [s for s in p.stdout.splitlines() if s.strip().startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "utterance-dp2"
+    assert out["config"]["global_batch"] == 64 and out["config"]["collective_backend"] == "gloo"
+    assert out["value"] > 0 and out["steps"] == 2
+
+
 @pytest.mark.parametrize("name", ["tiny.en", "small"])
 def test_two_rank_shards_equal_single_process(tmp_path, name):
     from whisper_context_biasing_amd.config import get_dims

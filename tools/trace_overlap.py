@@ -1,13 +1,17 @@
 """Concurrency analysis of a rocprofv3 kernel trace: per queue, busy time (union of its kernels'
 intervals) and the time during which >= 2 queues are busy at once, over a window.
-  python tools/trace_overlap.py run_kernel_trace.csv [t_skip_ms]"""
+  python tools/trace_overlap.py run_kernel_trace.csv [t_skip_ms]
+(a negative t_skip_ms keeps only the last |t_skip_ms| ms of the trace)"""
 import csv
 import sys
 from collections import defaultdict
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 skip = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0
-t0 = min(int(r["Start_Timestamp"]) for r in rows) + skip * 1e6
+if skip >= 0:
+    t0 = min(int(r["Start_Timestamp"]) for r in rows) + skip * 1e6
+else:
+    t0 = max(int(r["End_Timestamp"]) for r in rows) + skip * 1e6
 ev = defaultdict(list)
 for r in rows:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])

@@ -234,6 +234,9 @@ struct wcb_handle {
   // encoder GEMMs: the ping-pong kernel (option "enc_gemm" 1; gemm_impl.h gemm_pp_kernel) or the LDS-ring
   // kernel (0)
   int enc_gemm = 1;
+  // encoder stream CU reservation (option "enc_cu_reserve"): 1/n of the CUs kept free of encoder work so
+  // the decode chains of the batches in flight always find CUs (0: none)
+  int enc_cu_reserve = 0;
   // decode projections on gemm_dec_kernel (K supported): the LayerNorm consumers compute their row
   // statistics from the rows they load, so the producers publish no per-16-column partial sums
   bool dec_gemm = false;
@@ -604,6 +607,25 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
           HIPCHK(hipStreamCreateWithPriority(&D.hs, hipStreamNonBlocking, prio_hi));
         }
       }
+    } else if (n == "enc_cu_reserve") {
+      // the encoder stream on a CU mask that leaves 1/value of the CUs (logical CU bits i with
+      // (i >> 3) % value == value - 1: spread over every XCD whether the driver stripes mask bits over
+      // the XCDs or not) to the decode chains; 0: every CU
+      REQUIRE(value == 0 || (value >= 2 && value <= 32), "option enc_cu_reserve: 0 or 2..32");
+      quiesce(h);
+      HIPCHK(hipStreamDestroy(h->he));
+      h->he = nullptr;
+      if (value) {
+        int ncu = 0;
+        HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int cu = 0; cu < ncu; ++cu)
+          if ((cu >> 3) % value != value - 1) mask[cu / 32] |= 1u << (cu % 32);
+        HIPCHK(hipExtStreamCreateWithCUMask(&h->he, (uint32_t)mask.size(), mask.data()));
+      } else {
+        HIPCHK(hipStreamCreateWithPriority(&h->he, hipStreamNonBlocking, 0));
+      }
+      h->enc_cu_reserve = value;
     } else if (n == "steps_per_graph") {
       REQUIRE(value >= 1 && value <= 64, "option steps_per_graph: 1..64");
       h->steps_per_graph = value;

@@ -66,20 +66,30 @@ def broadcast_weights(dims: WhisperDims, device: torch.device, seed: int = 0, sr
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     n_el = sum(int(np.prod(s)) for _, s in param_shapes(dims))
+    # gloo moves host tensors: the blob crosses on the CPU and lands on `device` afterwards
+    comm = _comm_device(device)
     if rank == src:
-        flat = pack_state_dict(dims, make_weights(dims, seed=seed), dtype).to(device)
+        flat = pack_state_dict(dims, make_weights(dims, seed=seed), dtype).to(comm)
     else:
-        flat = torch.empty(n_el, dtype=dtype, device=device)
+        flat = torch.empty(n_el, dtype=dtype, device=comm)
     if world > 1:
         dist.broadcast(flat, src=src)
+    flat = flat.to(device)
     return unpack_state_dict_views(dims, flat) if views else unpack_state_dict(dims, flat)
+
+
+def _comm_device(device: torch.device) -> torch.device:
+    """Where a collective's tensors must live: the rank's GPU under nccl (RCCL), the host under gloo."""
+    if dist.is_initialized() and dist.get_backend() == "gloo":
+        return torch.device("cpu")
+    return torch.device(device)
 
 
 def max_over_ranks(value: float, device: torch.device) -> float:
     """The slowest rank's time (bench.py reports whole-job throughput against it)."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return float(value)
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device=_comm_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -95,6 +105,7 @@ def gather_shards(local: torch.Tensor, device: torch.device, pad_value: int) -> 
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return [local]
     world = dist.get_world_size()
+    device = _comm_device(device)
     one_d = local.dim() == 1
     local = local.reshape(local.shape[0], -1) if one_d else local
     shp = torch.tensor([local.shape[0], local.shape[1] if local.dim() > 1 else 1], dtype=torch.int64, device=device)
