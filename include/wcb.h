@@ -82,14 +82,11 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "decode_contexts" n  decode contexts in flight (1..4): calls decode on n streams from n buffers (4 is
  *                      refused while a step-wise decode owns context 3)
  *   "steps_per_graph" n  decode steps captured per replayed hipGraph (1..64, default 8)
- *   "decode_cu_split" 0/1  decode context k's stream on CU half k % 2 (CU-masked streams; 0: all CUs, default)
  *   "xenc_fm" 0/1      greedy encoder-space cross-attention reads the encoder output in the fragment-major chunk
  *                      layout (1, default; 1 KiB contiguous per load wave-instruction) or the row layout (0)
  *   "ring_kt" 1/2      decode rows > 64: 64-deep K sub-tiles per LDS-ring stage of the projection tiles
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)
- *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave), 4 (64 queries, default),
- *                      6 (64 queries, q pre-scaled by log2 e in the QKV epilogue, scores relative to the
- *                      running max)
+ *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave), 4 (64 queries, default)
  *   "enc_raster" n     encoder GEMM tile order: bands of n row panels, column tiles outer (8, default;
  *                      0: row-major); bit-identical */
 int wcb_set_option(wcb_handle* h, const char* name, int value);

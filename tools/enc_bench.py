@@ -33,7 +33,6 @@ if __name__ == "__main__":
     only = sys.argv[1] if len(sys.argv) > 1 else ""
     if only in ("", "attn"):
         attn_case(32, 12, 1500, 1500, 100)
-        attn_case(32, 12, 1500, 1500, 102)
         attn_case(32, 12, 1500, 1500, 1)
     shapes = [(48000, 2304, 768, 0, False), (48000, 768, 768, 0, True),
               (48000, 3072, 768, 1, False), (48000, 768, 3072, 0, True)]

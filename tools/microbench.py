@@ -115,6 +115,6 @@ if __name__ == "__main__":
     attn_case(16, 12, 1, 1500, 0)
     attn_case(16, 12, 1, 1500, 4)
     attn_case(32, 12, 1, 64, 0)
-    for code in (1, 100, 123, 124):   # encoder tilings (option enc_flash)
+    for code in (1, 100):   # encoder tilings (option enc_flash 2 / 4)
         attn_case(32, 12, 1500, 1500, code)
         attn_case(64, 16, 1500, 1500, code)

@@ -139,7 +139,6 @@ WCB_DEV float epi_store1(const GemmArgs& g, int m, int n, float v) {
 template <typename T, int EPI = E_RUNTIME>
 WCB_DEV float epi_pointwise(const GemmArgs& g, int m, int n, float v) {
   if (has<EPI>(g, E_BIAS)) v += g.bias[n];
-  if (n < g.col_scale_n) v *= g.col_scale;
   if (has<EPI>(g, E_GELU)) v = gelu_t<T>(v);
   if (has<EPI>(g, E_ADDROW)) v += g.addrow[(long)(g.c_Mb ? m % g.c_Mb : m) * g.N + n];
   return v;
@@ -492,7 +491,6 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {   // epi_pointwise's order: + bias, GELU, + row table
         if (has<EPI>(g, E_BIAS)) v[e] += b8[e];
-        if (n < g.col_scale_n) v[e] *= g.col_scale;
         if (has<EPI>(g, E_GELU)) v[e] = gelu_t<T>(v[e]);
         if (has<EPI>(g, E_ADDROW))
           v[e] += g.addrow[(long)(g.c_Mb ? min(m, g.M - 1) % g.c_Mb : min(m, g.M - 1)) * g.N + min(n + e, g.N - 1)];
@@ -769,7 +767,6 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
       if (cc.it == 0) GPROBE(5);
       const int rb = cc.m0 + 128 * wr + (lane & 15);
       const int cb = cc.n0 + 64 * wc + 4 * c0;
-      const float cs = cc.n0 < g.col_scale_n ? g.col_scale : 1.f;   // (col_scale_n % 256 == 0)
       f32x4 b4[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -786,7 +783,6 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           f32x4 v = acc[mi][j] + b4[j];
-          if (g.col_scale_n) v *= cs;
           acc[mi][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           if constexpr ((EPI & E_GELU) != 0) {
 #pragma unroll
@@ -841,7 +837,7 @@ static bool launch_pp(const GemmArgs& g, hipStream_t s) {
     return false;
   } else {
     if (g.N % 256 != 0 || g.N > 8192 || g.K % 64 != 0 || g.K < 128 || g.a_Mb || g.c_Mb || g.addrow || g.mode != 0 || g.clamp != 0.f ||
-        g.rst_out || g.out16 || g.M < 256 || (g.resid && !g.out_f32) || (g.resid && g.act) || g.col_scale_n % 256)
+        g.rst_out || g.out16 || g.M < 256 || (g.resid && !g.out_f32) || (g.resid && g.act))
       return false;
     if (g.pp == 1) {   // where the LDS-ring kernel takes 256x192 tiles (d-wide N = 768: fewer tile rounds), it
                        // measured faster (C2 out 99 vs 104 µs, fc2 271 vs 277 µs)

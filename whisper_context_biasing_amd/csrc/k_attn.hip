@@ -492,12 +492,7 @@ void attention_decode(DType t, const AttnArgs& a, hipStream_t s) {
 // the arguments are ≤ 0 here and results below 2^-126 contribute nothing.
 // NS LDS stages (NS - 1 K/V tiles in flight behind the one being multiplied). 2 everywhere: a
 // third stage measured 3.6 % slower on the beam cross-attention (C3: 90.9 vs 87.7 µs per launch).
-// QL2 (encoder variant 6): q arrives pre-scaled by log2(e) (the QKV GEMM epilogue, GemmArgs::col_scale), and
-// the score accumulators start at -m (the running max of the query, log2 units), so the MFMA leaves
-// s - m and the softmax is exp2 straight off the accumulator (no per-score multiply-add). When a tile
-// raises some query's max (and always on a range's first tile) the wave subtracts the increase and
-// rescales, as the plain form does on every tile.
-template <typename T, int QW, int NS, bool QL2 = false>
+template <typename T, int QW, int NS>
 __global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnArgs a) {
   using Frag = typename DT<T>::frag;
   constexpr int QB = 4 * QW * 16;     // query rows per workgroup
@@ -551,7 +546,7 @@ __global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnAr
   float mrow[QW], lrow[QW];
 #pragma unroll
   for (int qi = 0; qi < QW; ++qi) {
-    mrow[qi] = QL2 ? 0.f : -INFINITY; lrow[qi] = 0.f;
+    mrow[qi] = -INFINITY; lrow[qi] = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[qi][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -596,9 +591,7 @@ __global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnAr
       f32x4 s[4];
 #pragma unroll
       for (int mf = 0; mf < 4; ++mf) {
-        const float init = QL2 ? -mrow[qi] : 0.f;
-        s[mf] = f32x4{init, init, init, init};
-        s[mf] = mma16(kf[mf][0], qf[qi][0], s[mf]);
+        s[mf] = mma16(kf[mf][0], qf[qi][0], f32x4{0.f, 0.f, 0.f, 0.f});
         s[mf] = mma16(kf[mf][1], qf[qi][1], s[mf]);
       }
       if constexpr (TAIL) {
@@ -616,29 +609,6 @@ __global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnAr
       tmax = xor16_max(tmax);
       tmax = xor32_max(tmax);
       float ls = 0.f;
-      if constexpr (QL2) {
-        // tmax: the tile's max relative to the running one. A range's first tile sets the running max
-        // outright; later tiles only when it grows (one wave-uniform branch; rare after the first tiles)
-        if (kt == 0) {   // nothing accumulated yet: no rescale
-          mrow[qi] = tmax;
-#pragma unroll
-          for (int mf = 0; mf < 4; ++mf) s[mf] -= tmax;
-        } else if (__any(tmax > 0.f)) {
-          const float d = fmaxf(tmax, 0.f);
-          const float alpha = __builtin_amdgcn_exp2f(-d);
-          mrow[qi] += d;
-#pragma unroll
-          for (int mf = 0; mf < 4; ++mf) s[mf] -= d;
-          lrow[qi] *= alpha;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[qi][j] *= alpha;
-        }
-#pragma unroll
-        for (int mf = 0; mf < 4; ++mf)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { s[mf][e] = __builtin_amdgcn_exp2f(s[mf][e]); ls += s[mf][e]; }
-        lrow[qi] += ls;
-      } else {
       const float mnew = fmaxf(mrow[qi], tmax);
       const float alpha = __builtin_amdgcn_exp2f((mrow[qi] - mnew) * L2E);
       mrow[qi] = mnew;
@@ -651,7 +621,6 @@ __global__ __launch_bounds__(256, QW == 2 ? 3 : 2) void attn_flash_kernel(AttnAr
       if (__any(alpha != 1.f)) {   // the accumulator rescale only when some row's max moved (exact)
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[qi][j] *= alpha;
-      }
       }
       pf[qi][0] = pack_p<T>(s[0], s[1]);
       pf[qi][1] = pack_p<T>(s[2], s[3]);
@@ -900,13 +869,12 @@ static void launch_flash(const AttnArgs& a, hipStream_t s) {
   } else {   // one key range (the key split is the few-query form only); XCD-grouped query blocks
     AttnArgs b = a;
     b.nsplit = 1;
-    const int qb = a.variant == 4 || a.variant == 6 ? 256 : 128, nqb = (a.Sq + qb - 1) / qb, BH = a.B * a.H;
+    const int qb = a.variant == 4 ? 256 : 128, nqb = (a.Sq + qb - 1) / qb, BH = a.B * a.H;
     const bool xg = nqb > 1 && BH % 8 == 0;
     b.xcd_nqb = xg ? nqb : 0;
     const dim3 grid = xg ? dim3(nqb * BH) : dim3(nqb, BH);
     // encoder tilings (option enc_flash): 64 queries per wave (4, default) or 32 (2)
     if (a.variant == 4) WCB_LAUNCH((attn_flash_kernel<T, 4, 2>), grid, dim3(256), 0, s, b);
-    else if (a.variant == 6) WCB_LAUNCH((attn_flash_kernel<T, 4, 2, true>), grid, dim3(256), 0, s, b);
     else WCB_LAUNCH((attn_flash_kernel<T, 2, 2>), grid, dim3(256), 0, s, b);
   }
 }

@@ -108,9 +108,6 @@ struct GemmArgs {
   int raster = 0;
   // 16-bit encoder GEMMs: the ping-pong kernel (gemm_impl.h gemm_pp_kernel) where it covers the launch
   int pp = 0;
-  // output columns [0, col_scale_n) scaled by col_scale after the bias (the encoder's q pre-scaled by
-  // log2 e for the flash kernel's exp2 softmax); 0 = off
-  int col_scale_n = 0; float col_scale = 1.f;
   // lean QKV (mode 2, one position per row): the new token's self-attention in the same launch
   // (gemm_impl.h dec_lean_kernel SA): o_h → sa_att [M][sa_ld]; sa_cnt = the launch's arrival counters
   // ([row blocks][hs_H] ints, zeroed once at allocation, monotonic). Set only where the lean kernel takes

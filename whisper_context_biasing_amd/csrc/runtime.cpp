@@ -234,9 +234,6 @@ struct wcb_handle {
   // encoder GEMMs: the ping-pong kernel (option "enc_gemm" 1; gemm_impl.h gemm_pp_kernel) or the LDS-ring
   // kernel (0)
   int enc_gemm = 1;
-  // encoder stream CU reservation (option "enc_cu_reserve"): 1/n of the CUs kept free of encoder work so
-  // the decode chains of the batches in flight always find CUs (0: none)
-  int enc_cu_reserve = 0;
   // decode projections on gemm_dec_kernel (K supported): the LayerNorm consumers compute their row
   // statistics from the rows they load, so the producers publish no per-16-column partial sums
   bool dec_gemm = false;
@@ -428,22 +425,19 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     h->d = *desc;
     h->dt = DType(desc->dtype);
     h->device = device;
-    // The decode chain is latency-bound and the encoder of the next batch runs beside it: decode
-    // streams get the highest priority so their workgroups dispatch ahead of encoder tiles.
-    int prio_lo = 0, prio_hi = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    const int dprio = prio_hi;
     HIPCHK(hipStreamCreateWithPriority(&h->he, hipStreamNonBlocking, 0));
-    for (int ci = 0; ci < wcb_handle::kMaxCtx; ++ci) {   // every context (option decode_contexts picks how many)
+    // decode streams: created on first use (ensure_ctx_streams), one per decode context in use. HIP
+    // maps streams onto a small pool of hardware queues (GPU_MAX_HW_QUEUES, 4 by default); a context
+    // whose queue is shared with the caller's stream inherits the caller's cross-stream waits (the
+    // sync_out of every front-end call), which serialised the two decode chains (measured: C2 step
+    // 102-139 ms when the library's streams predated the caller's, 52 ms otherwise). Streams that are
+    // never used take no queue.
+    for (int ci = 0; ci < wcb_handle::kMaxCtx; ++ci) {
       DecCtx& D = h->dc[ci];
-      HIPCHK(hipStreamCreateWithPriority(&D.hs, hipStreamNonBlocking, dprio));
       HIPCHK(hipEventCreateWithFlags(&D.ev_fork, hipEventDisableTiming));
       HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&D.done_h), 2 * sizeof(int), hipHostMallocDefault));
       for (hipEvent_t& e : D.ev_poll) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      for (int i = 0; i < DecCtx::kMaxSub && h->n_sub > 1; ++i) {   // row-group streams only when used
-        HIPCHK(hipStreamCreateWithPriority(&D.sub[i], hipStreamNonBlocking, dprio));
-        HIPCHK(hipEventCreateWithFlags(&D.ev_join[i], hipEventDisableTiming));
-      }
+      for (int i = 0; i < DecCtx::kMaxSub; ++i) HIPCHK(hipEventCreateWithFlags(&D.ev_join[i], hipEventDisableTiming));
     }
     for (int i = 0; i < wcb_handle::kMaxCtx; ++i) {
       HIPCHK(hipEventCreateWithFlags(&h->ev_xkv[i], hipEventDisableTiming));
@@ -573,7 +567,7 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       REQUIRE(value >= 0 && value <= 3, "option xenc_variant: 0..3");
       h->xenc_variant = value;
     } else if (n == "enc_flash") {
-      REQUIRE(value == 2 || value == 4 || value == 6, "option enc_flash: 2, 4 or 6");
+      REQUIRE(value == 2 || value == 4, "option enc_flash: 2 or 4");
       h->enc_flash_qw = value;
     } else if (n == "xenc_split") {
       REQUIRE(!h->ready, "option xenc_split: set before the weights are finalized");
@@ -582,50 +576,6 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "ring_kt") {
       REQUIRE(value == 1 || value == 2, "option ring_kt: 1 or 2");
       h->ring_kt = value;
-    } else if (n == "decode_cu_split") {
-      // decode context k's stream on half k % 2 of the CUs (alternate CU bits), so two overlapping decode
-      // chains never share a CU; 0: every CU, high priority (the default). Re-creates the decode streams.
-      REQUIRE(value == 0 || value == 1, "option decode_cu_split: 0 or 1");
-      REQUIRE(!h->step_state, "option decode_cu_split: a step-wise decode is active");
-      quiesce(h);
-      drop_graphs(h);
-      int ncu = 0;
-      HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
-      const int words = (ncu + 31) / 32;
-      int prio_lo = 0, prio_hi = 0;
-      HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-      for (int ci = 0; ci < wcb_handle::kMaxCtx; ++ci) {
-        DecCtx& D = h->dc[ci];
-        if (D.hs) HIPCHK(hipStreamDestroy(D.hs));
-        D.hs = nullptr;
-        if (value) {
-          std::vector<uint32_t> mask(words, 0u);
-          for (int cu = 0; cu < ncu; ++cu)
-            if (cu % 2 == ci % 2) mask[cu / 32] |= 1u << (cu % 32);
-          HIPCHK(hipExtStreamCreateWithCUMask(&D.hs, (uint32_t)words, mask.data()));
-        } else {
-          HIPCHK(hipStreamCreateWithPriority(&D.hs, hipStreamNonBlocking, prio_hi));
-        }
-      }
-    } else if (n == "enc_cu_reserve") {
-      // the encoder stream on a CU mask that leaves 1/value of the CUs (logical CU bits i with
-      // (i >> 3) % value == value - 1: spread over every XCD whether the driver stripes mask bits over
-      // the XCDs or not) to the decode chains; 0: every CU
-      REQUIRE(value == 0 || (value >= 2 && value <= 32), "option enc_cu_reserve: 0 or 2..32");
-      quiesce(h);
-      HIPCHK(hipStreamDestroy(h->he));
-      h->he = nullptr;
-      if (value) {
-        int ncu = 0;
-        HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        for (int cu = 0; cu < ncu; ++cu)
-          if ((cu >> 3) % value != value - 1) mask[cu / 32] |= 1u << (cu % 32);
-        HIPCHK(hipExtStreamCreateWithCUMask(&h->he, (uint32_t)mask.size(), mask.data()));
-      } else {
-        HIPCHK(hipStreamCreateWithPriority(&h->he, hipStreamNonBlocking, 0));
-      }
-      h->enc_cu_reserve = value;
     } else if (n == "steps_per_graph") {
       REQUIRE(value >= 1 && value <= 64, "option steps_per_graph: 1..64");
       h->steps_per_graph = value;
@@ -988,10 +938,6 @@ void encode_impl(wcb_handle* h, const float* mel, int B, void* enc_out) {
     h->timed("layernorm", 0, M * d * (4.0 + e), h->he, [&] { layernorm(h->dt, h->x.as<float>(), w.ln1_w, w.ln1_b, h->h.p, (int)M, d, h->he); });
     GemmArgs q = rowgemm(h->h.p, d, w.qkv_w, (int)M, 3 * d, d, h->qkv.p, 3 * d);
     q.bias = w.qkv_b;
-    // enc_flash 6: q leaves the projection scaled by log2(e) (one rounding, in the epilogue) for the
-    // flash kernel's exp2 softmax
-    const bool ql2 = h->enc_flash_qw == 6 && h->dt != kF32;
-    if (ql2) { q.col_scale_n = d; q.col_scale = 1.4426950408889634f; }
     run_gemm(h, "enc_qkv", q);
     AttnArgs a;
     a.q = h->qkv.p; a.ldq = 3 * d; a.q_Sb = S; a.Sq = S;
@@ -1038,8 +984,24 @@ int prefill_chunk(int R) { return std::max(1, kPrefillRows / std::max(R, 1)); }
 // buffers for `rows` >= B rows (a prefill pass carries several positions per decoder row)
 // contexts [c0, c1) (default: the generate() contexts 0 .. nctx-1; the step-wise decode state owns
 // context kMaxCtx-1)
+// the decode streams of contexts [c0, c1), created on first use at the highest priority (the decode
+// chains are latency-bound and the next batch's encoder runs beside them: their workgroups dispatch
+// ahead of encoder tiles); row-group streams only when n_sub > 1
+void ensure_ctx_streams(wcb_handle* h, int c0, int c1) {
+  int prio_lo = 0, prio_hi = 0;
+  for (int ci = c0; ci < c1; ++ci) {
+    DecCtx& D = h->dc[ci];
+    if (D.hs && (h->n_sub <= 1 || D.sub[0])) continue;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    if (!D.hs) HIPCHK(hipStreamCreateWithPriority(&D.hs, hipStreamNonBlocking, prio_hi));
+    for (int i = 0; i < DecCtx::kMaxSub && h->n_sub > 1; ++i)
+      if (!D.sub[i]) HIPCHK(hipStreamCreateWithPriority(&D.sub[i], hipStreamNonBlocking, prio_hi));
+  }
+}
+
 void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode, int rows = 0, int c0 = 0, int c1 = -1) {
   if (c1 < 0) c1 = h->nctx;
+  ensure_ctx_streams(h, c0, c1);
   rows = std::max(rows, B);
   const size_t e = esize(h->d.dtype), d = h->d.d_model, L = h->d.n_layers, S = h->S();
   const DecCtx& D0 = h->dc[c1 - 1];   // every context of the range is sized together
@@ -2234,11 +2196,11 @@ int wcb_op_attention(int dtype, const void* q, const void* k, const void* v, voi
     a.k = k; a.v = v; a.k_sb = (long)Sk * ld; a.k_sh = 64; a.k_sk = ld;
     a.o = o; a.ldo = ld; a.o_Sb = Sq; a.B = B; a.H = H; a.nkeys = Sk;
     const bool beam = flash >= 200 && flash <= 202;
-    if (flash == 1 || flash == 100 || flash == 102 || beam || flash < 0) {
-      // 100: 64 queries per wave; 102: the same with q given pre-scaled by log2(e) (enc_flash 6);
+    if (flash == 1 || flash == 100 || beam || flash < 0) {
+      // 100: 64 queries per wave;
       // 200 / 201 / 202: the beam kernel (keys split over the waves, Sq <= 16; 4 waves x 2 stages, 2 x 4,
       // 2 x 5); -n: n key ranges + merge (Sq <= 16)
-      a.variant = flash == 100 ? 4 : flash == 102 ? 6 : beam ? 7 + (flash - 200) : 1;
+      a.variant = flash == 100 ? 4 : beam ? 7 + (flash - 200) : 1;
       REQUIRE(!beam || Sq <= 16, "the beam kernel takes at most 16 query rows per set");
       REQUIRE(dtype != WCB_F32, "flash attention needs a 16-bit dtype");
       static DevBuf fpart;
