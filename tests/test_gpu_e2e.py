@@ -245,23 +245,32 @@ def test_broadcast_blob_views_load_without_host_copy():
 
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 def test_fused_lean_launches_are_bit_identical(dtype):
-    """The lean decode path's in-launch fusions (gemm_impl.h dec_lean_kernel FZ): option xq_kq — q'_h =
-    W_k,hᵀ q_h inside the LN-fused q_proj launch — and option qkv_sa — the new token's self-attention inside
-    the QKV launch (common.h group_arrive_wait hand-offs) — against the separate launches they replace:
-    identical arithmetic, so identical ids even on the diverse recipe, whose near-ties (gaps ~1e-3) flip
-    on any rounding difference. 32 rows (32-row QKV blocks), 13 and 40 rows (16-row blocks, ragged),
-    1000-phrase boost."""
+    """The lean decode path's in-launch fusion (gemm_impl.h dec_lean_kernel FZ 2): option xq_kq — q'_h =
+    W_k,hᵀ q_h inside the LN-fused q_proj launch (common.h group_arrive_wait hand-off) — against the
+    separate launches it replaces: identical arithmetic, so identical ids even on the diverse recipe,
+    whose near-ties (gaps ~1e-3) flip on any rounding difference. 32 rows (32-row QKV blocks), 13 and 40
+    rows (16-row blocks, ragged), 1000-phrase boost. Then the fused model again with its 64-bit arrival
+    counters seeded just below 2^31 and 2^32 (an int32 generation count wrapped there): the
+    same ids, and no hand-off wait timed out (wcb_synchronize reports one as an error)."""
     dims = get_dims("small")
     sd = make_weights(dims, seed=0, recipe="diverse")
     phrases = synth_bias_list(1000, eot=dims.eos_token_id)
     models = [WhisperCB.from_state_dict(dims, sd, dtype=dtype, options=o)
-              for o in ({"xq_kq": 1, "qkv_sa": 1}, {"xq_kq": 0, "qkv_sa": 0}, {"xq_kq": 1, "qkv_sa": 0})]
+              for o in ({"xq_kq": 1}, {"xq_kq": 0})]
+    kw = dict(max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0)
     for B in (32, 13, 40):
         x = torch.from_numpy(W.log_mel(synth_batch(B, start=3), dims.n_mel))
-        kw = dict(max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0)
         out = [m.generate(x, **kw).cpu().numpy() for m in models]
         for o in out[1:]:
             np.testing.assert_array_equal(out[0], o)
+    fused = models[0]
+    x = torch.from_numpy(W.log_mel(synth_batch(32, start=3), dims.n_mel))
+    ref = fused.generate(x, **kw).cpu().numpy()
+    for seed in ((1 << 31) - 8, (1 << 32) - 8):
+        fused.set_option("kq_cnt_seed", seed // 4)
+        for _ in range(2):   # both decode contexts
+            np.testing.assert_array_equal(fused.generate(x, **kw).cpu().numpy(), ref)
+        fused.synchronize()
 
 
 def test_bias_from_another_handle_is_rejected():

@@ -160,6 +160,10 @@ def test_decode_contexts_guard_while_stepwise_decode_is_open():
     dec = m.decode_begin(m.encode(x), min_new_tokens=n)
     with pytest.raises(_lib.WcbError, match="decode_contexts"):
         m.set_option("decode_contexts", 4)
+    # the state's copy of the encoder output keeps the layout chosen at begin
+    for opt, v in (("xenc_fm", 0), ("xenc_variant", 0)):
+        with pytest.raises(_lib.WcbError, match=opt):
+            m.set_option(opt, v)
     steps = []
     for i in range(n):
         steps.append(dec.step()[0])

@@ -71,27 +71,30 @@ WCB_DEV float xor32_max(float x) {
 // the measured sc1 table; cdna_hip_programming.md §6 G16): the producers store the handed-off bytes
 // with sc1 (write-through) stores — st_sc1 — and call group_arrive_wait; it drains every wave's
 // stores (vmcnt(0)), joins the workgroup, lets one lane add to the group's counter (agent scope) and
-// poll it with sc1 loads until all n members of this generation arrived, then releases the other waves
-// at a second workgroup barrier. Readers load the bytes with sc1 loads only (ld_sc1). Counters are
-// monotonic (generation = the value an add returned / n) and zeroed between calls by the caller. The
-// spin is bounded (a co-residency failure cannot hang the GPU; results would then be wrong, which the
-// parity tests see).
+// poll it with sc1 loads until all n members of this generation arrived, and releases the other waves
+// at a second workgroup barrier (no release / acquire fence: every handed-off byte is an sc1 store
+// drained before the add and an sc1 load after the poll — the guide's measured row-1 form). Readers load the bytes
+// with sc1 loads only (ld_sc1). Counters are 64-bit and monotonic (generation = the value an add
+// returned / n; 2^64 arrivals do not wrap in any run). The spin is bounded (a co-residency failure cannot
+// hang the GPU): running it out sets *err, which the host reports as an error at wcb_synchronize.
 WCB_DEV void st_sc1(void* p, uint64_t v) {
   __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 WCB_DEV uint64_t ld_sc1(const void* p) {
   return __hip_atomic_load(reinterpret_cast<uint64_t*>(const_cast<void*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-WCB_DEV void group_arrive_wait(int* cnt, int n) {
+WCB_DEV void group_arrive_wait(unsigned long long* cnt, unsigned long long n, int* err) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int target = (old / n + 1) * n;
+    const unsigned long long old = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long target = (old / n + 1) * n;
+    bool ok = false;
     for (int spin = 0; spin < (1 << 22); ++spin) {
-      if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) { ok = true; break; }
       __builtin_amdgcn_s_sleep(1);
     }
+    if (!ok) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
 }
@@ -136,17 +139,6 @@ WCB_DEV float wave_max(float v) {
 }
 
 // Store 8 consecutive f32 values as T.
-// load8f of bytes handed off inside the launch (group_arrive_wait): two 8-byte sc1 loads
-template <typename T> WCB_DEV void load8f_sc1(const T* src, float* v) {
-  static_assert(sizeof(T) == 2, "16-bit types");
-  const uint64_t w[2] = {ld_sc1(src), ld_sc1(src + 4)};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const unsigned short bits = (unsigned short)(w[j >> 2] >> (16 * (j & 3)));
-    if constexpr (__is_same(T, bf16_t)) v[j] = bf16_to_f(bits);
-    else v[j] = float(__builtin_bit_cast(f16_t, bits));
-  }
-}
 template <typename T> WCB_DEV void store8(T* dst, const float* v);
 template <> WCB_DEV void store8<bf16_t>(bf16_t* dst, const float* v) {
   s16x8 o;

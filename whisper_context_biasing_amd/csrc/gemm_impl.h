@@ -16,7 +16,6 @@
 #include <stdexcept>
 #include "common.h"
 #include "kernels.h"
-#include "self_attn.h"
 
 #include <algorithm>
 #include <cstdio>
@@ -1387,19 +1386,14 @@ template <typename T> struct DecLean {
   unsigned long long* stamp = nullptr;   // tools/dec_kernel_bench: per-workgroup phase stamps (null: off)
   int cfm_nw = 0, cfm_kpw = 0;           // EPI 0: out written fragment-major for a consumer with this split (0: rows)
   T* out2 = nullptr;                     // EPI 1: the 16-bit copy again, fragment-major with (cfm_nw, cfm_kpw)
-  // FZ 1 (EPI 2): the self-attention of the new token in the same launch — att [M][ld_att] (T) receives
-  // o_h; FZ 2 (EPI 0, the cross-attention query): q'_h = W_k,hᵀ q_h in the same launch — kq_w = W_kt's
-  // fragment-major copy ([H·D/16 tiles][2 waves][lane][8]), qp [M][ld_att] (T). sa_cnt: the arrival
-  // counters of the (row block, head) groups ([gridDim.y][kvH], monotonic)
-  T* att = nullptr; int ld_att = 0; int* sa_cnt = nullptr;
+  // FZ 2 (EPI 0, the cross-attention query): q'_h = W_k,hᵀ q_h in the same launch — kq_w = W_kt's
+  // fragment-major copy ([H·D/16 tiles][2 waves][lane][8]), qp → att [M][ld_att] (T). cnt: the 64-bit
+  // arrival counters of the (row block, head) groups ([gridDim.y][kvH], monotonic); err: set when a wait
+  // ran out its bound
+  T* att = nullptr; int ld_att = 0; unsigned long long* cnt = nullptr; int* err = nullptr;
   const T* kq_w = nullptr;
 };
 
-//   SA (EPI 2): the QKV launch also runs the self-attention of the new token. The 12 column tiles of a
-//   head (4 of q, 4 of k, 4 of v) store their tiles write-through (sc1), meet at the head's arrival
-//   counter (common.h group_arrive_wait: one dependent hand-off instead of a kernel boundary and a
-//   launch), and their waves then run self_attn_wave (self_attn.h, the stand-alone kernel's body, sc1
-//   loads) for one row each — bit-identical to the two launches.
 //   FZ 2 (EPI 0, LN: the cross-attention query q_h = LN(x) W_q,hᵀ + b_q): the 4 column tiles of a head store
 //   q_h write-through, meet at the head's counter, and each then computes a quarter of q'_h = W_k,hᵀ q_h
 //   (the grouped K = 64 product of the kq launch it replaces: the same two 32-deep MFMA halves summed in
@@ -1407,7 +1401,6 @@ template <typename T> struct DecLean {
 template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP, bool WFM = false, bool AFM = false,
           int FZ = 0>
 __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
-  constexpr bool SA = FZ == 1 && EPI == 2;
   constexpr bool KQ = FZ == 2 && EPI == 0 && LN && !GELU && !GRP;
   using Frag = typename DT<T>::frag;
   constexpr int NT = NW * 64, K = NW * KPW * 32, R = MF * 16;
@@ -1538,7 +1531,7 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   // ---------------- epilogue: 4 consecutive columns of one row per thread
   const int row = mb + er;
   const bool live = er < R && row < p.M && ec < p.N;
-  if (!SA && !KQ && !live) return;   // (SA / KQ: every thread reaches the hand-off below)
+  if (!KQ && !live) return;   // (KQ: every thread reaches the hand-off below)
   if (live) {
   float v[4];
 #pragma unroll
@@ -1573,10 +1566,7 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
       const int n2 = ec - p.n_split, hh = n2 >> 6, dd = n2 & 63;
       const int kvs = hh / p.kvH, hd = hh % p.kvH;
       const long off = ((((long)kvs * p.kvB + row) * p.kvH + hd) * p.kvT + pos) * 64 + dd;
-      if constexpr (SA) st_sc1(p.kv + off, __builtin_bit_cast(uint64_t, hv));
-      else *reinterpret_cast<s4*>(p.kv + off) = hv;
-    } else if (EPI == 2 && SA) {         // q of the new token, handed to the head's attention waves
-      st_sc1(p.out + (long)row * p.ldo + ec, __builtin_bit_cast(uint64_t, hv));
+      *reinterpret_cast<s4*>(p.kv + off) = hv;
     } else if (EPI == 0 && p.cfm_nw) {   // fragment-major for the consumer's (waves, k-steps): 4 elements of one fragment
       const int kw = p.cfm_kpw * 32, w2 = ec / kw, ks2 = (ec % kw) >> 5, lg = (ec & 31) >> 3;
       const long off = ((((long)(row >> 4) * p.cfm_nw + w2) * p.cfm_kpw + ks2) * 64 + lg * 16 + (row & 15)) * 8 + (ec & 7);
@@ -1588,29 +1578,9 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
     }
   }
   }   // live
-  if constexpr (EPI == 2 && SA) {
-    // this tile's head and its index among the head's 12 tiles (q 0-3, k 4-7, v 8-11)
-    const int D = p.n_split;
-    int hg, j;
-    if (n0 < D) {
-      hg = n0 >> 6; j = (n0 >> 4) & 3;
-    } else {
-      const int hh = (n0 - D) >> 6;
-      hg = hh % p.kvH; j = 4 * (1 + hh / p.kvH) + (((n0 - D) >> 4) & 3);
-    }
-    group_arrive_wait(p.sa_cnt + blockIdx.y * p.kvH + hg, 12);
-    const int r = j * NW + wave;   // one row of the block per wave (12·NW >= R)
-    if (r < R && mb + r < p.M) {
-      const int b = mb + r;
-      const long kofs = (((long)b * p.kvH + hg) * p.kvT) * 64;
-      const long vofs = (long)p.kvB * p.kvH * p.kvT * 64;
-      self_attn_wave<T, true>(p.out + (long)b * p.ldo + hg * 64, p.kv + kofs, p.kv + vofs + kofs, p.kvT - 1,
-                              [&] { return pos + 1; }, p.att + (long)b * p.ld_att + hg * 64);
-    }
-  }
   if constexpr (KQ) {
     const int hq = n0 >> 6, jq = (n0 >> 4) & 3;
-    group_arrive_wait(p.sa_cnt + blockIdx.y * p.kvH + hq, 4);
+    group_arrive_wait(p.cnt + blockIdx.y * p.kvH + hq, 4, p.err);
     // A = q_h rows of this block (lane: row lane & 15, k = 32·kh + 8·(lane >> 4)), sc1 loads
     Frag qa[2];
     {
@@ -1668,19 +1638,11 @@ static void launch_lean_k(const GemmArgs& g, hipStream_t s) {
   if (g.c_fm || g.out16_fm) lean_cfg(g.N, p.cfm_nw, p.cfm_kpw);   // the consumer's split of K = this N
   p.out2 = reinterpret_cast<T*>(g.out16_fm);
   const dim3 grid((g.N + 15) / 16, (g.M + MF * 16 - 1) / (MF * 16));
-  if constexpr (EPI == 2 && !GRP) {
-    if (g.sa_att) {   // QKV + the new token's self-attention in one launch (fragment-major weights)
-      if (!g.W_fm) throw std::runtime_error("internal error: fused QKV self-attention needs the fragment-major weights");
-      p.att = reinterpret_cast<T*>(g.sa_att); p.ld_att = g.sa_ld; p.sa_cnt = g.sa_cnt;
-      if (g.a_fm) WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, true, 1>), grid, dim3(NW * 64), 0, s, p);
-      else WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, false, 1>), grid, dim3(NW * 64), 0, s, p);
-      return;
-    }
-  }
   if constexpr (EPI == 0 && LN && !GELU && !GRP) {
     if (g.kq_w) {   // the cross-attention query and q'_h = W_k,hᵀ q_h in one launch (fragment-major weights)
       if (!g.W_fm) throw std::runtime_error("internal error: fused cross-query needs the fragment-major weights");
-      p.att = reinterpret_cast<T*>(g.kq_out); p.ld_att = (int)g.kq_ld; p.sa_cnt = g.sa_cnt;
+      if (!g.kq_cnt || !g.kq_err) throw std::runtime_error("internal error: fused cross-query without its arrival counters");
+      p.att = reinterpret_cast<T*>(g.kq_out); p.ld_att = (int)g.kq_ld; p.cnt = g.kq_cnt; p.err = g.kq_err;
       p.kq_w = reinterpret_cast<const T*>(g.kq_w); p.kvH = g.hs_H;
       if (g.a_fm) WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, true, 2>), grid, dim3(NW * 64), 0, s, p);
       else WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, false, 2>), grid, dim3(NW * 64), 0, s, p);
@@ -1962,7 +1924,7 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
     // rows (measured C2: 1.074 vs 1.147 ms/token with 32-row workgroups); the LM head walks the
     // vocabulary persistently with 32-row workgroups, reading every weight tile once
     if (g.lean && launch_lean<T>(g, s)) return;
-    if (g.sa_att || g.kq_w) throw std::runtime_error("internal error: fused QKV self-attention / cross-query on a launch the lean kernel does not cover");
+    if (g.kq_w) throw std::runtime_error("internal error: fused cross-query on a launch the lean kernel does not cover");
     if (g.a_fm || g.c_fm || g.out16_fm)   // the runtime pairs fragment-major operands only where the lean path takes both
       throw std::runtime_error("internal error: fragment-major operand on a launch the lean kernel does not cover");
     const bool mf1 = (g.M <= 64 && !(g.sel_val && g.M > 16)) || g.K >= 4096;

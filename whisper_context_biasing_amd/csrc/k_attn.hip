@@ -433,7 +433,7 @@ __global__ __launch_bounds__(64 * WPG) void attn_self_lean_kernel(SelfLean a) {
   const int pair = min(blockIdx.y * WPG + (int)(threadIdx.x >> 6), a.npairs - 1);
   const int b = pair / a.H, h = pair % a.H;
   const long base = (long)((a.row0 + b) / a.b_div) * a.k_sb + (long)h * a.k_sh;
-  self_attn_wave<T, false>(reinterpret_cast<const T*>(a.q) + (long)b * a.ldq + h * 64,
+  self_attn_wave<T>(reinterpret_cast<const T*>(a.q) + (long)b * a.ldq + h * 64,
                            reinterpret_cast<const T*>(a.k) + base, reinterpret_cast<const T*>(a.v) + base, a.cap,
                            [&] { return __builtin_amdgcn_readfirstlane(__builtin_nontemporal_load(a.nkeys_dev)) + a.nkeys_add; },
                            reinterpret_cast<T*>(a.o) + (long)b * a.ldo + h * 64);

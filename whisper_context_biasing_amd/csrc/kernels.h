@@ -108,13 +108,12 @@ struct GemmArgs {
   int raster = 0;
   // 16-bit encoder GEMMs: the ping-pong kernel (gemm_impl.h gemm_pp_kernel) where it covers the launch
   int pp = 0;
-  // lean QKV (mode 2, one position per row): the new token's self-attention in the same launch
-  // (gemm_impl.h dec_lean_kernel SA): o_h → sa_att [M][sa_ld]; sa_cnt = the launch's arrival counters
-  // ([row blocks][hs_H] ints, zeroed once at allocation, monotonic). Set only where the lean kernel takes
-  // the launch (gemm() throws otherwise).
-  void* sa_att = nullptr; int sa_ld = 0; int* sa_cnt = nullptr;
   // lean LN-fused cross-attention query (EPI 0): q'_h = W_k,hᵀ q_h in the same launch (kq_w = W_kt's
-  // fragment-major copy, kq_out [M][kq_ld] = [M][H·d], arrival counters in sa_cnt, heads in hs_H)
+  // fragment-major copy, kq_out [M][kq_ld] = [M][H·d], heads in hs_H). kq_cnt: the launch's arrival
+  // counters ([row blocks][hs_H], 64-bit, zeroed once at allocation, monotonic: 2^64 arrivals never wrap);
+  // kq_err: a word set when a hand-off wait ran out its spin bound (the host reports it at synchronize).
+  // Set only where the lean kernel takes the launch (gemm() throws otherwise).
+  unsigned long long* kq_cnt = nullptr; int* kq_err = nullptr;
   const void* kq_w = nullptr; void* kq_out = nullptr; long kq_ld = 0;
 };
 

@@ -128,7 +128,7 @@ struct DecCtx {
   int dec_B = 0, dec_T = 0;
   DevBuf kvself, dx, dx16, dx16fm, dh, dq, dqp, du, datt, dffn, dstats, drst, xpart, xml, xticket, logits, part_val, part_idx, ints,
       pids, outbuf, forced, beam;
-  DevBuf sa_cnt;   // arrival counters of the fused lean launches [L][kMaxSub][QKV+SA | xq+kq][4][H] (monotonic)
+  DevBuf kq_cnt;   // 64-bit arrival counters of the fused xq+kq launches [L][kMaxSub][4 row blocks][H] (monotonic)
   int nchunk = 64;
   hipGraphExec_t gexec = nullptr;               // captured decode step
   hipGraphExec_t gexec_k = nullptr;             // steps_per_graph consecutive decode steps in one graph
@@ -221,11 +221,6 @@ struct wcb_handle {
   // lean path: the residual writers (embedding, out / xo / fc2 projections) also write the 16-bit rows
   // fragment-major for the LayerNorm-fused consumers (QKV, xq, fc1); option "lean_x"
   int lean_x = 1;
-  // lean path, one position per row: the new token's self-attention inside the QKV launch (option
-  // "qkv_sa"; gemm_impl.h dec_lean_kernel SA; bit-identical to the two launches). Off by default:
-  // measured slower than the two launches (rocprofv3, C2 decode: 13.2 µs fused against 5.3 + 5.1 µs;
-  // the attention's K/V reads must bypass the caches (sc1) behind the in-launch hand-off)
-  int qkv_sa = 0;
   struct wcb_state* step_state = nullptr;   // the active step-wise decode (wcb_decode_begin), if any
   // encoder GEMM tile order (option "enc_raster"): bands of n row panels with the column tiles outer
   // (GemmArgs::raster; 0 = row-major). 8 measured best with the round-3 ring kernel (whisper-small:
@@ -261,6 +256,9 @@ struct wcb_handle {
   // default (empty) bias automaton
   std::unique_ptr<wcb_bias> empty_bias;
   std::vector<wcb_bias*> biases;     // live automatons created on this handle (lifetime, wcb.h)
+  // device error word: set by a kernel whose in-launch hand-off wait ran out its spin bound (common.h
+  // group_arrive_wait); read and cleared by wcb_synchronize (and the blocking calls that wait anyway)
+  DevBuf dev_err;
   // profiling
   bool prof = false, prof_stamps = false;
   std::vector<ProfEntry> prof_e;
@@ -497,6 +495,7 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     eb->st_depth.ensure(4);   // root: depth 0, keep 0 (zeroed)
     eb->st_keep.ensure(4);
     h->empty_bias = std::move(eb);
+    h->dev_err.ensure(4);
     *out = h.release();
   });
 }
@@ -510,7 +509,7 @@ void wcb_destroy(wcb_handle* h) {
     if (D.gexec) (void)hipGraphExecDestroy(D.gexec);
     if (D.gexec_k) (void)hipGraphExecDestroy(D.gexec_k);
     for (DevBuf* b : {&D.kvself, &D.dx, &D.dx16, &D.dx16fm, &D.dh, &D.dq, &D.dqp, &D.du, &D.datt, &D.dffn, &D.dstats, &D.drst, &D.xpart, &D.xml, &D.xticket,
-                      &D.logits, &D.part_val, &D.part_idx, &D.ints, &D.outbuf, &D.forced, &D.beam, &D.sa_cnt})
+                      &D.logits, &D.part_val, &D.part_idx, &D.ints, &D.outbuf, &D.forced, &D.beam, &D.kq_cnt})
       b->release();
     if (D.ev_fork) (void)hipEventDestroy(D.ev_fork);
     for (hipEvent_t e : D.ev_poll)
@@ -524,7 +523,7 @@ void wcb_destroy(wcb_handle* h) {
   }
   for (auto& b : h->owned) b.release();
   for (DevBuf* b : {&h->dft, &h->mel_lo, &h->mel_hi, &h->mel_w, &h->clip_max, &h->xt, &h->hbuf, &h->x, &h->h,
-                    &h->qkv, &h->att, &h->ffn, &h->encout, &h->stamps, &h->stamp_acc})
+                    &h->qkv, &h->att, &h->ffn, &h->encout, &h->stamps, &h->stamp_acc, &h->dev_err})
     b->release();
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
@@ -565,6 +564,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       h->group_rows = value;
     } else if (n == "xenc_variant") {
       REQUIRE(value >= 0 && value <= 3, "option xenc_variant: 0..3");
+      // the step-wise state's copy of the encoder output was laid out for the variant at begin time
+      REQUIRE(!h->step_state, "option xenc_variant: a step-wise decode is active (wcb_decode_end first)");
       h->xenc_variant = value;
     } else if (n == "enc_flash") {
       REQUIRE(value == 2 || value == 4, "option enc_flash: 2 or 4");
@@ -576,10 +577,21 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "ring_kt") {
       REQUIRE(value == 1 || value == 2, "option ring_kt: 1 or 2");
       h->ring_kt = value;
+    } else if (n == "kq_cnt_seed") {
+      // test hook: every allocated arrival counter of the fused xq+kq launches set to 4·value (a generation
+      // boundary of the 4-member groups), e.g. just below 2^31 or 2^32 to check that no counter width wraps
+      REQUIRE(value >= 0, "option kq_cnt_seed: >= 0");
+      quiesce(h);
+      for (DecCtx& D : h->dc) {
+        if (!D.kq_cnt.p) continue;
+        std::vector<unsigned long long> v(D.kq_cnt.bytes / 8, 4ull * (unsigned long long)value);
+        HIPCHK(hipMemcpy(D.kq_cnt.p, v.data(), v.size() * 8, hipMemcpyHostToDevice));
+      }
     } else if (n == "steps_per_graph") {
       REQUIRE(value >= 1 && value <= 64, "option steps_per_graph: 1..64");
       h->steps_per_graph = value;
     } else if (n == "xenc_fm") {
+      REQUIRE(!h->step_state, "option xenc_fm: a step-wise decode is active (wcb_decode_end first)");
       h->xenc_fm = value != 0;
     } else if (n == "xq_kq") {
       h->xq_kq = value != 0;
@@ -595,8 +607,6 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       h->lean = value != 0;
     } else if (n == "lean_x") {
       h->lean_x = value != 0;
-    } else if (n == "qkv_sa") {
-      h->qkv_sa = value != 0;
     } else if (n == "merge_v") {
       h->merge_v = value != 0;
     } else if (n == "ln_fold") {
@@ -853,6 +863,16 @@ void sync_out(wcb_handle* h, void* stream, hipStream_t from) {
   HIPCHK(hipStreamWaitEvent((hipStream_t)stream, h->ev_out, 0));
   HIPCHK(hipGetLastError());
 }
+// the device error word (after the streams drained): a hand-off that ran out its bound means the launch's
+// workgroups were not co-resident and its outputs are unsynchronised — an error, never silent
+void check_dev_err(wcb_handle* h) {
+  int e = 0;
+  HIPCHK(hipMemcpy(&e, h->dev_err.p, 4, hipMemcpyDeviceToHost));
+  if (e) {
+    HIPCHK(hipMemset(h->dev_err.p, 0, 4));
+    throw WcbError(WCB_ERR_HIP, "an in-launch hand-off wait timed out (workgroups not co-resident): outputs invalid");
+  }
+}
 // drain every library stream (before any workspace reallocation)
 void quiesce(wcb_handle* h) {
   HIPCHK(hipStreamSynchronize(h->he));
@@ -1036,7 +1056,7 @@ void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode
     D.dqp.ensure((size_t)rows * h->H() * d * e);
     D.du.ensure((size_t)rows * h->H() * d * e);
     D.xticket.ensure((size_t)rows * h->H() * 4);     // zeroed on allocation; combiners reset their slot
-    D.sa_cnt.ensure((size_t)L * DecCtx::kMaxSub * 2 * 4 * h->H() * 4);   // zeroed on allocation, monotonic
+    D.kq_cnt.ensure((size_t)L * DecCtx::kMaxSub * 4 * h->H() * 8);   // zeroed on allocation, monotonic
     D.pids.ensure((size_t)rows * 4);
     D.logits.ensure((size_t)B * h->vocab_pad * 4);
     D.nchunk = lm_head_partials(h->dt, (int)d, h->d.vocab);   // argmax partials per row of the LM head
@@ -1181,14 +1201,6 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
     q.kv_rps = rps; q.ln_u = w.ln1_u; q.ln_c = w.ln1_c; q.ln_wg = w.qkv_wg; q.W_fm = w.qkv_fm;
     if (x16fm) { q.ln_a16 = x16fm; q.a_fm = 1; }
-    // the new token's self-attention in the QKV launch: one position per row on the lean kernel with
-    // the fragment-major weights (the conditions under which launch_lean takes this launch)
-    const bool sa = h->qkv_sa && h->lean && fm_ok && rps == 1 && w.qkv_fm && !c.phys &&
-                    (d == 512 || d == 768 || d == 1024 || d == 1280);   // launch_lean's LayerNorm table
-    if (sa) {
-      q.sa_att = datt; q.sa_ld = d;
-      q.sa_cnt = D.sa_cnt.as<int>() + (((size_t)l * DecCtx::kMaxSub + chain) * 2 + 0) * 4 * H;
-    }
     proj("dec_qkv", q);
     AttnArgs a;
     a.q = dq; a.ldq = d; a.q_Sb = rps; a.Sq = rps; a.causal = rps > 1;
@@ -1198,7 +1210,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     a.row0 = b0; a.phys = c.phys; a.phys_ld = T;
     a.o = datt; a.ldo = d; a.o_Sb = rps; a.B = nb; a.H = H; a.nkeys_dev = pos; a.nkeys_add = 1;
     a.kv_rows = rps == 1 ? T : 0;
-    if (!sa) {
+    {
       const double t_keys = c.host_pos >= 0 ? c.host_pos + 1 : 0;   // keys this step (eager pass)
       h->timed("dec_self_attn", 4.0 * nb * H * t_keys * 64, nb * H * t_keys * 128.0 * e, st_,
                [&] { attention_decode(h->dt, a, st_); });
@@ -1219,7 +1231,8 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       const bool kqf = h->xq_kq && h->lean && fm_ok && w.xq_fm && w.xkt_fm && (d == 512 || d == 768 || d == 1024 || d == 1280);
       if (kqf) {
         xq.kq_w = w.xkt_fm; xq.kq_out = dqp; xq.kq_ld = (long)H * d; xq.hs_H = H;
-        xq.sa_cnt = D.sa_cnt.as<int>() + (((size_t)l * DecCtx::kMaxSub + chain) * 2 + 1) * 4 * H;
+        xq.kq_cnt = D.kq_cnt.as<unsigned long long>() + ((size_t)l * DecCtx::kMaxSub + chain) * 4 * H;
+        xq.kq_err = h->dev_err.as<int>();
       }
       proj("dec_xq", xq);
       if (!kqf) {
@@ -1744,6 +1757,7 @@ int wcb_decode_end(wcb_handle* h, wcb_state* st) {
   return guarded(h, [&] {
     REQUIRE(h && st && st->h == h && h->step_state == st, "bad argument (state of this handle)");
     HIPCHK(hipStreamSynchronize(h->dc[wcb_handle::kMaxCtx - 1].hs));
+    check_dev_err(h);
     h->step_state = nullptr;
     delete st;
   });
@@ -1754,6 +1768,7 @@ int wcb_synchronize(wcb_handle* h) {
     REQUIRE(h, "null handle");
     quiesce(h);
     HIPCHK(hipGetLastError());
+    check_dev_err(h);
   });
 }
 

@@ -1,11 +1,9 @@
 // Decoder self-attention of one new token for one (row, head) pair on one wave
-// ([tf] modeling_whisper.py:284-356, the decoder's self_attn with a KV cache): shared by the
-// stand-alone kernel (k_attn.hip attn_self_lean_kernel) and the QKV projection that runs it in the same
-// launch (gemm_impl.h dec_lean_kernel, SA) — one body, so both give the same bits.
+// ([tf] modeling_whisper.py:284-356, the decoder's self_attn with a KV cache): the body of the
+// stand-alone kernel (k_attn.hip attn_self_lean_kernel).
 // 8 lanes per key (16 B of K and of V each), 8 keys per load, the first 64 keys requested before the
 // key count is known (rows past it clamped to the cache capacity `cap` and masked); longer contexts
-// continue in 64-key chunks with an online softmax. SC1: every q / K / V load is an sc1 load (bytes
-// handed off inside the launch, common.h group_arrive_wait).
+// continue in 64-key chunks with an online softmax.
 #pragma once
 #include "common.h"
 
@@ -13,15 +11,12 @@ namespace wcb {
 
 // q, o: the pair's 64 values; k0 / v0: its key 0 (keys 64 elements apart); nkeys(): the key count,
 // called after the first K / V loads are issued
-template <typename T, bool SC1, typename NK>
+template <typename T, typename NK>
 WCB_DEV void self_attn_wave(const T* q, const T* k0, const T* v0, int cap, NK&& nkeys, T* o) {
   const int lane = threadIdx.x & 63, seg = lane & 7, kg = lane >> 3;
   const T* kb = k0 + seg * 8;
   const T* vb = v0 + seg * 8;
-  auto ld8 = [&](const T* p, float* v) {
-    if constexpr (SC1) load8f_sc1<T>(p, v);
-    else load8f<T>(p, v);
-  };
+  auto ld8 = [&](const T* p, float* v) { load8f<T>(p, v); };
   float qv[8], kv[8][8], vv[8][8];
   ld8(q + seg * 8, qv);
 #pragma unroll
