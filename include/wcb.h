@@ -133,20 +133,38 @@ int wcb_encode(wcb_handle* h, const float* mel, int B, void* enc_out, void* stre
 int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg, const wcb_bias* bias,
                  const int32_t* prefix, int prefix_len, int32_t* out_ids, int32_t* out_steps, void* stream);
 
-/* Step-wise greedy decoding (SURVEY §8(b) wcb_decode_begin / wcb_decode_step): the decode step of
- * wcb_generate one token per call, for callers that inspect every step (the reference's surface is
- * generate(); this is the streaming form of it). `enc` = encoder output [B][1500][d] in the model dtype
- * (DEVICE, copied / projected at begin: not retained), `prefix` = per-row prompt [B][prefix_len] (HOST,
- * NULL: decoder_start_token_id only; positions 0 .. prefix_len-2 are prefilled, the last one is the first
- * step's input), num_beams must be 1 (beam search reorders past tokens: wcb_generate), EOS masked while
- * fewer than min_new_tokens were generated. One active state per handle (it owns decode context 3, so
- * decode_contexts must be <= 3). wcb_decode_step writes next_ids [B] (int32, DEVICE) and, when non-NULL,
- * scores [B] (f32, DEVICE: the chosen token's logit + bias boost; 0 for finished rows); finished rows
- * emit pad_token_id. The bias automaton must be the same (or NULL) at every step of one decode. */
+/* Step-wise decoding (SURVEY §8(b) wcb_decode_begin / wcb_decode_step): the decode step of wcb_generate
+ * one token per call, for callers that inspect every step (the reference's surface is generate(); this is
+ * the streaming form of it). `enc` = encoder output [B][1500][d] in the model dtype (DEVICE, copied /
+ * projected at begin: not retained), `prefix` = per-utterance prompt [B][prefix_len] (HOST, NULL:
+ * decoder_start_token_id only; positions 0 .. prefix_len-2 are prefilled, the last one is the first step's
+ * input), EOS masked while fewer than min_new_tokens were generated. One active state per handle (it owns
+ * decode context 3, so decode_contexts must be <= 3). The bias automaton must be the same (or NULL) at
+ * every step of one decode.
+ *  - greedy (num_beams = 1): wcb_decode_step writes next_ids [B] (int32, DEVICE) and, when non-NULL,
+ *    scores [B] (f32, DEVICE: the chosen token's logit + bias boost; 0 for finished rows); finished rows
+ *    emit pad_token_id.
+ *  - beam search (num_beams = nb in 2..8, HF _beam_search, [tf] generation/utils.py:3208-3524, one
+ *    iteration per step; rows R = B·nb, beam i of utterance b = row b·nb + i): wcb_decode_begin caps the
+ *    length at max_target_positions as generate() does by default, wcb_decode_begin_beams at prefix +
+ *    max_new_tokens (generate(max_length=...); the cap is a stopping criterion, so it changes the beams).
+ *    wcb_decode_step writes the token each running beam appended, next_ids [R], and when non-NULL the
+ *    running log-prob sums, scores [R]; wcb_decode_parents then gives parents [R] (int32, DEVICE): the
+ *    beam (0..nb-1 of the same utterance) each running beam extends — the running sequences are the
+ *    parents' sequences plus next_ids. Once every utterance is done a step changes nothing.
+ *  - wcb_decode_result: out_ids [B][max_new] (int32, DEVICE; max_new = max_target_positions - prefix_len
+ *    for wcb_decode_begin, max_new_tokens for wcb_decode_begin_beams) and *out_steps (host) = the columns
+ *    generated: greedy, the steps taken (finished rows padded); beams, the best finished sequence of each
+ *    utterance so far with *out_steps its longest length — after the steps generate() takes, exactly
+ *    generate()'s output. */
 typedef struct wcb_state wcb_state;
 int wcb_decode_begin(wcb_handle* h, const void* enc, int B, int num_beams, const int32_t* prefix, int prefix_len,
                      float bias_boost, int min_new_tokens, wcb_state** out, void* stream);
+int wcb_decode_begin_beams(wcb_handle* h, const void* enc, int B, int num_beams, const int32_t* prefix, int prefix_len,
+                           int max_new_tokens, float bias_boost, int min_new_tokens, wcb_state** out, void* stream);
 int wcb_decode_step(wcb_handle* h, wcb_state* st, const wcb_bias* bias, int32_t* next_ids, float* scores, void* stream);
+int wcb_decode_parents(wcb_handle* h, wcb_state* st, int32_t* parents, void* stream);
+int wcb_decode_result(wcb_handle* h, wcb_state* st, int32_t* out_ids, int32_t* out_steps, void* stream);
 int wcb_decode_end(wcb_handle* h, wcb_state* st);
 
 /* wait for every queued front-end / encoder / decode operation of the handle */
@@ -224,8 +242,7 @@ int wcb_op_layernorm(int dtype, const float* x, const float* w, const float* b, 
                      void* stream);
 /* o[B][Sq][H*64] = softmax(q kᵀ) v per head (q pre-scaled), k/v [B][Sk][H*64];
  * flash=1 selects the MFMA kernel (16-bit dtypes; Sq <= 16: the few-query form of beam search), 100 the
- * MFMA kernel with 64 queries per wave, 102 the same with q given pre-scaled by log2(e) (softmax in
- * base 2), 200 / 201 / 202 (Sq <= 16) the beam kernel (the keys of a (set,
+ * MFMA kernel with 64 queries per wave, 200 / 201 / 202 (Sq <= 16) the beam kernel (the keys of a (set,
  * head) split over its waves, merged in the workgroup: 4 waves x 2 LDS stages, 2 x 4, 2 x 5), -n (Sq <= 16)
  * the MFMA kernel over n key ranges merged in
  * fixed order; 0 the decode kernel; n >= 2 the decode kernel with n split-KV key chunks combined by the

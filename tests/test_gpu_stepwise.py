@@ -1,6 +1,7 @@
-"""GPU: step-wise greedy decoding (wcb_decode_begin / wcb_decode_step) against
-generate() on the same clips: the same decode step one token per call, so the ids must be identical
-(f32 K/V cross-attention and bf16 encoder-space paths, the bias boost, a prompt prefix); and the
+"""GPU: step-wise decoding (wcb_decode_begin / wcb_decode_step) against generate() on the
+same clips: the same decode step one token per call, so the ids must be identical (greedy on the f32 K/V
+cross-attention and bf16 encoder-space paths, the bias boost, a prompt prefix; beam search with parents and
+the best finished sequences, also against the reference beam goldens); and the
 reference forward()'s encoder_outputs / past_key_values / use_cache arguments (wcb_forward_enc,
 wcb_forward_cached)."""
 import os
@@ -61,6 +62,42 @@ def test_stepwise_scores_lm_head_layernorm_split_bit_identical(size, dtype, B):
         del m
     assert torch.equal(out[0][0], out[1][0])
     assert torch.equal(out[0][1], out[1][1])
+
+
+# ---------------------------------------------------------------- step-wise beam search
+def _golden(size, recipe, seed):
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", f"model_{size}_{recipe}_s{seed}.npz"))
+    return g, eval(str(g["meta"][0]), {})
+
+
+@pytest.mark.parametrize("dtype,boost,prompt", [("f32", False, False), ("bf16", False, False), ("bf16", True, False),
+                                                ("bf16", True, True)])
+def test_stepwise_beam5_equals_generate(dtype, boost, prompt):
+    """Step-wise beam search (wcb_decode_begin_beams / wcb_decode_step / wcb_decode_parents /
+    wcb_decode_result) against generate(num_beams=5) ([tf] generation/utils.py:3208) on the
+    same clips: one HF beam iteration per step, so after the steps generate() takes the best finished
+    sequences are identical — on whisper-small's high-margin recipe also identical to the reference
+    model's own beam-5 goldens; with the 1000-phrase boost (lambda 2, EOS masked) and with a prompt
+    prefix against generate() with the same arguments. Every parent index lies in [0, 5)."""
+    dims = get_dims("small")
+    g, meta = _golden("small", "margin", 1)
+    m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=1, recipe="margin"), dtype=dtype)
+    B, L = meta["B"], meta["beam_len"]
+    x = torch.from_numpy(W.log_mel(synth_batch(B), dims.n_mel))
+    kw = dict(bias_list=synth_bias_list(1000, eot=dims.eos_token_id), bias_boost=2.0, min_new_tokens=L) if boost else {}
+    pr = [50360, 1000, 2000, 3000] if prompt else None
+    ref = m.generate(x, max_length=L, num_beams=5, prompt_ids=pr, **kw).cpu().numpy()
+    if not boost and not prompt:
+        assert np.array_equal(ref, g["beam5_ids"]), (ref, g["beam5_ids"])
+    dec = m.decode_begin(m.encode(x), num_beams=5, max_length=L, prompt_ids=pr, **kw)
+    for _ in range(L):
+        toks, scores = dec.step()
+        par = dec.parents().cpu().numpy()
+        assert toks.shape == (B * 5,) and ((par >= 0) & (par < 5)).all()
+        assert torch.isfinite(scores[::5]).all()
+    got = dec.result(L).cpu().numpy()
+    dec.close()
+    assert np.array_equal(got, ref), (got, ref)
 
 
 # ---------------------------------------------------------------- forward(encoder_outputs / past_key_values)

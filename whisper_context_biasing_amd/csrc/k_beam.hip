@@ -367,6 +367,7 @@ __global__ __launch_bounds__(256) void beam_step_kernel(BeamArgs a) {
     const int i = tid, k = sel[i];
     if (cur < a.T) a.phys[(long)(R0 + i) * a.T + cur] = R0 + i;   // the next step writes its own row
     a.next_ids[R0 + i] = tt[k];
+    if (a.parent) a.parent[R0 + i] = tb[k];
     a.run_sc[R0 + i] = rlp[k];
     a.state[R0 + i] = a.lam != 0.f ? ac_delta(a, st_old[tb[k]], tt[k]) : 0;
     const int m = fsrc[i];

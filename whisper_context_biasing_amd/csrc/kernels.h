@@ -254,6 +254,7 @@ struct BeamArgs {
   float* fin_sc = nullptr; int* fin_done = nullptr; int* fin_len = nullptr; int* fin_seq = nullptr;  // [B·nb](·(Lt-P))
   int* flags = nullptr;                                 // [B][2]: heuristic unsatisfied, all K hit
   int* out_ids = nullptr; int out_ld = 0; int* out_len = nullptr;
+  int* parent = nullptr;                                // [R] (nullable): the beam each running beam extends
 };
 void beam_init(const BeamArgs& a, hipStream_t s);
 void beam_select(const BeamArgs& a, hipStream_t s);   // per-row top-K + per-utterance step

@@ -1437,6 +1437,51 @@ void prefill_step(wcb_handle* h, StepCfg c, int np, const int* src, int ld) {
   add_i32(pos, np, D.hs);
 }
 
+// Beam-search state of decode context D (utterances B, nb beams each, R = B·nb rows): one buffer carved
+// into [R] running / finished scores, finished flags and lengths, [R][Lg] running and finished
+// sequences, [R][Tc] key map, [R][K] per-row candidates, [B][2] utterance flags, [R] parent beams.
+// ensure_beam_buf sizes it (draining the streams first when it grows); beam_args carves it.
+constexpr int kBeamBufs = 11;
+void beam_words(int B, int nb, int Lg, int Tc, size_t* w) {
+  const size_t R = (size_t)B * nb, K = 2 * (size_t)nb;
+  const size_t v[kBeamBufs] = {R, R, R, R, R * Lg, R * Lg, R * Tc, R * K, R * K, (size_t)B * 2, R};
+  std::copy(v, v + kBeamBufs, w);
+}
+void ensure_beam_buf(wcb_handle* h, DecCtx& D, int B, int nb, int Lg, int Tc) {
+  size_t w[kBeamBufs], bytes = 0;
+  beam_words(B, nb, Lg, Tc, w);
+  for (size_t x : w) bytes += (x * 4 + 255) / 256 * 256;
+  if (bytes > D.beam.bytes) { quiesce(h); D.beam.ensure(bytes); }
+}
+void beam_set_bias(BeamArgs& bm, const wcb_bias* bs) {
+  bm.root_bits = bs->root_bits.as<uint32_t>(); bm.root_child = bs->root_child.as<int>();
+  bm.trans_off = bs->trans_off.as<int>(); bm.trans_tok = bs->trans_tok.as<int>(); bm.trans_dst = bs->trans_dst.as<int>();
+  bm.st_depth = bs->st_depth.as<int>(); bm.st_keep = bs->st_keep.as<int>();
+}
+// Lt: the total length cap (prefix + max new tokens, MaxLength), Tc: cache positions, Lg: max new tokens
+BeamArgs beam_args(wcb_handle* h, DecCtx& D, int B, int nb, int P, int Lt, int Tc, int Lg, int min_new, float lam,
+                   const wcb_bias* bs) {
+  size_t w[kBeamBufs];
+  beam_words(B, nb, Lg, Tc, w);
+  char* p = (char*)D.beam.p;
+  auto take = [&](int i) { char* q = p; p += (w[i] * 4 + 255) / 256 * 256; return q; };
+  const int R = B * nb;
+  int* ints = D.ints.as<int>();
+  BeamArgs bm;
+  bm.run_sc = (float*)take(0); bm.fin_sc = (float*)take(1); bm.fin_done = (int*)take(2); bm.fin_len = (int*)take(3);
+  bm.run_seq = (int*)take(4); bm.fin_seq = (int*)take(5); bm.phys = (int*)take(6);
+  bm.cand_val = (float*)take(7); bm.cand_tok = (int*)take(8); bm.flags = (int*)take(9); bm.parent = (int*)take(10);
+  bm.logits = D.logits.as<float>(); bm.ld = h->vocab_pad; bm.V = h->d.vocab;
+  bm.B = B; bm.nb = nb; bm.K = 2 * nb; bm.P = P; bm.Lt = Lt; bm.T = Tc;
+  bm.eos = h->d.eos_token_id; bm.pad = h->d.pad_token_id; bm.min_new = min_new;
+  bm.lam = lam; bm.len_pen = 1.f;
+  beam_set_bias(bm, bs);
+  bm.step = ints + I_STEP; bm.pos = ints + I_POS; bm.all_done = ints + I_DONE; bm.ticket = ints + I_TICKET;
+  bm.next_ids = ints + I_NEXT; bm.state = ints + I_NEXT + R;
+  bm.out_ids = D.outbuf.as<int>(); bm.out_ld = Lg; bm.out_len = ints + I_UNFIN;
+  return bm;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1501,12 +1546,7 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     const int buf = h->gen_count++ % h->nctx;
     DecCtx& D = h->dc[buf];
     // beam state [R] / [R][max_new] / [R][Tc] / [R][K] / [B][2] in one buffer
-    const int K = 2 * nb, Lg = cfg->max_new_tokens;
-    const size_t beam_words[] = {(size_t)R, (size_t)R, (size_t)R, (size_t)R, (size_t)R * Lg, (size_t)R * Lg,
-                                 (size_t)R * Tc, (size_t)R * K, (size_t)R * K, (size_t)B * 2};
-    size_t beam_bytes = 0;
-    for (size_t w : beam_words) beam_bytes += (w * 4 + 255) / 256 * 256;
-    if (nb > 1 && beam_bytes > D.beam.bytes) { quiesce(h); D.beam.ensure(beam_bytes); }
+    if (nb > 1) ensure_beam_buf(h, D, B, nb, cfg->max_new_tokens, Tc);
     // ---- encoder stream: front end → encoder → cross-K/V into buffer `buf` once the decode that
     //      last read that buffer has finished. It overlaps the previous call's decode.
     sync_in(h, stream, h->he);
@@ -1532,21 +1572,7 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     }
     BeamArgs bm;
     if (nb > 1) {
-      char* p = (char*)D.beam.p;
-      auto take = [&](int i) { char* q = p; p += (beam_words[i] * 4 + 255) / 256 * 256; return q; };
-      bm.run_sc = (float*)take(0); bm.fin_sc = (float*)take(1); bm.fin_done = (int*)take(2); bm.fin_len = (int*)take(3);
-      bm.run_seq = (int*)take(4); bm.fin_seq = (int*)take(5); bm.phys = (int*)take(6);
-      bm.cand_val = (float*)take(7); bm.cand_tok = (int*)take(8); bm.flags = (int*)take(9);
-      bm.logits = D.logits.as<float>(); bm.ld = h->vocab_pad; bm.V = h->d.vocab;
-      bm.B = B; bm.nb = nb; bm.K = K; bm.P = P; bm.Lt = T; bm.T = Tc;
-      bm.eos = h->d.eos_token_id; bm.pad = h->d.pad_token_id; bm.min_new = cfg->min_new_tokens;
-      bm.lam = cfg->bias_boost; bm.len_pen = 1.f;
-      bm.root_bits = bs->root_bits.as<uint32_t>(); bm.root_child = bs->root_child.as<int>();
-      bm.trans_off = bs->trans_off.as<int>(); bm.trans_tok = bs->trans_tok.as<int>(); bm.trans_dst = bs->trans_dst.as<int>();
-      bm.st_depth = bs->st_depth.as<int>(); bm.st_keep = bs->st_keep.as<int>();
-      bm.step = ints + I_STEP; bm.pos = ints + I_POS; bm.all_done = ints + I_DONE; bm.ticket = ints + I_TICKET;
-      bm.next_ids = ints + I_NEXT; bm.state = ints + I_NEXT + R;
-      bm.out_ids = D.outbuf.as<int>(); bm.out_ld = out_ld; bm.out_len = ints + I_UNFIN;
+      bm = beam_args(h, D, B, nb, P, T, Tc, cfg->max_new_tokens, cfg->min_new_tokens, cfg->bias_boost, bs);
       beam_init(bm, D.hs);   // before the prefill: the self-attention reads keys through bm.phys
     }
     StepCfg sc{R, Tc, out_ld, buf, false, false, D.logits.as<float>(), (long)h->vocab_pad, bs, cfg->bias_boost,
@@ -1672,14 +1698,85 @@ struct wcb_state {
   int fwd = 0;   // positions appended by wcb_forward_cached (a forward-cache state takes no decode steps)
   float lam = 0.f;
   uint64_t bias_id = 0;
+  int nb = 1;    // beams per utterance (> 1: beam search, rows R = B·nb; the running beams in bm)
+  BeamArgs bm;
 };
+
+// step-wise beam search: the beam path of wcb_generate one step per call (begin: cross-K/V of the
+// given encoder output, beam state, causal prefill of the per-clip prefix on every beam row)
+static void decode_begin_beams(wcb_handle* h, const void* enc, int B, int nb, const int32_t* prefix, int prefix_len,
+                               int max_new_tokens, float bias_boost, int min_new_tokens, wcb_state** out, void* stream) {
+  REQUIRE(h && enc && out && B > 0 && B <= 64, "bad argument (1 <= B <= 64, enc and out required)");
+  if (!h->ready) throw WcbError(WCB_ERR_STATE, "weights not finalized");
+  REQUIRE(nb >= 2 && nb <= kMaxBeams, "num_beams must be in [1, 8]");
+  const int R = B * nb;
+  REQUIRE(R <= 64 * DecCtx::kMaxSub, "batch x num_beams > 512 rows: split the batch");
+  REQUIRE(h->nctx < wcb_handle::kMaxCtx, "step-wise decoding needs a free decode context (decode_contexts <= 3)");
+  REQUIRE(!h->step_state, "a step-wise decode is already active on this handle (wcb_decode_end first)");
+  REQUIRE(bias_boost >= 0.f && min_new_tokens >= 0 && max_new_tokens >= 1,
+          "bias_boost and min_new_tokens must be >= 0, max_new_tokens >= 1");
+  REQUIRE(bias_boost == 0.f || h->d.vocab <= kBeamMaxVocab, "beam search boost: vocabulary too large");
+  const int P = prefix ? prefix_len : 1;
+  REQUIRE(P >= 1 && P < h->d.n_text_ctx, "prefix_len must be in [1, max_target_positions)");
+  // generate(): the length cap is prefix + max_length, at most max_target_positions
+  const int Lt = std::min(P + max_new_tokens, h->d.n_text_ctx), max_new = Lt - P, Tc = Lt;
+  REQUIRE(Tc <= kBeamMaxLen, "beam search: more than 448 positions");
+  const int ci = wcb_handle::kMaxCtx - 1;
+  const int xm = h->beam_xmode;
+  ensure_dec_ws(h, B, R, Tc, max_new, xm, P > 1 ? R * std::min(prefill_chunk(R), P - 1) : R, ci, ci + 1);
+  DecCtx& D = h->dc[ci];
+  ensure_beam_buf(h, D, B, nb, max_new, Tc);
+  sync_in(h, stream, D.hs);
+  if (xm == 1) {
+    fill_xenc(h, ci, enc, B, D.hs);
+  } else {
+    sync_in(h, stream, h->he);
+    cross_kv(h, B, ci, enc);                        // on the encoder stream
+    HIPCHK(hipStreamSynchronize(h->he));
+  }
+  int* ints = D.ints.as<int>();
+  HIPCHK(hipMemsetAsync(ints, 0, (size_t)(I_NEXT + 4 * R) * 4, D.hs));
+  if (prefix) {   // per-clip prefixes [B][P] (host) on every beam row of the clip: [R][P]
+    std::vector<int32_t> rows((size_t)R * P);
+    for (int r = 0; r < R; ++r) std::copy(prefix + (size_t)(r / nb) * P, prefix + (size_t)(r / nb + 1) * P, rows.begin() + (size_t)r * P);
+    if (rows.size() * 4 > D.forced.bytes) { quiesce(h); D.forced.ensure(rows.size() * 4); }
+    HIPCHK(hipMemcpyAsync(D.forced.p, rows.data(), rows.size() * 4, hipMemcpyHostToDevice, D.hs));
+    HIPCHK(hipStreamSynchronize(D.hs));   // pageable host source
+  } else {
+    fill_i32(ints + I_NEXT, h->d.decoder_start_token_id, R, D.hs);
+  }
+  auto* st = new wcb_state;
+  st->h = h; st->B = B; st->P = P; st->T = Tc; st->max_new = max_new; st->min_new = min_new_tokens;
+  st->xmode = xm; st->lam = bias_boost; st->nb = nb;
+  st->bm = beam_args(h, D, B, nb, P, Lt, Tc, max_new, min_new_tokens, bias_boost, h->empty_bias.get());
+  beam_init(st->bm, D.hs);   // before the prefill: the self-attention reads keys through the key map
+  StepCfg sc{R, Tc, max_new, ci, false, false, D.logits.as<float>(), (long)h->vocab_pad, h->empty_bias.get(),
+             bias_boost, min_new_tokens, D.forced.as<int>(), P};
+  sc.clips = B;
+  sc.nb = nb;
+  sc.xmode = xm;
+  sc.phys = st->bm.phys;
+  for (int p0 = 0, np; p0 + 1 < P; p0 += np) {
+    np = std::min(prefill_chunk(R), P - 1 - p0);
+    prefill_step(h, sc, np, D.forced.as<int>(), P);
+  }
+  if (prefix) gather_col(ints + I_NEXT, D.forced.as<int>(), R, P, P - 1, D.hs);
+  HIPCHK(hipStreamSynchronize(D.hs));
+  h->step_state = st;
+  *out = st;
+  sync_out(h, stream, D.hs);
+}
 
 int wcb_decode_begin(wcb_handle* h, const void* enc, int B, int num_beams, const int32_t* prefix, int prefix_len,
                      float bias_boost, int min_new_tokens, wcb_state** out, void* stream) {
   return guarded(h, [&] {
     REQUIRE(h && enc && out && B > 0 && B <= 64, "bad argument (1 <= B <= 64, enc and out required)");
     if (!h->ready) throw WcbError(WCB_ERR_STATE, "weights not finalized");
-    REQUIRE(num_beams == 1, "step-wise decoding is greedy: beam search reorders past tokens, use wcb_generate");
+    if (num_beams != 1) {   // beam search to the default length cap (generate()'s max_length 448)
+      if (num_beams < 1) throw WcbError(WCB_ERR_ARG, "num_beams must be >= 1");
+      return decode_begin_beams(h, enc, B, num_beams, prefix, prefix_len, h->d.n_text_ctx, bias_boost, min_new_tokens, out,
+                                stream);
+    }
     REQUIRE(h->nctx < wcb_handle::kMaxCtx, "step-wise decoding needs a free decode context (decode_contexts <= 3)");
     REQUIRE(!h->step_state, "a step-wise decode is already active on this handle (wcb_decode_end first)");
     REQUIRE(bias_boost >= 0.f && min_new_tokens >= 0, "bias_boost and min_new_tokens must be >= 0");
@@ -1739,16 +1836,68 @@ int wcb_decode_step(wcb_handle* h, wcb_state* st, const wcb_bias* bias, int32_t*
     const int ci = wcb_handle::kMaxCtx - 1;
     DecCtx& D = h->dc[ci];
     sync_in(h, stream, D.hs);
-    StepCfg sc{st->B, st->T, st->max_new, ci, true, true, D.logits.as<float>(), (long)h->vocab_pad, bs, st->lam,
+    const int R = st->B * st->nb;
+    StepCfg sc{R, st->T, st->max_new, ci, true, true, D.logits.as<float>(), (long)h->vocab_pad, bs, st->lam,
                st->min_new, D.forced.as<int>(), 0};
     sc.clips = st->B;
     sc.xmode = st->xmode;
     sc.host_pos = st->P - 1 + st->steps;
-    sc.score_out = scores;
+    if (st->nb > 1) {   // beam step: the running beams' new tokens, their scores (running log-prob sums)
+      beam_set_bias(st->bm, bs);
+      sc.nb = st->nb;
+      sc.phys = st->bm.phys;
+      sc.beam = &st->bm;
+    } else {
+      sc.score_out = scores;
+    }
     decode_step(h, sc);
-    HIPCHK(hipMemcpyAsync(next_ids, D.ints.as<int>() + I_NEXT, (size_t)st->B * 4, hipMemcpyDeviceToDevice, D.hs));
+    HIPCHK(hipMemcpyAsync(next_ids, D.ints.as<int>() + I_NEXT, (size_t)R * 4, hipMemcpyDeviceToDevice, D.hs));
+    if (st->nb > 1 && scores)
+      HIPCHK(hipMemcpyAsync(scores, st->bm.run_sc, (size_t)R * 4, hipMemcpyDeviceToDevice, D.hs));
     st->bias_id = bs->id;
     ++st->steps;
+    sync_out(h, stream, D.hs);
+  });
+}
+
+int wcb_decode_begin_beams(wcb_handle* h, const void* enc, int B, int num_beams, const int32_t* prefix, int prefix_len,
+                           int max_new_tokens, float bias_boost, int min_new_tokens, wcb_state** out, void* stream) {
+  return guarded(h, [&] {
+    REQUIRE(num_beams >= 2, "wcb_decode_begin_beams: num_beams must be >= 2 (greedy: wcb_decode_begin)");
+    decode_begin_beams(h, enc, B, num_beams, prefix, prefix_len, max_new_tokens, bias_boost, min_new_tokens, out, stream);
+  });
+}
+
+int wcb_decode_parents(wcb_handle* h, wcb_state* st, int32_t* parents, void* stream) {
+  return guarded(h, [&] {
+    REQUIRE(h && st && st->h == h && h->step_state == st && parents, "bad argument (state of this handle, parents)");
+    REQUIRE(st->nb > 1, "wcb_decode_parents: not a beam-search state");
+    REQUIRE(st->steps > 0, "wcb_decode_parents: no step taken yet");
+    DecCtx& D = h->dc[wcb_handle::kMaxCtx - 1];
+    sync_in(h, stream, D.hs);
+    HIPCHK(hipMemcpyAsync(parents, st->bm.parent, (size_t)st->B * st->nb * 4, hipMemcpyDeviceToDevice, D.hs));
+    sync_out(h, stream, D.hs);
+  });
+}
+
+int wcb_decode_result(wcb_handle* h, wcb_state* st, int32_t* out_ids, int32_t* out_steps, void* stream) {
+  return guarded(h, [&] {
+    REQUIRE(h && st && st->h == h && h->step_state == st && out_ids && out_steps, "bad argument");
+    REQUIRE(st->fwd == 0, "wcb_decode_result on a forward cache (wcb_forward_cached state)");
+    DecCtx& D = h->dc[wcb_handle::kMaxCtx - 1];
+    int* ints = D.ints.as<int>();
+    sync_in(h, stream, D.hs);
+    int n = st->steps;
+    if (st->nb > 1) {   // the best finished sequence of every utterance so far (generate()'s beam output)
+      HIPCHK(hipMemsetAsync(ints + I_UNFIN, 0, 4, D.hs));
+      beam_output(st->bm, D.hs);
+      int olen = 0;
+      HIPCHK(hipMemcpyAsync(&olen, ints + I_UNFIN, 4, hipMemcpyDeviceToHost, D.hs));
+      HIPCHK(hipStreamSynchronize(D.hs));
+      n = std::min(olen, st->max_new);
+    }
+    HIPCHK(hipMemcpyAsync(out_ids, D.outbuf.p, (size_t)st->B * st->max_new * 4, hipMemcpyDeviceToDevice, D.hs));
+    *out_steps = n;
     sync_out(h, stream, D.hs);
   });
 }

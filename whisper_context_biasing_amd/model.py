@@ -88,19 +88,39 @@ class BiasList:
 
 
 class StepDecoder:
-    """One step-wise greedy decode (WhisperCB.decode_begin): step() -> (next ids [B] int32, scores [B]
-    f32: the chosen token's logit + bias boost), both on the model's device; close() ends it."""
+    """One step-wise decode (WhisperCB.decode_begin). Greedy: step() -> (next ids [B] int32, scores [B] f32:
+    the chosen token's logit + bias boost). Beam search (num_beams = nb > 1): step() -> (the token each
+    running beam appended [B·nb] int32, the running log-prob sums [B·nb] f32), parents() -> [B·nb] int32,
+    the beam (0..nb-1 of the same clip) each running beam extends. result() -> generate()'s output for the
+    steps taken (beams: the best finished sequence of every clip so far). All on the model's device;
+    close() ends the decode."""
 
-    def __init__(self, model, st, B, bias):
-        self.model, self._st, self.B, self._bias = model, st, B, bias
+    def __init__(self, model, st, B, bias, num_beams=1):
+        self.model, self._st, self.B, self._bias, self.num_beams = model, st, B, bias, num_beams
 
     def step(self):
         m = self.model
-        ids = torch.empty(self.B, dtype=torch.int32, device=m.device)
-        sc = torch.empty(self.B, dtype=torch.float32, device=m.device)
+        R = self.B * self.num_beams
+        ids = torch.empty(R, dtype=torch.int32, device=m.device)
+        sc = torch.empty(R, dtype=torch.float32, device=m.device)
         _lib.check(m._lib.wcb_decode_step(m._h, self._st, self._bias._h if self._bias else None, _ptr(ids), _ptr(sc),
                                           _stream(m.device)), m._h, "wcb_decode_step")
         return ids, sc
+
+    def parents(self):
+        m = self.model
+        par = torch.empty(self.B * self.num_beams, dtype=torch.int32, device=m.device)
+        _lib.check(m._lib.wcb_decode_parents(m._h, self._st, _ptr(par), _stream(m.device)), m._h, "wcb_decode_parents")
+        return par
+
+    def result(self, max_new: int):
+        """[B, n] int64 ids as generate() returns them (Whisper-trimmed), n = the generated columns."""
+        m = self.model
+        out = torch.empty(self.B, max_new, dtype=torch.int32, device=m.device)
+        n = C.c_int32(0)
+        _lib.check(m._lib.wcb_decode_result(m._h, self._st, _ptr(out), C.byref(n), _stream(m.device)), m._h,
+                   "wcb_decode_result")
+        return m._whisper_trim(out[:, :n.value].to(torch.int64))
 
     def close(self):
         if self._st:
@@ -436,10 +456,12 @@ class WhisperCB:
         return self._whisper_trim(ids)
 
     def decode_begin(self, encoder_outputs, prompt_ids=None, bias_list=None, bias_boost: float = 0.0,
-                     min_new_tokens: int = 0) -> "StepDecoder":
-        """Step-wise greedy decoding from an encoder output [B, 1500, d] (this model's dtype, on its device):
-        the streaming form of generate() (wcb_decode_begin). `prompt_ids` = one prompt for every row or
-        a [B, P] array of per-row prompts (decoder_start_token_id is appended as generate() does)."""
+                     min_new_tokens: int = 0, num_beams: int = 1, max_length: Optional[int] = None) -> "StepDecoder":
+        """Step-wise decoding from an encoder output [B, 1500, d] (this model's dtype, on its device): the
+        streaming form of generate() (wcb_decode_begin / wcb_decode_begin_beams). Greedy (num_beams = 1) or
+        beam search (num_beams 2..8; `max_length` = generate()'s, the beams' length cap: None = the
+        max_target_positions cap). `prompt_ids` = one prompt for every clip or a [B, P] array of per-clip
+        prompts (decoder_start_token_id is appended as generate() does)."""
         enc = self._encoder_state(encoder_outputs)   # [B, 1500, d] checked: the library copies B·1500·d
         B = enc.shape[0]
         if B > 64:
@@ -459,10 +481,18 @@ class WhisperCB:
         else:
             bl = self.bias_list(bias_list) if (bias_list and bias_boost > 0) else None
         st = C.c_void_p()
-        _lib.check(self._lib.wcb_decode_begin(self._h, _ptr(enc), B, 1, pre.ctypes.data if pre is not None else None,
-                                              pre.shape[1] if pre is not None else 1, float(bias_boost), int(min_new_tokens),
-                                              C.byref(st), _stream(self.device)), self._h, "wcb_decode_begin")
-        return StepDecoder(self, st, B, bl)
+        nb = int(num_beams)
+        if nb > 1 and max_length is not None:
+            _lib.check(self._lib.wcb_decode_begin_beams(self._h, _ptr(enc), B, nb, pre.ctypes.data if pre is not None else None,
+                                                        pre.shape[1] if pre is not None else 1, int(max_length),
+                                                        float(bias_boost), int(min_new_tokens), C.byref(st),
+                                                        _stream(self.device)), self._h, "wcb_decode_begin_beams")
+        else:
+            _lib.check(self._lib.wcb_decode_begin(self._h, _ptr(enc), B, nb, pre.ctypes.data if pre is not None else None,
+                                                  pre.shape[1] if pre is not None else 1, float(bias_boost),
+                                                  int(min_new_tokens), C.byref(st), _stream(self.device)), self._h,
+                       "wcb_decode_begin")
+        return StepDecoder(self, st, B, bl, nb)
 
     @staticmethod
     def max_clips_per_call(num_beams: int = 1) -> int:
