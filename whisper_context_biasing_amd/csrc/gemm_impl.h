@@ -1407,6 +1407,7 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   static_assert(R * 4 <= NT, "epilogue: 4 columns per thread");
   __shared__ __attribute__((aligned(16))) float red[NW][R][17];
   __shared__ float2 rst[LN ? NW : 1][LN ? R : 1];
+  __shared__ __attribute__((aligned(16))) float lnp[LN ? 2 * K : 4];   // γ [K], β [K]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ct = blockIdx.x, mb = blockIdx.y * R, n0 = ct * 16;
   const int kb = wave * (KPW * 32) + 8 * (lane >> 4);
@@ -1439,14 +1440,13 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
       for (int ks = 0; ks < KPW; ++ks) a[i][ks] = load_frag<T>(ar + ks * 32);
     }
   }
-  f32x4 lg[LN ? KPW : 1][2], lb[LN ? KPW : 1][2];
+  // LayerNorm γ / β: into LDS by LDS-DMA with the burst (one 16-byte piece per lane, K / 4 lanes each), read
+  // per k-step after the statistics barrier (held in registers they took 2·KPW·8 floats per lane and kept
+  // the LN-fused instances at one workgroup per CU)
   if constexpr (LN) {
-#pragma unroll
-    for (int ks = 0; ks < KPW; ++ks) {
-      lg[ks][0] = *reinterpret_cast<const f32x4*>(p.gam + kb + ks * 32);
-      lg[ks][1] = *reinterpret_cast<const f32x4*>(p.gam + kb + ks * 32 + 4);
-      lb[ks][0] = *reinterpret_cast<const f32x4*>(p.bet + kb + ks * 32);
-      lb[ks][1] = *reinterpret_cast<const f32x4*>(p.bet + kb + ks * 32 + 4);
+    for (int c = wave * 64; c < K / 4; c += NT) {   // (K / 4 is a multiple of 64: wave-uniform)
+      glds16(p.gam + 4 * (c + lane), lnp + 4 * c);
+      glds16(p.bet + 4 * (c + lane), lnp + K + 4 * c);
     }
   }
   // epilogue operands: thread → row er (local), columns ec .. ec + 3
@@ -1478,7 +1478,12 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   if (p.stamp) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); t1 = stamp_now(); }
   // ---------------- LayerNorm of the A rows (gemm_dec_kernel AM = 2 arithmetic)
   if constexpr (LN) {
-    float xv[MF][KPW][8];
+    // (the f32 value of an element is re-derived from its 16-bit bits where needed: exact, no copy kept)
+    auto xf = [&](int i, int ks, int e) -> float {
+      if constexpr (__is_same(T, bf16_t)) return bf16_to_f((bf16_t)a[i][ks][e]);
+      else return float(a[i][ks][e]);
+    };
+    float mean[MF], rstd[MF];
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
       float s1 = 0.f, s2 = 0.f;
@@ -1486,10 +1491,7 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
       for (int ks = 0; ks < KPW; ++ks) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float v;
-          if constexpr (__is_same(T, bf16_t)) v = bf16_to_f((bf16_t)a[i][ks][e]);
-          else v = float(a[i][ks][e]);
-          xv[i][ks][e] = v;
+          const float v = xf(i, ks, e);
           s1 += v;
           s2 = fmaf(v, v, s2);
         }
@@ -1498,20 +1500,28 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
       s1 = xor32_add(s1); s2 = xor32_add(s2);
       if (lane < 16) rst[wave][i * 16 + lane] = float2{s1, s2};
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's γ / β pieces landed (LDS-DMA)
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int q = 0; q < NW; ++q) { const float2 t = rst[q][i * 16 + (lane & 15)]; s1 += t.x; s2 += t.y; }
-      const float mean = s1 / K;
-      const float rstd = rsqrtf(fmaxf(s2 / K - mean * mean, 0.f) + 1e-5f);
+      mean[i] = s1 / K;
+      rstd[i] = rsqrtf(fmaxf(s2 / K - mean[i] * mean[i], 0.f) + 1e-5f);
+    }
 #pragma unroll
-      for (int ks = 0; ks < KPW; ++ks) {
+    for (int ks = 0; ks < KPW; ++ks) {
+      const f32x4 g0 = *reinterpret_cast<const f32x4*>(lnp + kb + ks * 32);
+      const f32x4 g1 = *reinterpret_cast<const f32x4*>(lnp + kb + ks * 32 + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(lnp + K + kb + ks * 32);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(lnp + K + kb + ks * 32 + 4);
+#pragma unroll
+      for (int i = 0; i < MF; ++i) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float gw = lg[ks][e >> 2][e & 3], gb = lb[ks][e >> 2][e & 3];
-          const float v = (xv[i][ks][e] - mean) * rstd * gw + gb;
+          const float gw = e < 4 ? g0[e] : g1[e - 4], gb = e < 4 ? b0[e] : b1[e - 4];
+          const float v = (xf(i, ks, e) - mean[i]) * rstd[i] * gw + gb;
           a[i][ks][e] = __builtin_bit_cast(typename std::remove_reference<decltype(a[0][0][0])>::type, DT<T>::fromf(v));
         }
       }

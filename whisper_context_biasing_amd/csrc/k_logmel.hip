@@ -6,7 +6,8 @@
 //
 // logmel_power_mel_kernel: one workgroup = 64 frames of one clip. The 10,480-sample window span is
 // staged once in LDS (reflect padding resolved at load), the windowed 400-point real DFT runs as
-// an exact-f32 MFMA product (v_mfma_f32_16x16x4_f32) of the frame matrix with a [416 × 416] table
+// an exact-f32 MFMA product (v_mfma_f32_16x16x4_f32; each wave: the 64 frames x a quarter of the
+// columns) of the frame matrix with a [416 × 416] table
 // whose columns interleave (cos, −sin) per bin, so |X|² of a bin is lane ⊕ 1 in the accumulator
 // (one shuffle). Power goes to LDS, the sparse mel filters are applied from it, log10 is written
 // and the clip maximum reduced with one atomicMax (order-preserving int encoding of the float).
@@ -49,35 +50,50 @@ __global__ __launch_bounds__(256) void logmel_power_mel_kernel(const float* __re
     lds[i] = j < nv ? x[j] : 0.f;
   }
   __syncthreads();
-  // DFT: wave handles frames f0 + wave*16 .. +15; acc over 26 column fragments
-  f32x4 acc[26];
+  // DFT: every wave takes all 64 frames of the workgroup (4 row fragments) against its share of the 26
+  // column fragments (7, 7, 6, 6): each table fragment read from L2 feeds 4 row fragments (the earlier
+  // split, 16 frames x all 26 column fragments per wave, re-read the 692 KB table 4x as often). The K
+  // order of every output element is unchanged: bit-identical.
+  constexpr int kCF = 26, kCW = 7;                       // column fragments, per wave (at most)
+  const int cf0 = wave < 2 ? wave * kCW : 2 * kCW + (wave - 2) * (kCW - 1);
+  const int ncf = wave < 2 ? kCW : kCW - 1;
+  f32x4 acc[4][kCW];
 #pragma unroll
-  for (int j = 0; j < 26; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int fl = wave * 16 + (lane & 15);
-  const float* arow = lds + fl * kHop + 8 * (lane >> 4);
-  const float* brow = dft + (lane & 15) * kNCol + 8 * (lane >> 4);
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < kCW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* brow = dft + (long)(cf0 * 16 + (lane & 15)) * kNCol + 8 * (lane >> 4);
   for (int kb = 0; kb < kNCol; kb += 32) {
-    f32x8 a;
+    f32x8 a[4];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) a[e] = arow[kb + e];
+    for (int i = 0; i < 4; ++i) {
+      const float* arow = lds + (i * 16 + (lane & 15)) * kHop + 8 * (lane >> 4) + kb;
 #pragma unroll
-    for (int j = 0; j < 26; ++j) {
-      const f32x8 bf = *reinterpret_cast<const f32x8*>(brow + (long)j * 16 * kNCol + kb);
-      acc[j] = mma16(a, bf, acc[j]);
+      for (int e = 0; e < 8; ++e) a[i][e] = arow[e];
+    }
+#pragma unroll
+    for (int j = 0; j < kCW; ++j) {
+      if (j < ncf) {
+        const f32x8 bf = *reinterpret_cast<const f32x8*>(brow + (long)j * 16 * kNCol + kb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] = mma16(a[i], bf, acc[i][j]);
+      }
     }
   }
   __syncthreads();   // samples no longer needed: reuse LDS for the power spectrum
-  // acc[j][e]: frame row (lane>>4)*4+e of this wave, column 16j + (lane&15): even = re, odd = im
+  // acc[i][j][e]: frame row 16i + (lane>>4)*4 + e, column 16(cf0 + j) + (lane&15): even = re, odd = im
 #pragma unroll
-  for (int j = 0; j < 26; ++j)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float v = acc[j][e];
-      const float p = v * v + __shfl_xor(v, 1, 64) * __shfl_xor(v, 1, 64);
-      const int col = j * 16 + (lane & 15);
-      if ((col & 1) == 0 && (col >> 1) < kBins)
-        lds[(wave * 16 + (lane >> 4) * 4 + e) * kPowLd + (col >> 1)] = p;
-    }
+    for (int j = 0; j < kCW; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = acc[i][j][e];
+        const float p = v * v + __shfl_xor(v, 1, 64) * __shfl_xor(v, 1, 64);
+        const int col = (cf0 + j) * 16 + (lane & 15);
+        if (j < ncf && (col & 1) == 0 && (col >> 1) < kBins)
+          lds[(i * 16 + (lane >> 4) * 4 + e) * kPowLd + (col >> 1)] = p;
+      }
   __syncthreads();
   // mel + log10: thread -> (mel m, frame f) with frames fastest (coalesced output rows)
   float lmax = -INFINITY;

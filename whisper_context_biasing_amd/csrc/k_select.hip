@@ -60,9 +60,13 @@ __global__ __launch_bounds__(256) void select_partial_kernel(SelectArgs a) {
 }
 
 // One wave per row; the last row to finish (atomic ticket) advances the step/position counters.
+// EMB: the row's next-step input embedding in the same launch (k_norm.hip embed_kernel's arithmetic and
+// stats grouping, 64 columns per pass).
+template <typename T, bool EMB>
 __global__ __launch_bounds__(64) void select_finalize_kernel(SelectArgs a) {
   const int m = blockIdx.x, lane = threadIdx.x;
   const int step = *a.step;
+  const int pos0 = EMB ? *a.pos : 0;   // read before this row's ticket: the last arriver advances it
   const bool mask_eos = step < a.min_new;
   float bv = -INFINITY;
   int bi = 0x7fffffff;
@@ -100,6 +104,47 @@ __global__ __launch_bounds__(64) void select_finalize_kernel(SelectArgs a) {
     if (a.trans_tok[t] == tok) dst = a.trans_dst[t];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) dst = max(dst, __shfl_xor(dst, o, 64));
+  if constexpr (EMB) {
+    // 8 consecutive columns per lane (16-byte accesses of T; the fragment-major copy holds them
+    // contiguously too), the optional per-st_w-column partials in embed_kernel's lane-butterfly order
+    const int d = a.d, p = min(pos0 + 1, a.n_pos - 1);
+    const T* er = reinterpret_cast<const T*>(a.emb) + (long)tok * d;
+    const T* pr = reinterpret_cast<const T*>(a.pemb) + (long)p * d;
+    if (a.st) {   // (older skinny consumers only) one column per lane, as embed_kernel
+      for (int c0 = 0; c0 < d; c0 += 64) {
+        const int c = c0 + lane;
+        const float v = DT<T>::tof(er[c]) + DT<T>::tof(pr[c]);
+        float s1 = v, s2 = v * v;
+        if (a.st_w == 32) {
+#pragma unroll
+          for (int o = 1; o < 32; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+        } else {
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+        }
+        if ((c & (a.st_w - 1)) == 0) {
+          a.st[((long)m * (d / a.st_w) + c / a.st_w) * 2] = s1;
+          a.st[((long)m * (d / a.st_w) + c / a.st_w) * 2 + 1] = s2;
+        }
+      }
+    }
+    for (int c = lane * 8; c < d; c += 512) {   // (d % 8 == 0)
+      float v[8];
+      float ev[8], pv[8];
+      load8f<T>(er + c, ev);
+      load8f<T>(pr + c, pv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = ev[e] + pv[e];
+      float* xr = a.x + (long)m * d + c;
+      *reinterpret_cast<f32x4*>(xr) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(xr + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      if (a.x16) store8<T>(reinterpret_cast<T*>(a.x16) + (long)m * d + c, v);
+      if (a.x16fm) {
+        const int kw = a.fm_kpw * 32, w2 = c / kw, ks2 = (c % kw) >> 5, lg = (c & 31) >> 3;
+        store8<T>(reinterpret_cast<T*>(a.x16fm) + ((((long)(m >> 4) * a.fm_nw + w2) * a.fm_kpw + ks2) * 64 + lg * 16 + (m & 15)) * 8, v);
+      }
+    }
+  }
   if (lane == 0) {
     if (dst < 0) dst = (tok >= 0 && tok < a.V && a.root_child[tok] >= 0) ? a.root_child[tok] : 0;
     a.state[m] = dst;
@@ -173,12 +218,20 @@ void write_i32(int* dst, const int* host_src, int n, hipStream_t s) {
 }
 
 void select_finalize(const SelectArgs& a, hipStream_t s) {
-  WCB_LAUNCH(select_finalize_kernel, dim3(a.M), dim3(64), 0, s, a);
+  if (!a.emb) {
+    WCB_LAUNCH((select_finalize_kernel<float, false>), dim3(a.M), dim3(64), 0, s, a);
+  } else if (a.dtype == kBF16) {
+    WCB_LAUNCH((select_finalize_kernel<bf16_t, true>), dim3(a.M), dim3(64), 0, s, a);
+  } else if (a.dtype == kF16) {
+    WCB_LAUNCH((select_finalize_kernel<f16_t, true>), dim3(a.M), dim3(64), 0, s, a);
+  } else {
+    WCB_LAUNCH((select_finalize_kernel<float, true>), dim3(a.M), dim3(64), 0, s, a);
+  }
 }
 
 void select_greedy(const SelectArgs& a, hipStream_t s) {
   WCB_LAUNCH(select_partial_kernel, dim3(a.nchunk, a.M), dim3(256), 0, s, a);
-  WCB_LAUNCH(select_finalize_kernel, dim3(a.M), dim3(64), 0, s, a);
+  select_finalize(a, s);
 }
 
 }  // namespace wcb

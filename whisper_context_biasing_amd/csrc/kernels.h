@@ -226,6 +226,13 @@ struct SelectArgs {
   int* all_done = nullptr;
   unsigned long long* ticket_unfin = nullptr;   // arrivals | unfinished << 32, zero between steps (reset by the last row)
   float* out_score = nullptr;        // optional: the chosen token's (boosted) logit per row (0 for finished rows)
+  // the next step's embedding written by the finalize (emb non-null; DType dtype): x [M][d] f32 =
+  // emb[tok] + pemb[min(pos + 1, n_pos - 1)], its T copy x16, the fragment-major T copy x16fm (fm_nw,
+  // fm_kpw; nullable) and the per-st_w-column (Σx, Σx²) partials st (nullable) — embed()'s outputs bit
+  // for bit, one launch fewer per step
+  const void* emb = nullptr; const void* pemb = nullptr; int n_pos = 0, d = 0, dtype = 0;
+  float* x = nullptr; void* x16 = nullptr; void* x16fm = nullptr; int fm_nw = 0, fm_kpw = 0;
+  float* st = nullptr; int st_w = 16;
 };
 void select_greedy(const SelectArgs& a, hipStream_t s);          // vocabulary pass + finalize
 void select_finalize(const SelectArgs& a, hipStream_t s);        // partials already written (fused LM head)

@@ -1103,6 +1103,9 @@ struct StepCfg {
   const BeamArgs* beam = nullptr;      // beam search selection (replaces the greedy select)
   int rps = 1;                         // positions per decoder row in this pass (> 1: causal prefill)
   float* score_out = nullptr;          // greedy select: the chosen token's (boosted) logit per row (step-wise API)
+  // greedy: the step's input embedding was written by the previous step's select_finalize (or by
+  // step_embed before the first step), and this step's finalize writes the next one
+  bool embedded = false;
 };
 
 // the residual's fragment-major copy applies (lean path): the lean LayerNorm table covers d, every
@@ -1358,18 +1361,27 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
 // whose layer chains run on separate streams (fork/join events, captured into the same graph) so
 // the latency-bound projections of one group overlap the HBM-bound cross-attention of another;
 // token selection (or teacher forcing) joins them.
+// the decode step's input embedding (next_ids at the device position) into the residual rows, their
+// 16-bit copies and LayerNorm partials
+void step_embed(wcb_handle* h, const StepCfg& c) {
+  DecCtx& D = h->dc[c.buf];
+  const int d = h->d.d_model, B = c.B;
+  int* ints = D.ints.as<int>();
+  const bool r32 = h->dec_gemm && lnf_possible(h);   // 32-column stats for the folded LayerNorm (rows > 64)
+  h->timed("dec_embed", 0, (double)B * d * (2.0 * esize(h->d.dtype) + 4), D.hs, [&] {
+    embed(h->dt, h->tok_emb, h->dec_pos, ints + I_NEXT, ints + I_POS, D.dx.as<float>(),
+          !h->dec_gemm ? D.dstats.as<float>() : r32 ? D.drst.as<float>() : nullptr, B, d, D.hs, D.dx16.p, h->d.vocab, 1,
+          r32 ? 32 : 16, xfm_possible(h) ? D.dx16fm.p : nullptr);
+  });
+}
+
 void decode_step(wcb_handle* h, const StepCfg& c) {
   DecCtx& D = h->dc[c.buf];
   const int d = h->d.d_model, B = c.B;
   int* ints = D.ints.as<int>();
   int* pos = ints + I_POS;
   int* next_ids = ints + I_NEXT;
-  const bool r32 = h->dec_gemm && lnf_possible(h);   // 32-column stats for the folded LayerNorm (rows > 64)
-  h->timed("dec_embed", 0, (double)B * d * (2.0 * esize(h->d.dtype) + 4), D.hs, [&] {
-    embed(h->dt, h->tok_emb, h->dec_pos, next_ids, pos, D.dx.as<float>(),
-          !h->dec_gemm ? D.dstats.as<float>() : r32 ? D.drst.as<float>() : nullptr, B, d, D.hs, D.dx16.p, h->d.vocab, 1,
-          r32 ? 32 : 16, xfm_possible(h) ? D.dx16fm.p : nullptr);
-  });
+  if (!c.embedded) step_embed(h, c);
   // rows per chain: the skinny projections split rows over grid.y, so a chain can take any number
   // of rows (WCB_GROUP_ROWS; more chains overlap latency, fewer re-read the weights less often)
   const int ngrp = (B + h->group_rows - 1) / h->group_rows;
@@ -1407,6 +1419,18 @@ void decode_step(wcb_handle* h, const StepCfg& c) {
     s.all_done = ints + I_DONE;
     s.ticket_unfin = reinterpret_cast<unsigned long long*>(ints + I_TU);
     s.out_score = c.score_out;
+    if (c.embedded) {   // the next step's input embedding in the same launch (embed()'s outputs)
+      const bool r32 = h->dec_gemm && lnf_possible(h);
+      s.emb = h->tok_emb; s.pemb = h->dec_pos; s.n_pos = h->d.n_text_ctx; s.d = d; s.dtype = h->dt;
+      s.x = D.dx.as<float>(); s.x16 = D.dx16.p;
+      // (greedy decodes <= 64 rows: the decode-GEMM consumers compute their own LayerNorm statistics, so
+      // the 32-column partials of the > 64-row folded path are not published; the older skinny consumers
+      // still read 16-column ones)
+      s.st = !h->dec_gemm ? D.dstats.as<float>() : nullptr; s.st_w = 16;
+      (void)r32;
+      int nw = 0, kpw = 0;
+      if (xfm_possible(h) && lean_cfg(d, nw, kpw)) { s.x16fm = D.dx16fm.p; s.fm_nw = nw; s.fm_kpw = kpw; }
+    }
     h->timed("dec_select", 0, (double)B * D.nchunk * 8, D.hs, [&] { select_finalize(s, D.hs); });
   } else {
     advance_forced(next_ids, c.forced, B, c.forced_ld, pos, D.hs);
@@ -1590,6 +1614,10 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     if (P > 1) gather_col(ints + I_NEXT, D.forced.as<int>(), R, 0, P - 1, D.hs);
     sc.lm_head = true;
     sc.select = true;
+    if (nb == 1) {   // greedy: every step's finalize embeds the next step's input; the first one here
+      sc.embedded = true;
+      step_embed(h, sc);
+    }
     char key[256];
     snprintf(key, sizeof key, "%d/%d/%d/%d/%llu/%a/%d/%d/%d/%d", B, nb, Tc, out_ld, (unsigned long long)bs->id,
              cfg->bias_boost, cfg->min_new_tokens, h->n_sub, (int)h->prof_stamps, P);
@@ -1814,6 +1842,7 @@ int wcb_decode_begin(wcb_handle* h, const void* enc, int B, int num_beams, const
       prefill_step(h, sc, np, D.forced.as<int>(), P);
     }
     if (prefix) gather_col(ints + I_NEXT, D.forced.as<int>(), B, P, P - 1, D.hs);
+    step_embed(h, sc);   // the first step's input (every step's finalize embeds the next one)
     HIPCHK(hipStreamSynchronize(D.hs));
     auto* st = new wcb_state;
     st->h = h; st->B = B; st->P = P; st->T = T; st->max_new = max_new; st->min_new = min_new_tokens;
@@ -1849,6 +1878,7 @@ int wcb_decode_step(wcb_handle* h, wcb_state* st, const wcb_bias* bias, int32_t*
       sc.beam = &st->bm;
     } else {
       sc.score_out = scores;
+      sc.embedded = true;   // (wcb_decode_begin embedded the first input; each finalize embeds the next)
     }
     decode_step(h, sc);
     HIPCHK(hipMemcpyAsync(next_ids, D.ints.as<int>() + I_NEXT, (size_t)R * 4, hipMemcpyDeviceToDevice, D.hs));

@@ -16,22 +16,28 @@ WCB_DEV void self_attn_wave(const T* q, const T* k0, const T* v0, int cap, NK&& 
   const int lane = threadIdx.x & 63, seg = lane & 7, kg = lane >> 3;
   const T* kb = k0 + seg * 8;
   const T* vb = v0 + seg * 8;
-  auto ld8 = [&](const T* p, float* v) { load8f<T>(p, v); };
-  float qv[8], kv[8][8], vv[8][8];
-  ld8(q + seg * 8, qv);
+  // K / V stay in their 16-bit bits until use (converted per product: exact), q in f32
+  using Frag = typename DT<T>::frag;
+  auto cv = [](const Frag& f, int e) -> float {
+    if constexpr (__is_same(T, bf16_t)) return bf16_to_f((bf16_t)f[e]);
+    else return float(f[e]);
+  };
+  float qv[8];
+  Frag kv[8], vv[8];
+  load8f<T>(q + seg * 8, qv);
 #pragma unroll
-  for (int u = 0; u < 8; ++u) ld8(kb + (long)min(u * 8 + kg, cap) * 64, kv[u]);
+  for (int u = 0; u < 8; ++u) kv[u] = load_frag<T>(kb + (long)min(u * 8 + kg, cap) * 64);
 #pragma unroll
-  for (int u = 0; u < 8; ++u) ld8(vb + (long)min(u * 8 + kg, cap) * 64, vv[u]);
+  for (int u = 0; u < 8; ++u) vv[u] = load_frag<T>(vb + (long)min(u * 8 + kg, cap) * 64);
   const int nk = nkeys();
   float m = -INFINITY, l = 0.f;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int j0 = 0; j0 < nk; j0 += 64) {
     if (j0) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) ld8(kb + (long)min(min(j0 + u * 8 + kg, nk - 1), cap) * 64, kv[u]);
+      for (int u = 0; u < 8; ++u) kv[u] = load_frag<T>(kb + (long)min(min(j0 + u * 8 + kg, nk - 1), cap) * 64);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) ld8(vb + (long)min(min(j0 + u * 8 + kg, nk - 1), cap) * 64, vv[u]);
+      for (int u = 0; u < 8; ++u) vv[u] = load_frag<T>(vb + (long)min(min(j0 + u * 8 + kg, nk - 1), cap) * 64);
     }
     float sc[8];
     float mx = -INFINITY;
@@ -39,7 +45,7 @@ WCB_DEV void self_attn_wave(const T* q, const T* k0, const T* v0, int cap, NK&& 
     for (int u = 0; u < 8; ++u) {
       float d = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d = fmaf(qv[e], kv[u][e], d);
+      for (int e = 0; e < 8; ++e) d = fmaf(qv[e], cv(kv[u], e), d);
 #pragma unroll
       for (int x = 1; x < 8; x <<= 1) d += __shfl_xor(d, x, 64);
       sc[u] = (j0 + u * 8 + kg < nk) ? d : -INFINITY;
@@ -56,7 +62,7 @@ WCB_DEV void self_attn_wave(const T* q, const T* k0, const T* v0, int cap, NK&& 
       const float p = live ? __expf(sc[u] - mn) : 0.f;
       if (seg == 0) l += p;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] = live ? fmaf(p, vv[u][e], acc[e]) : acc[e];
+      for (int e = 0; e < 8; ++e) acc[e] = live ? fmaf(p, cv(vv[u], e), acc[e]) : acc[e];
     }
     m = mn;
   }
