@@ -43,8 +43,9 @@ double time_graph(int n, const std::function<void(int, hipStream_t)>& launch) {
 typedef float f4 __attribute__((ext_vector_type(4)));
 template <int NT, int WPL, int APL>
 __global__ __launch_bounds__(NT) void k_stream(const f4* __restrict__ w, long w_stride_wg, const f4* __restrict__ act_in,
-                                               long act_elems, f4* __restrict__ act_out) {
+                                               long act_elems, f4* __restrict__ act_out, unsigned long long* st) {
   const int tid = threadIdx.x;
+  const unsigned long long t0 = st ? stamp_now() : 0ull;
   const f4* wp = w + blockIdx.x * w_stride_wg + tid;
   f4 acc = f4{0.f, 0.f, 0.f, 0.f};
   f4 wv[WPL > 0 ? WPL : 1];
@@ -53,11 +54,18 @@ __global__ __launch_bounds__(NT) void k_stream(const f4* __restrict__ w, long w_
   f4 av[APL > 0 ? APL : 1];
 #pragma unroll
   for (int i = 0; i < APL; ++i) av[i] = act_in[(blockIdx.x * 64 + tid + i * NT) % act_elems];
+  unsigned long long t1 = 0;
+  if (st) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); t1 = stamp_now(); }
 #pragma unroll
   for (int i = 0; i < WPL; ++i) acc += wv[i];
 #pragma unroll
   for (int i = 0; i < APL; ++i) acc += av[i];
   if (tid < 64) act_out[(blockIdx.x * 64 + tid) % act_elems] = acc;
+  if (st && tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned long long* p = st + blockIdx.x * 4;
+    p[0] = t0; p[1] = t1; p[2] = t1; p[3] = stamp_now();
+  }
 }
 
 char* g_w;
@@ -103,24 +111,9 @@ void run_lean(const char* name, GemmArgs g0) {
 // per-workgroup phase stamps of every launch of a 100-launch chain (s_memrealtime, 10 ns ticks):
 // median over launches 10..99 of: dispatch gap (first start - previous launch's last end), start spread,
 // loads landed, LN + MFMA + LDS exchange, epilogue + store drain, launch span
-void run_lean_stamped(const char* name, GemmArgs g0) {
-  const long wbytes = (long)g0.N * g0.K * 2;
-  const long nreg = (long)(kW / wbytes);
-  const int nwg = ((g0.N + 15) / 16) * ((g0.M + 15) / 16);
-  const int n = 100;
-  unsigned long long* st;
-  CHK(hipMalloc(&st, (size_t)n * nwg * 32));
-  CHK(hipMemset(st, 0, (size_t)n * nwg * 32));
-  time_graph(n, [&](int i, hipStream_t s) {
-    GemmArgs g = g0;
-    g.W = g_w + (i % nreg) * wbytes;
-    g_lean_stamp = st + (long)i * nwg * 4;
-    launch_lean<bf16_t>(g, s);
-    g_lean_stamp = nullptr;
-  });
+void stamp_report(const char* name, const unsigned long long* dev, int n, int nwg) {
   std::vector<unsigned long long> h((size_t)n * nwg * 4);
-  CHK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
-  CHK(hipFree(st));
+  CHK(hipMemcpy(h.data(), dev, h.size() * 8, hipMemcpyDeviceToHost));
   auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
   std::vector<double> gap, spread, ld, mid, ep, span, wgdur;
   for (int i = 10; i < n; ++i) {
@@ -142,8 +135,27 @@ void run_lean_stamped(const char* name, GemmArgs g0) {
   fflush(stdout);
 }
 
+void run_lean_stamped(const char* name, GemmArgs g0) {
+  const long wbytes = (long)g0.N * g0.K * 2;
+  const long nreg = (long)(kW / wbytes);
+  const int nwg = ((g0.N + 15) / 16) * ((g0.M + 15) / 16);
+  const int n = 100;
+  unsigned long long* st;
+  CHK(hipMalloc(&st, (size_t)n * nwg * 32));
+  CHK(hipMemset(st, 0, (size_t)n * nwg * 32));
+  time_graph(n, [&](int i, hipStream_t s) {
+    GemmArgs g = g0;
+    g.W = g_w + (i % nreg) * wbytes;
+    g_lean_stamp = st + (long)i * nwg * 4;
+    launch_lean<bf16_t>(g, s);
+    g_lean_stamp = nullptr;
+  });
+  stamp_report(name, st, n, nwg);
+  CHK(hipFree(st));
+}
+
 // the lean out-projection with fragment-major weights (layout only: the bench's weights are zeros)
-template <int NW, int KPW, bool LN, int EPI, int MF = 1>
+template <int NW, int KPW, bool LN, int EPI, int MF = 1, bool AFM = false>
 void run_wfm(const char* name, GemmArgs g0, bool stamped) {
   const long wbytes = (long)g0.N * g0.K * 2;
   const long nreg = (long)(kW / wbytes);
@@ -160,11 +172,11 @@ void run_wfm(const char* name, GemmArgs g0, bool stamped) {
     p.M = g0.M; p.N = g0.N; p.lda = (int)g0.lda; p.ldo = (int)g0.ldc;
     p.n_split = g0.n_split; p.kvB = g0.hs_B; p.kvH = g0.hs_H; p.kvT = g0.kv_T; p.grp_n = 0; p.grp_off = 0;
     p.stamp = st ? st + (long)i * nwg * 4 : nullptr;
-    hipLaunchKernelGGL((dec_lean_kernel<bf16_t, MF, NW, KPW, LN, EPI, false, false, true>),
+    hipLaunchKernelGGL((dec_lean_kernel<bf16_t, MF, NW, KPW, LN, EPI, false, false, true, AFM>),
                        dim3((g0.N + 15) / 16, (g0.M + 16 * MF - 1) / (16 * MF)), dim3(NW * 64), 0, s, p);
   });
-  printf("%-40s lean, fragment-major W, %d-row wgs: %6.2f us/launch\n", name, 16 * MF, us);
-  if (st) CHK(hipFree(st));
+  printf("%-40s lean, fragment-major W%s, %d-row wgs: %6.2f us/launch\n", name, AFM ? " and A" : "", 16 * MF, us);
+  if (st) { stamp_report(name, st, 100, nwg); CHK(hipFree(st)); }
   fflush(stdout);
 }
 
@@ -261,19 +273,23 @@ void run_lm_head(bool boost) {
 }
 
 template <int NT, int WPL, int APL>
-void run_stream(const char* name, int grid) {
+void run_stream(const char* name, int grid, bool stamped = false) {
   const long per_wg = (long)NT * WPL, per_launch = per_wg * grid;
   const long nreg = (long)(kW / 16) / per_launch;
   const long act_elems = 98304 / 16;
+  unsigned long long* st = nullptr;
+  if (stamped) { CHK(hipMalloc(&st, (size_t)100 * grid * 32)); CHK(hipMemset(st, 0, (size_t)100 * grid * 32)); }
   double us = time_graph(100, [&](int i, hipStream_t s) {
     const f4* w = reinterpret_cast<const f4*>(g_w) + (i % nreg) * per_launch;
     f4* in = reinterpret_cast<f4*>(g_x) + (i & 1) * act_elems;
     f4* out = reinterpret_cast<f4*>(g_x) + ((i + 1) & 1) * act_elems;
-    hipLaunchKernelGGL((k_stream<NT, WPL, APL>), dim3(grid), dim3(NT), 0, s, w, per_wg, in, act_elems, out);
+    hipLaunchKernelGGL((k_stream<NT, WPL, APL>), dim3(grid), dim3(NT), 0, s, w, per_wg, in, act_elems, out,
+                       st ? st + (long)i * grid * 4 : nullptr);
   });
   printf("%-40s NT=%d W/wg=%5.1f KB A/wg=%5.1f KB grid=%4d: %6.2f us/launch\n", name, NT, WPL * NT * 16 / 1024.0,
          APL * NT * 16 / 1024.0, grid, us);
   fflush(stdout);
+  if (st) { stamp_report(name, st, 100, grid); CHK(hipFree(st)); }
 }
 
 int main() {
@@ -297,6 +313,20 @@ int main() {
   CHK(hipMalloc(&g_pos, 64));
   CHK(hipMemset(g_pos, 0, 64));
 
+  if (getenv("OUT_ONLY")) {   // the out projection's load phase against the byte-matched stream kernel
+    GemmArgs o = base(768, 768, 0);
+    o.A = g_a; o.bias = g_bias; o.resid = g_x; o.out = g_x; o.out_f32 = 1; o.out16 = g_x16;
+    run_stream<256, 0, 0>("stream: nothing", 96, true);
+    run_stream<256, 6, 6>("stream: out-proj bytes", 96, true);
+    run_stream<256, 6, 0>("stream: out-proj W only", 96, true);
+    run_wfm<4, 6, false, 1>("out", o, true);
+    run_wfm<4, 6, false, 1, 1, true>("out", o, true);
+    GemmArgs x = base(768, 768, 0);
+    x.ln_w = g_lnw; x.ln_b = g_lnb; x.ln_a16 = g_x16; x.A = g_x; x.bias = g_bias; x.out = g_out;
+    run_wfm<4, 6, true, 0>("xq (LN)", x, true);
+    run_wfm<4, 6, true, 0, 1, true>("xq (LN)", x, true);
+    return 0;
+  }
   // reference points: empty-ish and byte-matched stream kernels
   run_stream<256, 0, 0>("stream: nothing", 96);
   run_stream<256, 6, 6>("stream: out-proj bytes", 96);
