@@ -1,12 +1,12 @@
 #!/bin/bash
-# GPU check + A/B of one handle option (C2 bench): the named test selection, then the bench line with
+# GPU check + A/B of one handle option (C2 bench): the named test selection (TESTS, optional -k K), then the bench line with
 # the defaults (profiling pass on: per-class phases) and with OPT (e.g. OPT="xattn_mv=0"), then the
 # overlap probe. Every GPU step has its own limit; the chain stops at the first failure.
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1
 O="$R/gpurun_out/ab"; mkdir -p "$O"
 if [ -n "${TESTS:-}" ]; then
-  timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread $TESTS > "$O/tests.log" 2>&1 || { tail -30 "$O/tests.log"; exit 1; }
+  timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread $TESTS ${K:+-k "$K"} > "$O/tests.log" 2>&1 || { tail -30 "$O/tests.log"; exit 1; }
   tail -3 "$O/tests.log"
 fi
 timeout -k 10 400 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench_default.json" 2> "$O/bench_default.err" || { tail -20 "$O/bench_default.err"; exit 1; }

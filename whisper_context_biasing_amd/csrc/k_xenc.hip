@@ -481,34 +481,30 @@ __global__ __launch_bounds__(256) void xenc_merge_kernel(XencArgs a, T* u, long 
 
 // xenc_merge_v_kernel: the range merge and the value projection in one launch (replaces
 // xenc_merge_kernel + the grouped W_v decode GEMM: one dependent launch fewer per layer).
-// Workgroup = (head h, row): u = Σ_s w_s·part_s / L as in xenc_merge_kernel (rounded to T, as the
-// unfused path stores it), kept in LDS; then o[h·64 + j] = Σ_c W_v[h·64 + j][c]·u[c] + b_v[h·64 + j],
-// 16 lanes per output (each 16-byte weight load of a lane group covers 256 contiguous bytes of a
-// W_v row), 64 outputs in 4 passes of the 4 waves. Every weight load is issued before the partials
-// arrive (they do not depend on them).
-template <typename T, int D, int MS = kXencMaxSplit, int RPW = 1>
+// Workgroup = (head h, RPW rows): u = Σ_s w_s·part_s / L as in xenc_merge_kernel (rounded to T, as the
+// unfused path stores it), kept in LDS; then o = W_v,h·u + b_v as 16×16×32 MFMAs — wave w takes outputs
+// 16w .. 16w + 15 of the head as the A rows, the rows' u the B columns 0 .. RPW-1, K = D in D/32 steps
+// (u is exactly representable in T, so the B operand is u itself). Every weight load is issued before
+// the partials (they do not depend on them). The MFMA form replaced VALU dot products (r04 probe: 7.6k
+// cycles of the launch): 7.55 -> 7.08 us per C2 launch in the bench's serialised pass.
+template <typename T, int D, int MS, int RPW>
 __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* wv, const float* bv, T* out, long ldo) {
   using Frag = typename DT<T>::frag;
-  constexpr int CPL = D / 128;          // 16-byte chunks per lane per output row (D/8 chunks over 16 lanes)
+  constexpr int KS = D / 32;
+  static_assert(D <= 1024 && D % 32 == 0, "one 4-column group per thread");
+  static_assert(RPW <= 16, "the rows are the B columns of one MFMA");
   const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ns = a.nsplit;
   __shared__ float2 sv[RPW][MS];
   __shared__ __attribute__((aligned(16))) float us[RPW][D];
   MPROBE(0);
-  // weights first: pass p, output j = 16p + 4·wave + (lane >> 4), chunks (k·16 + (lane & 15))
-  Frag wf[4][CPL];
+  // W_v,h rows 16·wave + (lane & 15), k = 32·ks + 8·(lane >> 4): the A fragments of the wave's outputs
+  Frag wf[KS];
+  {
+    const T* wr = wv + (long)(h * 64 + 16 * wave + (lane & 15)) * D + 8 * (lane >> 4);
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int j = 16 * p + 4 * wave + (lane >> 4);
-    const T* wr = wv + (long)(h * 64 + j) * D + (lane & 15) * 8;
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) wf[p][k] = load_frag<T>(wr + k * 128);
+    for (int ks = 0; ks < KS; ++ks) wf[ks] = load_frag<T>(wr + ks * 32);
   }
-  // the range partials of this thread's 4 columns and the ranges' (max, Σp) go out in the same burst
-  // as the weights (issued behind the (max, Σp) exchange they cost a second memory round trip);
-  // D <= 1024: one 4-column group per thread, threads past D re-load the last group and discard it.
-  // RPW rows per workgroup share the head's W_v,h registers (rows past the batch re-read the last row)
-  static_assert(D <= 1024, "one 4-column group per thread");
   const int c = min(tid * 4, D - 4);
   f32x4 pv[RPW][MS];
 #pragma unroll
@@ -550,32 +546,33 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
   }
   __syncthreads();
   MPROBE(3);
+  // B: column lane & 15 = row r of this workgroup (zero past RPW), k = 32·ks + 8·(lane >> 4)
+  const int r = lane & 15;
+  f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int r = 0; r < RPW; ++r) {
-    const int b = blockIdx.y * RPW + r;
+  for (int ks = 0; ks < KS; ++ks) {
+    Frag uf = Frag{};
+    if (r < RPW) {
+      const f32x4 u0 = *reinterpret_cast<const f32x4*>(&us[r][ks * 32 + 8 * (lane >> 4)]);
+      const f32x4 u1 = *reinterpret_cast<const f32x4*>(&us[r][ks * 32 + 8 * (lane >> 4) + 4]);
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      float dsum = 0.f;
-#pragma unroll
-      for (int k = 0; k < CPL; ++k) {
-        const int cc = (k * 16 + (lane & 15)) * 8;
-        const f32x4 u0 = *reinterpret_cast<const f32x4*>(&us[r][cc]);
-        const f32x4 u1 = *reinterpret_cast<const f32x4*>(&us[r][cc + 4]);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float wv_e;
-          if constexpr (__is_same(T, bf16_t)) wv_e = bf16_to_f((bf16_t)wf[p][k][e]);
-          else wv_e = float(wf[p][k][e]);
-          dsum = fmaf(wv_e, e < 4 ? u0[e] : u1[e - 4], dsum);
-        }
-      }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) dsum += __shfl_xor(dsum, o, 64);
-      if ((lane & 15) == 0 && b < a.rows) {
-        const int n = h * 64 + 16 * p + 4 * wave + (lane >> 4);
-        out[(long)b * ldo + n] = DT<T>::fromf(dsum + bv[n]);
+      for (int e = 0; e < 4; ++e) {
+        uf[e] = __builtin_bit_cast(typename std::remove_reference<decltype(uf[0])>::type, DT<T>::fromf(u0[e]));
+        uf[4 + e] = __builtin_bit_cast(typename std::remove_reference<decltype(uf[0])>::type, DT<T>::fromf(u1[e]));
       }
     }
+    o = mma16(wf[ks], uf, o);
+  }
+  // C: lane holds outputs 16·wave + 4·(lane >> 4) + e of row lane & 15
+  const int b = blockIdx.y * RPW + r;
+  if (r < RPW && b < a.rows) {
+    const int n = h * 64 + 16 * wave + 4 * (lane >> 4);
+    const f32x4 b4 = *reinterpret_cast<const f32x4*>(bv + n);
+    typedef short s4 __attribute__((ext_vector_type(4)));
+    s4 hv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) hv[e] = __builtin_bit_cast(short, DT<T>::fromf(o[e] + b4[e]));
+    *reinterpret_cast<s4*>(out + (long)b * ldo + n) = hv;
   }
 #ifdef WCB_XENC_PROBE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -708,17 +705,14 @@ void xenc_merge(DType t, const XencArgs& a, void* u, long ldu, hipStream_t s) {
 
 template <typename T>
 static void launch_merge_v_t(const XencArgs& a, const void* wv, const float* bv, void* o, long ldo, hipStream_t s) {
-  const dim3 grid(a.H, a.rows);
-  // MS: the partial loads per thread (the key-range count rounded up to 8 or 16; ranges past nsplit
-  // carry weight 0)
-  // two rows per workgroup (the head's W_v,h registers serve both: half the weight re-reads) where the
-  // rows split evenly and the split count fits the 8-range form
+  // two rows per workgroup (the head's W_v,h fragments serve both: half the weight re-reads; 4 measured
+  // slower); MS: the partial loads per thread (the key-range count rounded up to 8 or 16; ranges past
+  // nsplit carry weight 0)
+  const dim3 grid(a.H, (a.rows + 1) / 2);
 #define WCB_XC(DD)                                                                                                    \
   case DD:                                                                                                            \
-    if (a.nsplit <= 8 && a.rows % 2 == 0)                                                                             \
-      WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8, 2>), dim3(a.H, a.rows / 2), dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo); \
-    else if (a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8>), grid, dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo); \
-    else WCB_LAUNCH((xenc_merge_v_kernel<T, DD>), grid, dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo);            \
+    if (a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8, 2>), grid, dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo); \
+    else WCB_LAUNCH((xenc_merge_v_kernel<T, DD, kXencMaxSplit, 2>), grid, dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo);   \
     break;
   switch (a.D) { WCB_XC(128) WCB_XC(256) WCB_XC(384) WCB_XC(512) WCB_XC(768) WCB_XC(1024) default: break; }
 #undef WCB_XC
