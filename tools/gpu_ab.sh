@@ -11,8 +11,9 @@ if [ -n "${TESTS:-}" ]; then
 fi
 timeout -k 10 400 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > "$O/bench_default.json" 2> "$O/bench_default.err" || { tail -20 "$O/bench_default.err"; exit 1; }
 python -c "import json;d=json.load(open('$O/bench_default.json'));print('default', d['value'], d['ms_per_step'])"
-for o in ${OPT:-}; do
-  timeout -k 10 300 python bench.py --no-cpu-baseline --no-profile ${BENCH_ARGS:-} --opt $o > "$O/bench_$o.json" 2> "$O/bench_$o.err" || { tail -20 "$O/bench_$o.err"; exit 1; }
+for o in ${OPT:-}; do   # one run per word; NAME=V,NAME2=V2 sets several options in one run
+  a=""; for kv in ${o//,/ }; do a="$a --opt $kv"; done
+  timeout -k 10 300 python bench.py --no-cpu-baseline --no-profile ${BENCH_ARGS:-} $a > "$O/bench_$o.json" 2> "$O/bench_$o.err" || { tail -20 "$O/bench_$o.err"; exit 1; }
   python -c "import json;d=json.load(open('$O/bench_$o.json'));print('$o', d['value'], d['ms_per_step'])"
 done
 if [ "${PROBE:-0}" = 1 ]; then
