@@ -86,7 +86,10 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)
  *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave), 4 (64 queries, default)
  *   "enc_raster" n     encoder GEMM tile order: bands of n row panels, column tiles outer (8, default;
- *                      0: row-major); bit-identical */
+ *                      0: row-major); bit-identical
+ *   "enc_gemm" v       encoder GEMM kernels: 4 (default) the ping-pong kernel, 256- or 192-wide tiles by the
+ *                      fewer tile rounds; 1 the LDS-ring kernel's 256x192 tiles where 192-wide wins; 0 the
+ *                      LDS-ring kernel everywhere */
 int wcb_set_option(wcb_handle* h, const char* name, int value);
 
 /* replaces from_pretrained / load_state_dict: one HF state-dict tensor (host f32, C order), staged
@@ -227,9 +230,10 @@ int wcb_debug_copy(wcb_handle* h, const char* name, void* dst, int64_t bytes, in
 int wcb_op_gemm(int dtype, const void* A, const void* W, int M, int N, int K, const float* bias, int act,
                 const float* resid, void* out, int out_f32, void* stream);
 /* the same with the encoder-GEMM kernel chosen: kernel 1 = the ping-pong kernel where it covers the shape
- * and is the faster one (16-bit, N % 256 == 0, K % 64 == 0, K >= 128, M >= 256, no residual epilogue; the
- * runtime's default, option "enc_gemm"), 2 = the ping-pong kernel for every shape it covers (residual
- * epilogue included), 0 = the LDS-ring / tile kernels */
+ * and is the faster one (16-bit, N % 256 == 0, K % 64 == 0, K >= 128, M >= 256; the LDS-ring kernel's
+ * 256x192 tiles where those leave fewer tile rounds), 4 = the same with the ping-pong kernel's own 192-wide
+ * tiles there (option "enc_gemm"), 2 / 5 = the ping-pong kernel's 256- / 192-wide tiles for every shape they
+ * cover (residual epilogue included), 0 = the LDS-ring / tile kernels */
 int wcb_op_gemm_kernel(int dtype, const void* A, const void* W, int M, int N, int K, const float* bias, int act,
                        const float* resid, void* out, int out_f32, int kernel, void* stream);
 /* decode-step fused form: out[M][N] = act(LN(X) · W[N][K]ᵀ + bias), X f32 [M][K] (M <= 64), with the

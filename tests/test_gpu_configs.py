@@ -428,7 +428,7 @@ def test_encoder_tile_raster_bit_identical(raster):
 
 # every non-default formulation a handle option selects, against the reference goldens (high-margin
 # recipe: greedy and beam-5 ids exact in bf16, as the defaults are in check_16bit_greedy / _beam5)
-ALT_OPTIONS = [{"merge_v": 0}, {"xenc_split": 4}, {"xenc_split": 12}, {"xenc_variant": 0}, {"xenc_variant": 2},
+ALT_OPTIONS = [{"merge_v": 0}, {"enc_gemm": 1}, {"enc_gemm": 0}, {"xenc_split": 4}, {"xenc_split": 12}, {"xenc_variant": 0}, {"xenc_variant": 2},
                {"xenc_variant": 3}, {"decode_contexts": 1}, {"enc_flash": 2}, {"flash_split": 1},
                {"beam_xattn": 1}, {"beam_xattn": 2}, {"ring_kt": 1}, {"lean": 0, "lean_x": 0}]
 

@@ -290,11 +290,15 @@ def test_gemm_ring_encoder_shapes(dt, M, N, K, act, resid):
     (1000, 1024, 320, 0, False, False, True),   # f32 out without a residual
     # more tiles than workgroups (256): each workgroup streams several tiles' K tiles back to back
     (8200, 2304, 128, 0, False, True, False), (16500, 1024, 192, 1, False, True, False),
-    (48000, 768, 768, 0, True, True, True), (33000, 2304, 768, 0, False, True, False)])
-def test_gemm_pingpong_kernel(dt, M, N, K, act, resid, bias, f32):
-    """The ping-pong encoder GEMM (gemm_pp_kernel: 256x256 tiles, staggered wave halves, counted LDS-DMA
-    waits, persistent K-tile stream) through wcb_op_gemm_kernel(kernel=2), every K-tile count of its piece schedule's tail (1, 2, 3,
-    many), ragged M, each epilogue, vs fp64 and against the LDS-ring kernel (kernel=0)."""
+    (48000, 768, 768, 0, True, True, True), (33000, 2304, 768, 0, False, True, False),
+    # 192-wide tiles (kernel 5): two / three K tiles, ragged M, the d-wide shapes of the encoder
+    (700, 192, 128, 1, False, True, False), (257, 576, 192, 0, True, True, True), (20000, 768, 3072, 0, True, True, True)])
+@pytest.mark.parametrize("kernel", [2, 5])
+def test_gemm_pingpong_kernel(dt, M, N, K, act, resid, bias, f32, kernel):
+    """The ping-pong encoder GEMM (gemm_pp_kernel: 256x256 (kernel 2) or 256x192 (kernel 5: where N % 192 ==
+    0, else the LDS-ring kernel takes the launch) tiles, staggered wave halves, counted LDS-DMA waits,
+    persistent K-tile stream) through wcb_op_gemm_kernel, every K-tile count of its piece schedule's tail
+    (1, 2, 3, many), ragged M, each epilogue, vs fp64 and against the LDS-ring kernel (kernel=0)."""
     lib = _lib.load()
     g = torch.Generator(device="cpu").manual_seed(M + N + K + 1)
     A = torch.randn(M, K, generator=g).to(DT[dt][0]).cuda()
@@ -312,7 +316,7 @@ def test_gemm_pingpong_kernel(dt, M, N, K, act, resid, bias, f32):
                                           _s()), None, "gemm")
         torch.cuda.synchronize()
         return out
-    out = run(2)
+    out = run(kernel)
     ref = A.double() @ W.double().T
     if bias:
         ref = ref + b.double()
@@ -323,7 +327,7 @@ def test_gemm_pingpong_kernel(dt, M, N, K, act, resid, bias, f32):
     tol = 1e-4 if f32 else (8e-3 if dt == "bf16" else 1e-3)
     err = ((out.double() - ref).abs() - tol * ref.abs()).max().item()
     assert err < 2e-4, err
-    assert torch.equal(run(2), out)   # deterministic
+    assert torch.equal(run(kernel), out)   # deterministic
     other = run(0)
     err0 = ((other.double() - ref).abs() - tol * ref.abs()).max().item()
     assert err0 < 2e-4, err0

@@ -42,8 +42,9 @@ if __name__ == "__main__":
         only = "gemm"
     for (M, N, K, act, resid) in shapes:
         if only in ("", "gemm"):
-            for kernel in (0, 2):
-                gemm_case(M, N, K, kernel=kernel, act=act, resid=resid)
+            for kernel in (0, 2, 5):   # LDS ring, ping-pong 256- / 192-wide tiles
+                if kernel != 5 or N % 192 == 0:
+                    gemm_case(M, N, K, kernel=kernel, act=act, resid=resid)
     if only == "":
         ln_case(48000, 768)
         xenc_case()

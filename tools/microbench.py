@@ -37,8 +37,8 @@ def stream():
 
 
 def gemm_case(M, N, K, dt=torch.bfloat16, kernel=1, act=0, resid=False):
-    """kernel 1: the runtime's encoder-GEMM choice (ping-pong kernel where it is the faster one), 2: the
-    ping-pong kernel wherever it covers the shape, 0: the LDS-ring / tile kernels; act 1 = bias + GELU, resid = bias + residual into f32 (the encoder epilogues)"""
+    """kernel 1: the runtime's encoder-GEMM choice (ping-pong kernel where it is the faster one), 2 / 5: the
+    ping-pong kernel's 256- / 192-wide tiles wherever they cover the shape, 0: the LDS-ring / tile kernels; act 1 = bias + GELU, resid = bias + residual into f32 (the encoder epilogues)"""
     A = torch.randn(M, K, device="cuda").to(dt)
     W = torch.randn(N, K, device="cuda").to(dt)
     bias = torch.randn(N, device="cuda")

@@ -583,20 +583,26 @@ __device__ __attribute__((aligned(16))) char wcb_pp_scratch[64 * 16];   // store
 
 template <int N> WCB_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N < 63 ? N : 63) : "memory"); }
 
-template <typename T, int EPI>
+template <typename T, int EPI, int BN = 256>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
   using Frag = typename DT<T>::frag;
   constexpr int BUF = 65536, WOFF = 32768;
-  // vector-memory operations a tile's epilogue issues: 32 stores (+ 32 residual loads). (Wave 0 also
-  // moves the tile's 256 bias values into LDS by one more DMA in phase 0 of its first K tile: every
-  // count below then over-waits by one for that wave, which is safe.)
-  constexpr int S = 32 + ((EPI & E_RESID) ? 32 : 0);
+  // BN = 256 or 192 output columns per tile: each wave's 16·FW columns are FW fragments, the weight
+  // tile FW DMA pieces of 64 rows (192: the d-wide N = 768 shapes tile the chip in whole rounds)
+  static_assert(BN == 256 || BN == 192, "tile width");
+  constexpr int FW = BN / 64;
+  // vector-memory operations per wave per K tile (A quarters 2, 3 of the next tile, W pieces + A quarters
+  // 0, 1 of the one after), and a tile's epilogue: 8·FW stores (+ 8·FW residual loads). (Wave 0 also
+  // moves the tile's bias values into LDS by one more DMA in phase 0 of its first K tile: every count
+  // below then over-waits by one for that wave, which is safe.)
+  constexpr int OPK = FW + 4;
+  constexpr int S = 8 * FW + ((EPI & E_RESID) ? 8 * FW : 0);
   constexpr int BIAS_LDS = 2 * BUF;   // [tile parity][256] f32
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   GPROBE(0);
-  const int tiles_n = g.N >> 8, tiles_m = (g.M + 255) >> 8, ntiles = tiles_m * tiles_n;
+  const int tiles_n = g.N / BN, tiles_m = (g.M + 255) >> 8, ntiles = tiles_m * tiles_n;
   const int nk = g.K >> 6;
   const int my = (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;   // tiles of this workgroup
   const int total = my * nk;                                             // K tiles of its stream
@@ -606,10 +612,10 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
       const int band = g.raster * tiles_n;
       const int fm = (wg / band) * g.raster, gm = min(tiles_m - fm, g.raster), r = wg % band;
       m0 = (fm + r % gm) * 256;
-      n0 = (r / gm) * 256;
+      n0 = (r / gm) * BN;
     } else {
       m0 = (wg / tiles_n) * 256;
-      n0 = (wg % tiles_n) * 256;
+      n0 = (wg % tiles_n) * BN;
     }
   };
   auto swzr = [](int r) { return (r >> 1) & 7; };
@@ -627,7 +633,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
     const int cs = (ch ^ swzr(ar)) << 3;
     aoff[p] = ar * (int)g.lda + cs;
     aoff_last[p] = (min(m_last + ar, g.M - 1) - m_last) * (int)g.lda + cs;
-    boff[p] = (64 * p + i8) * (int)g.ldw + ((ch ^ swzr(64 * p + i8)) << 3);
+    boff[p] = (64 * min(p, FW - 1) + i8) * (int)g.ldw + ((ch ^ swzr(64 * p + i8)) << 3);
   }
   // stream cursors: tile iteration, K tile, tile origin, and the tile's A / W panel pointers advanced to
   // the K tile (scalar: a DMA adds only the lane's offset)
@@ -659,11 +665,11 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][FW];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   Cur cc;   // the K tile being multiplied
   cc.it = 0; cc.kt = 0;
@@ -673,11 +679,16 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
   advance(c2);
   advance(c2);
   // K tiles 0 and 1 in the steady-state piece order
-  dma_b(0, cc, 0); dma_b(1, cc, 0); dma_a(0, cc, 0); dma_b(2, cc, 0); dma_b(3, cc, 0); dma_a(1, cc, 0);
-  dma_a(2, cc, 0); dma_a(3, cc, 0);
-  if (total > 1) { dma_b(0, c1, 1); dma_b(1, c1, 1); dma_a(0, c1, 1); dma_b(2, c1, 1); dma_b(3, c1, 1); dma_a(1, c1, 1); }
+  dma_b(0, cc, 0); dma_b(1, cc, 0); dma_a(0, cc, 0); dma_b(2, cc, 0);
+  if constexpr (FW == 4) dma_b(3, cc, 0);
+  dma_a(1, cc, 0); dma_a(2, cc, 0); dma_a(3, cc, 0);
+  if (total > 1) {
+    dma_b(0, c1, 1); dma_b(1, c1, 1); dma_a(0, c1, 1); dma_b(2, c1, 1);
+    if constexpr (FW == 4) dma_b(3, c1, 1);
+    dma_a(1, c1, 1);
+  }
   GPROBE(1);
-  if (total > 1) vm_wait<9>();   // W(0) and A q0(0) landed
+  if (total > 1) vm_wait<3 + FW + 2>();   // W(0) and A q0(0) landed
   else vm_wait<3>();
   GPROBE(2);
   barrier();
@@ -692,7 +703,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
   // base, so a read address is a per-lane constant (one per k-step) plus a compile-time offset
   const int sl = (lane >> 1) & 7;
   const int lo0 = (lane & 15) * 128 + ((c0 ^ sl) << 4), lo1 = (lane & 15) * 128 + (((4 + c0) ^ sl) << 4);
-  const int wb0 = WOFF + 64 * wc * 128 + lo0, wb1 = WOFF + 64 * wc * 128 + lo1;   // this wave's W rows
+  const int wb0 = WOFF + 16 * FW * wc * 128 + lo0, wb1 = WOFF + 16 * FW * wc * 128 + lo1;   // this wave's W rows
   const int ab0 = 128 * wr * 128 + lo0, ab1 = 128 * wr * 128 + lo1;                 // this wave's A rows
   auto ktile = [&](int gk, auto steady_tag) {
     constexpr bool ST = decltype(steady_tag)::value;
@@ -702,21 +713,21 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
     const bool e0 = !ST && cc.kt == 0 && cc.it > 0, e1 = !ST && cc.kt == 1 && cc.it > 0;
     // the plain counts (one scalar branch per phase; the general cases below run on <= 3 K tiles a tile)
     const bool plain = ST || (n2 && !e0 && !e1);
-    Frag bw[4][2];
+    Frag bw[FW][2];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       // retire the piece the NEXT phase reads (this phase's own pieces were retired one phase ago)
       if (plain) {
-        if (p < 3) vm_wait<8>();
+        if (p < 3) vm_wait<OPK>();
         else vm_wait<6>();
       } else if (p == 0) {
-        if (n1) { if (e0 || e1) vm_wait<8 + S>(); else vm_wait<8>(); }
+        if (n1) { if (e0 || e1) vm_wait<OPK + S>(); else vm_wait<OPK>(); }
         else { if (e0 || e1) vm_wait<2 + S>(); else vm_wait<2>(); }
       } else if (p == 1) {
-        if (n1) { if (e0) vm_wait<8 + S>(); else vm_wait<8>(); }
+        if (n1) { if (e0) vm_wait<OPK + S>(); else vm_wait<OPK>(); }
         else { if (e0) vm_wait<1 + S>(); else vm_wait<1>(); }
       } else if (p == 2) {
-        if (n1) { if (e0) vm_wait<8 + S>(); else vm_wait<8>(); }
+        if (n1) { if (e0) vm_wait<OPK + S>(); else vm_wait<OPK>(); }
         else { if (e0) vm_wait<S>(); else vm_wait<0>(); }
       } else if (n1) {
         if (n2) { if (e0) vm_wait<6 + S>(); else vm_wait<6>(); }
@@ -724,14 +735,14 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
       }
       if (p == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < FW; ++j) {
           bw[j][0] = *reinterpret_cast<const Frag*>(buf + wb0 + j * 16 * 128);
           bw[j][1] = *reinterpret_cast<const Frag*>(buf + wb1 + j * 16 * 128);
         }
       }
       if (!ST && p == 0 && cc.kt == 0 && wave == 0)   // this tile's bias into LDS (a global load in the
                                                       // epilogue would make hipcc wait for every DMA piece)
-        glds16(bias + cc.n0 + 4 * lane, smem + BIAS_LDS + (cc.it & 1) * 1024);
+        glds16(bias + (BN == 256 ? cc.n0 + 4 * lane : min(cc.n0 + 4 * lane, g.N - 4)), smem + BIAS_LDS + (cc.it & 1) * 1024);
       Frag af[2][2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -741,7 +752,11 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
       if (p == 0 && n1) dma_a(2, c1, gk + 1);
       if (p == 1 && n1) dma_a(3, c1, gk + 1);
       if (p == 2 && n2) { dma_b(0, c2, gk + 2); dma_b(1, c2, gk + 2); dma_a(0, c2, gk + 2); }
-      if (p == 3 && n2) { dma_b(2, c2, gk + 2); dma_b(3, c2, gk + 2); dma_a(1, c2, gk + 2); }
+      if (p == 3 && n2) {
+        dma_b(2, c2, gk + 2);
+        if constexpr (FW == 4) dma_b(3, c2, gk + 2);
+        dma_a(1, c2, gk + 2);
+      }
       barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
@@ -750,7 +765,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[2 * p + i][j] = mma16(bw[j][ks], af[i][ks], acc[2 * p + i][j]);
+          for (int j = 0; j < FW; ++j) acc[2 * p + i][j] = mma16(bw[j][ks], af[i][ks], acc[2 * p + i][j]);
       __builtin_amdgcn_s_setprio(0);
       barrier();
     }
@@ -765,22 +780,22 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
       // n0 + 64·wc + 16·j + 4·(lane >> 4) + e; exactly S vector-memory operations per wave
       if (cc.it == 0) GPROBE(5);
       const int rb = cc.m0 + 128 * wr + (lane & 15);
-      const int cb = cc.n0 + 64 * wc + 4 * c0;
-      f32x4 b4[4];
+      const int cb = cc.n0 + 16 * FW * wc + 4 * c0;
+      f32x4 b4[FW];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        b4[j] = *reinterpret_cast<const f32x4*>(smem + BIAS_LDS + (cc.it & 1) * 1024 + (64 * wc + 4 * c0 + 16 * j) * 4);
+      for (int j = 0; j < FW; ++j)
+        b4[j] = *reinterpret_cast<const f32x4*>(smem + BIAS_LDS + (cc.it & 1) * 1024 + (16 * FW * wc + 4 * c0 + 16 * j) * 4);
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi) {
         const int m = rb + 16 * mi;
         const long off = (long)min(m, g.M - 1) * g.ldc + cb;
-        f32x4 r4[4];
+        f32x4 r4[FW];
         if constexpr ((EPI & E_RESID) != 0) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) r4[j] = *reinterpret_cast<const f32x4*>(g.resid + off + 16 * j);
+          for (int j = 0; j < FW; ++j) r4[j] = *reinterpret_cast<const f32x4*>(g.resid + off + 16 * j);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < FW; ++j) {
           f32x4 v = acc[mi][j] + b4[j];
           acc[mi][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           if constexpr ((EPI & E_GELU) != 0) {
@@ -811,18 +826,18 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
   if (wr == 0) barrier();   // balance the stagger
 }
 
-template <typename T, int EPI>
+template <typename T, int EPI, int BN = 256>
 static void launch_pp_e(const GemmArgs& g, hipStream_t s) {
   constexpr int kLds = 2 * 65536 + 2048;   // two K-tile buffers + two tiles' bias
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<T, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<T, EPI, BN>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
     attr_set = true;
   }
-  const int tiles = ((g.M + 255) / 256) * (g.N / 256);
+  const int tiles = ((g.M + 255) / 256) * (g.N / BN);
   // one persistent workgroup per CU (LDS-bound); pp 3 (tools/gemm_probe): one tile per workgroup
   const dim3 grid((unsigned)(g.pp == 3 ? tiles : std::min(tiles, 256)));
-  WCB_LAUNCH((gemm_pp_kernel<T, EPI>), grid, dim3(512), kLds, s, g);
+  WCB_LAUNCH((gemm_pp_kernel<T, EPI, BN>), grid, dim3(512), kLds, s, g);
 }
 
 // the ping-pong kernel where it covers the launch: 16-bit, N % 256 == 0, K % 64 == 0 (>= 128), plain
@@ -835,16 +850,34 @@ static bool launch_pp(const GemmArgs& g, hipStream_t s) {
   if constexpr (sizeof(T) != 2) {
     return false;
   } else {
-    if (g.N % 256 != 0 || g.N > 8192 || g.K % 64 != 0 || g.K < 128 || g.a_Mb || g.c_Mb || g.addrow || g.mode != 0 || g.clamp != 0.f ||
-        g.rst_out || g.out16 || g.M < 256 || (g.resid && !g.out_f32) || (g.resid && g.act))
+    const bool n256 = g.N % 256 == 0, n192 = g.N % 192 == 0;
+    if ((!n256 && !n192) || g.N > 8192 || g.K % 64 != 0 || g.K < 128 || g.a_Mb || g.c_Mb || g.addrow || g.mode != 0 ||
+        g.clamp != 0.f || g.rst_out || g.out16 || g.M < 256 || (g.resid && !g.out_f32) || (g.resid && g.act))
       return false;
-    if (g.pp == 1) {   // where the LDS-ring kernel takes 256x192 tiles (d-wide N = 768: fewer tile rounds), it
-                       // measured faster (C2 out 99 vs 104 µs, fc2 271 vs 277 µs)
+    // 192-wide tiles where they leave fewer tile rounds on 256 CUs (d-wide N = 768). pp 1: those shapes go
+    // to the LDS-ring kernel's 256x192 tiles instead (measured faster than 256-wide ping-pong tiles: C2 out
+    // 99 vs 104 µs, fc2 271 vs 277 µs); pp 4: the ping-pong kernel's own 192-wide tiles; pp 2 / 5 (tests,
+    // microbenchmarks): 256- / 192-wide ping-pong tiles wherever N allows
+    bool w192;
+    if (g.pp == 2 || g.pp == 5) {
+      w192 = g.pp == 5;
+    } else {
       const long tm = (g.M + 255) / 256;
-      const long r256 = (tm * ((g.N + 255) / 256) + 255) / 256, r192 = (tm * ((g.N + 191) / 192) + 255) / 256;
-      if (g.N % 192 == 0 && r192 * 192 * 10 < r256 * 256 * 9) return false;
+      const long r256 = n256 ? (tm * (g.N / 256) + 255) / 256 : 0, r192 = n192 ? (tm * (g.N / 192) + 255) / 256 : 0;
+      w192 = !n256 || (n192 && r192 * 192 * 10 < r256 * 256 * 9);
+      if (w192 && g.pp == 1) return false;
     }
+    if ((w192 && !n192) || (!w192 && !n256)) return false;
     const int bits = (g.act == 1 ? E_GELU : 0) | (g.resid ? E_RESID : 0) | (g.out_f32 ? E_F32 : 0);
+    if (w192) {
+      switch (bits) {
+        case 0: launch_pp_e<T, 0, 192>(g, s); return true;
+        case E_GELU: launch_pp_e<T, E_GELU, 192>(g, s); return true;
+        case E_F32: launch_pp_e<T, E_F32, 192>(g, s); return true;
+        case E_RESID | E_F32: launch_pp_e<T, E_RESID | E_F32, 192>(g, s); return true;
+        default: return false;
+      }
+    }
     switch (bits) {
       case 0: launch_pp_e<T, 0>(g, s); return true;
       case E_GELU: launch_pp_e<T, E_GELU>(g, s); return true;

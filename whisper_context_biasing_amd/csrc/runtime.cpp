@@ -226,9 +226,11 @@ struct wcb_handle {
   // (GemmArgs::raster; 0 = row-major). 8 measured best with the round-3 ring kernel (whisper-small:
   // QKV 185 -> 177, fc1 297 -> 281, out 118 -> 116 us, fc2 within noise; profiles/r03f_enc_gemm_bench.txt)
   int enc_raster = 8;
-  // encoder GEMMs: the ping-pong kernel (option "enc_gemm" 1; gemm_impl.h gemm_pp_kernel) or the LDS-ring
-  // kernel (0)
-  int enc_gemm = 1;
+  // encoder GEMMs (option "enc_gemm"): the ping-pong kernel (gemm_impl.h gemm_pp_kernel), 256-wide tiles
+  // and 192-wide where those leave fewer tile rounds (4, default: C2 out 90.4 -> 89.2, fc2 273.4 -> 261.2 µs
+  // against the LDS-ring kernel's 256x192 tiles, tools/enc_bench.py gemm; the bench line within noise),
+  // the LDS-ring kernel for those (1), or the LDS-ring kernel everywhere (0)
+  int enc_gemm = 4;
   // decode projections on gemm_dec_kernel (K supported): the LayerNorm consumers compute their row
   // statistics from the rows they load, so the producers publish no per-16-column partial sums
   bool dec_gemm = false;
@@ -596,7 +598,7 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "xq_kq") {
       h->xq_kq = value != 0;
     } else if (n == "enc_gemm") {
-      REQUIRE(value == 0 || value == 1, "option enc_gemm: 0 or 1");
+      REQUIRE(value == 0 || value == 1 || value == 4, "option enc_gemm: 0, 1 or 4");
       h->enc_gemm = value;
     } else if (n == "enc_raster") {
       REQUIRE(value >= 0 && value <= 64, "option enc_raster: 0..64");
@@ -2263,7 +2265,7 @@ int wcb_op_gemm_kernel(int dtype, const void* A, const void* W, int M, int N, in
     REQUIRE(A && W && out && M > 0 && N > 0 && K > 0, "bad argument");
     REQUIRE(N % 8 == 0, "N must be a multiple of 8");
     REQUIRE(K % (dtype == WCB_F32 ? 32 : 64) == 0, "K must be a multiple of the 128-byte K tile");
-    REQUIRE(kernel >= 0 && kernel <= 2, "kernel: 0, 1 or 2");
+    REQUIRE(kernel >= 0 && kernel <= 5 && kernel != 3, "kernel: 0, 1, 2, 4 or 5");
     GemmArgs g = rowgemm(A, K, W, M, N, K, out, N);
     g.bias = bias; g.act = act; g.resid = resid; g.out_f32 = out_f32;
     g.raster = 8;
