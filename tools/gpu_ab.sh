@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU check + A/B of one handle option (C2 bench): the named test selection (TESTS, optional -k K), then the bench line with
-# the defaults (profiling pass on: per-class phases) and with OPT (e.g. OPT="xattn_mv=0"), then the
+# the defaults (profiling pass on: per-class phases) and with OPT (e.g. OPT="merge_v=0"), then the
 # overlap probe. Every GPU step has its own limit; the chain stops at the first failure.
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 1
