@@ -45,23 +45,25 @@ def test_stepwise_decode_equals_generate(size, dtype, prompt):
 
 @pytest.mark.parametrize("size,dtype,B", [("small", "bf16", 32), ("medium", "f16", 5)])
 def test_stepwise_scores_lm_head_layernorm_split_bit_identical(size, dtype, B):
-    """The lean LM head takes the final LayerNorm in a launch of its own (gemm_impl.h ln_rows_kernel, the
-    same K split, sum order and normalisation as the fused form): the chosen tokens' boosted logits
-    returned per step must equal the fused form's (option lean = 0) bit for bit."""
+    """The lean LM head with the final LayerNorm inside its column walk (default), in a launch of its own
+    (option lm_ln_split: gemm_impl.h ln_rows_kernel, the same K split, sum order and normalisation), and
+    the general decode kernel's fused form (option lean = 0): the chosen tokens' boosted logits returned
+    per step must be equal bit for bit."""
     dims = get_dims(size)
     sd = make_weights(dims, seed=1, recipe="diverse")
     x = torch.from_numpy(W.log_mel(synth_batch(B), dims.n_mel))
     phrases = synth_bias_list(200, eot=dims.eos_token_id)
     out = []
-    for lean in (1, 0):
-        m = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options={"lean": lean})
+    for opts in ({"lean": 1}, {"lean": 1, "lm_ln_split": 1}, {"lean": 0}):
+        m = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options=opts)
         dec = m.decode_begin(m.encode(x), bias_list=phrases, bias_boost=2.0, min_new_tokens=6)
         steps = [dec.step() for _ in range(6)]
         dec.close()
         out.append((torch.stack([i for i, _ in steps], 1).cpu(), torch.stack([s for _, s in steps], 1).float().cpu()))
         del m
-    assert torch.equal(out[0][0], out[1][0])
-    assert torch.equal(out[0][1], out[1][1])
+    for o in out[1:]:
+        assert torch.equal(out[0][0], o[0])
+        assert torch.equal(out[0][1], o[1])
 
 
 # ---------------------------------------------------------------- step-wise beam search

@@ -1217,7 +1217,15 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
   __builtin_amdgcn_sched_barrier(0);
   // ---------------- LayerNorm of the A rows: statistics from the loaded values, parameters via LDS
   if constexpr (LN) {
-    float xv[MF][KPW][8];
+    // the f32 value of an element is re-derived where needed (from the f32 rows, or exactly from the
+    // loaded 16-bit bits): no f32 copy of the A fragments held across the statistics barrier (it put the
+    // LN-fused LM-head walker at 256 VGPRs)
+    auto xv = [&](int i, int ks, int e) -> float {
+      if constexpr (AM == 1) return xf[i][ks][e >> 2][e & 3];
+      else if constexpr (sizeof(T) == 4) return a[i][ks][e];
+      else if constexpr (__is_same(T, bf16_t)) return bf16_to_f((bf16_t)a[i][ks][e]);
+      else return float(a[i][ks][e]);
+    };
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
       float s1 = 0.f, s2 = 0.f;
@@ -1225,12 +1233,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
       for (int ks = 0; ks < KPW; ++ks) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float v;
-          if constexpr (AM == 1) v = xf[i][ks][e >> 2][e & 3];
-          else if constexpr (sizeof(T) == 4) v = a[i][ks][e];
-          else if constexpr (__is_same(T, bf16_t)) v = bf16_to_f((bf16_t)a[i][ks][e]);
-          else v = float(a[i][ks][e]);
-          xv[i][ks][e] = v;
+          const float v = xv(i, ks, e);
           s1 += v;
           s2 = fmaf(v, v, s2);
         }
@@ -1245,6 +1248,12 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
       if (c < 2 * K) *reinterpret_cast<f32x4*>(lnp + c) = lq[j];
     }
     __syncthreads();
+    if constexpr (AM == 2) {   // opaque to hipcc: the f32 values are converted again, not kept across the barrier
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int ks = 0; ks < KPW; ++ks) asm volatile("" : "+v"(a[i][ks]));
+    }
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
       float s1 = 0.f, s2 = 0.f;
@@ -1258,13 +1267,15 @@ __global__ __launch_bounds__(NW * 64) void gemm_dec_kernel(GemmArgs g) {
         const f32x4 w1 = *reinterpret_cast<const f32x4*>(lnp + kb + ks * 32 + 4);
         const f32x4 b0 = *reinterpret_cast<const f32x4*>(lnp + K + kb + ks * 32);
         const f32x4 b1 = *reinterpret_cast<const f32x4*>(lnp + K + kb + ks * 32 + 4);
+        Frag o;   // the fragment rebuilt whole (element-wise writes into a[i][ks] kept every f32 alive)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float gw = e < 4 ? w0[e] : w1[e - 4], gb = e < 4 ? b0[e] : b1[e - 4];
-          const float v = (xv[i][ks][e] - mean) * rstd * gw + gb;
-          if constexpr (sizeof(T) == 4) a[i][ks][e] = v;
-          else a[i][ks][e] = __builtin_bit_cast(typename std::remove_reference<decltype(a[0][0][0])>::type, DT<T>::fromf(v));
+          const float v = (xv(i, ks, e) - mean) * rstd * gw + gb;
+          if constexpr (sizeof(T) == 4) o[e] = v;
+          else o[e] = __builtin_bit_cast(typename std::remove_reference<decltype(o[0])>::type, DT<T>::fromf(v));
         }
+        a[i][ks] = o;
       }
     }
   }

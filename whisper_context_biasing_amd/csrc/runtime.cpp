@@ -187,6 +187,10 @@ struct wcb_handle {
   // decode rows > 64: 64-deep K sub-tiles per ring stage of the 64x32 / 32x32 tiles (option "ring_kt",
   // 1 or 2; C5 1,594 -> 1,644 audio-s/s)
   int ring_kt = 2;
+  // greedy LM head: the final LayerNorm in a launch of its own (option "lm_ln_split" 1) or inside the
+  // column walk (0, default: with the f32 copies of the A rows no longer held across the statistics
+  // barrier the fused walker is 22.46 vs 22.19 µs + the LayerNorm launch, tools/dec_kernel_bench.hip)
+  int lm_ln_split = 0;
   // encoder flash attention tiling (option "enc_flash"): 2 = 32 queries per wave, 4 = 64 queries per
   // wave. Measured (tools/microbench.py, small / medium encoder shapes, µs): 2: 358 / 878, 4: 313 / 808
   // (3 / 4 LDS stages at 32 queries measured 328 / 887 and 399 / 1041: removed)
@@ -576,6 +580,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       REQUIRE(!h->ready, "option xenc_split: set before the weights are finalized");
       REQUIRE(value >= 1 && value <= kXencMaxSplit, "option xenc_split: 1..16");
       h->xenc_split = value;
+    } else if (n == "lm_ln_split") {
+      h->lm_ln_split = value != 0;
     } else if (n == "ring_kt") {
       REQUIRE(value == 1 || value == 2, "option ring_kt: 1 or 2");
       h->ring_kt = value;
@@ -1342,7 +1348,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     if (lm_tiled) lm.N = h->vocab_pad;
     lm.ln_w = h->dec_ln_w; lm.ln_b = h->dec_ln_b; lm.st_in = st; lm.st_nb = nbk; lm.ln_a16 = lna;
     if (h->lean) lm.W_fm = h->tok_emb_fm;
-    if (h->lean && !tiled && rps == 1) lm.ln_scratch = dh;   // the final LayerNorm in a launch of its own
+    if (h->lean && !tiled && rps == 1 && h->lm_ln_split) lm.ln_scratch = dh;   // the final LayerNorm in a launch of its own
     lm.out_f32 = 1;
     if (c.select && !c.beam) {   // argmax partials with the root boost + EOS mask fused into the LM head
       lm.sel_val = D.part_val.as<float>() + (size_t)b0 * D.nchunk;
