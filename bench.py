@@ -389,18 +389,23 @@ def main():
     # timed again under the timed region's own conditions — graphs, batches in flight, the encoder of
     # the next batch beside it — from device stamps in its graph nodes (HIP events cannot bracket a
     # graph node): the per-launch time rocprofv3 sees over the same command
-    xattn_live = None
+    xattn_live, graph_us = None, {}
     if not args.no_profile and args.num_beams == 1 and use_graph:
         model.profile_enable(True, events=False, stamps=True)
         for i in range(max(2, prof_steps)):
             step()
         model.synchronize()
         torch.cuda.synchronize()
-        e = model.profile_read().get("dec_xattn")
+        live = model.profile_read()
+        e = live.get("dec_xattn")
         model.profile_enable(False)
         keep.clear()
         if e and e["launches"] and e["ms"] > 0:
             xattn_live = {"avg_ms": e["ms"] / e["launches"], "launches": e["launches"], "bytes": e["bytes"] / e["launches"]}
+        # the lean decode projections stamped the same way (first workgroup start to last workgroup end of
+        # each launch inside the replayed graph, both decode chains and the encoder in flight)
+        graph_us = {k.split("@")[0]: round(v["ms"] / v["launches"] * 1e3, 3)
+                    for k, v in live.items() if k.endswith("@graph") and v["launches"]}
     roof, others = None, {}
     if prof:
         peak_mfma = {"bf16": PEAK_BF16_TFLOPS, "f16": PEAK_F16_TFLOPS}.get(args.dtype, PEAK_F32_TFLOPS)
@@ -555,6 +560,9 @@ def main():
             "roofline": roof,
             "roofline_other": others or None,
             "phases": phases,
+            # µs per launch of the lean decode projections inside the replayed decode graph (device stamps,
+            # pipelined as the timed region), beside the serialised pass's phases above
+            "decode_graph_launch_us": graph_us or None,
             "cpu_baseline": cpu,
             "biased_wer": bias_plumb,
         }

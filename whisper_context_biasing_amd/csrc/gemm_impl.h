@@ -1436,6 +1436,7 @@ template <typename T> struct DecLean {
   // ran out its bound
   T* att = nullptr; int ld_att = 0; unsigned long long* cnt = nullptr; int* err = nullptr;
   const T* kq_w = nullptr;
+  Stamp lst;                             // stamps pass: launch start / end inside the decode graph
 };
 
 //   FZ 2 (EPI 0, LN: the cross-attention query q_h = LN(x) W_q,hᵀ + b_q): the 4 column tiles of a head store
@@ -1455,7 +1456,7 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ct = blockIdx.x, mb = blockIdx.y * R, n0 = ct * 16;
   const int kb = wave * (KPW * 32) + 8 * (lane >> 4);
-  const unsigned long long t0 = p.stamp ? stamp_now() : 0ull;
+  const unsigned long long t0 = (p.stamp || p.lst.base) ? stamp_now() : 0ull;
   // ---------------- the launch's loads, one burst
   Frag w[KPW];
   if constexpr (WFM) {   // fragment-major weights: [tile][wave][k-step][lane][8], 1 KiB per wave-instruction
@@ -1672,6 +1673,7 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
     unsigned long long* st = p.stamp + (long)(blockIdx.y * gridDim.x + blockIdx.x) * 4;
     st[0] = t0; st[1] = t1; st[2] = t2; st[3] = stamp_now();
   }
+  if (p.lst.base && tid == 0) stamp_commit(p.lst, t0);   // (thread 0 stores in every workgroup)
 }
 
 inline thread_local unsigned long long* g_lean_stamp = nullptr;   // tools/dec_kernel_bench only
@@ -1680,6 +1682,7 @@ template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool
 static void launch_lean_k(const GemmArgs& g, hipStream_t s) {
   DecLean<T> p;
   p.stamp = g_lean_stamp;
+  if (g.lstamp) p.lst = *g.lstamp;
   p.W = reinterpret_cast<const T*>(g.W_fm ? g.W_fm : g.W);
   p.A = reinterpret_cast<const T*>(LN ? g.ln_a16 : g.A);
   p.bias = g.bias; p.gam = g.ln_w; p.bet = g.ln_b;

@@ -115,6 +115,9 @@ struct GemmArgs {
   // Set only where the lean kernel takes the launch (gemm() throws otherwise).
   unsigned long long* kq_cnt = nullptr; int* kq_err = nullptr;
   const void* kq_w = nullptr; void* kq_out = nullptr; long kq_ld = 0;
+  // profiling (stamps pass): the launch's first-workgroup start / last-workgroup end, recorded by the lean
+  // kernel inside the replayed decode graph (common.h stamp_commit); null base: off
+  struct Stamp* lstamp = nullptr;
 };
 
 void gemm(DType t, const GemmArgs& g, hipStream_t s);

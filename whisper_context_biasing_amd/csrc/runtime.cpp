@@ -117,6 +117,14 @@ struct wcb_bias {
   DevBuf st_depth, st_keep;         // per state: trie depth, deepest completed phrase on its path
 };
 
+// lean decode projection classes stamped inside the replayed decode graph (stamps pass), by region
+static const char* const kLeanStampClass[] = {"dec_xattn", "dec_qkv", "dec_out", "dec_xq", "dec_xo", "dec_fc1", "dec_fc2"};
+static int lean_stamp_region(const char* cls) {
+  for (int r = 1; r < 7; ++r)
+    if (!strcmp(cls, kLeanStampClass[r])) return r;
+  return 0;
+}
+
 // Decode state of one in-flight generate call. Two contexts (one per cross-K/V buffer) let call
 // i+1 decode on its own stream while call i is still decoding: two latency-bound step chains share
 // the GPU instead of one.
@@ -270,7 +278,12 @@ struct wcb_handle {
   std::vector<ProfEntry> prof_e;
   std::deque<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
   std::vector<hipEvent_t> ev_pool;
-  DevBuf stamps, stamp_acc;                   // decode cross-attention device stamps (graph nodes)
+  DevBuf stamps, stamp_acc;                   // decode device stamps (graph nodes): cross-attention + the lean projections
+  // stamp regions per decode context: 0 the cross-attention, 1.. the lean projection classes
+  static constexpr int kStampRegions = 7;
+  unsigned long long* stamp_base(int buf, int region) {
+    return stamps.as<unsigned long long>() + ((size_t)buf * kStampRegions + region) * stamp_slots() * 2 * kStampSub;
+  }
   double xattn_bytes = 0, xattn_flops = 0;    // algorithmic work of the stamped launches
   long stamp_slots() const { return (long)d.n_text_ctx * d.n_layers * kMaxSub; }   // per context
 
@@ -1175,6 +1188,8 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
   // (one position per row: the lean QKV appends one key per row)
   char* x16fm = fm_ok && rps == 1 && xfm_possible(h) ? (char*)D.dx16fm.p + (size_t)r0 * d * e : nullptr;
   char* dh = (char*)D.dh.p + (size_t)r0 * d * e;
+  int cur_l = 0;   // the layer being issued (the lean launches' stamp slot)
+  Stamp lst;
   auto proj = [&](const char* cls, GemmArgs g) {
     const bool lm = g.W == h->tok_emb;
     // > 64 rows, 16-bit: every non-grouped projection on the 32/64-row LDS-ring tiles (tile 2; C5's
@@ -1198,6 +1213,12 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       if (ring && g.resid && g.out16 && lnf_ok) g.rst_out = rst;   // residual writer: stats for the next LN
     } else {
       g.lean = h->lean;   // <= 64 rows: the lean single-tile kernel where it covers the launch
+      const int region = h->prof_stamps ? lean_stamp_region(cls) : 0;
+      if (region) {   // stamps pass: this launch's start / end inside the replayed graph
+        lst.base = h->stamp_base(c.buf, region);
+        lst.pos = pos; lst.stride = L * wcb_handle::kMaxSub; lst.idx = cur_l * wcb_handle::kMaxSub + chain;
+        g.lstamp = &lst;
+      }
     }
     dgemm(h, cls, g, st_);
   };
@@ -1205,6 +1226,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
   const int clips = c.clips ? c.clips : B;
   const size_t xkv_l = 2 * (size_t)clips * H * S * 64;
   for (int l = 0; l < L; ++l) {
+    cur_l = l;
     const LayerW& w = h->dec[l];
     char* cache = (char*)D.kvself.p + (l * cache_l + (size_t)b0 * H * T * 64) * e;
     GemmArgs q = drow(x, d, w.qkv_w, M, 3 * d, d, dq, d);    // LayerNorm fused (f32 A rows)
@@ -1260,7 +1282,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       xa.part = D.xpart.as<float>() + (size_t)r0 * h->xenc_split * H * d;
       xa.ml = D.xml.as<float>() + (size_t)r0 * h->xenc_split * H * 2;
       if (h->prof_stamps) {
-        xa.stamp.base = h->stamps.as<unsigned long long>() + (size_t)c.buf * h->stamp_slots() * 2 * kStampSub;
+        xa.stamp.base = h->stamp_base(c.buf, 0);
         xa.stamp.pos = pos;
         xa.stamp.stride = L * wcb_handle::kMaxSub; xa.stamp.idx = l * wcb_handle::kMaxSub + chain;
       }
@@ -1296,7 +1318,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       xa.ticket = D.xticket.as<int>() + (size_t)r0 * H;
       xa.variant = h->xvariant;   // fixed per handle: the same clip decodes alike in any batch
       if (h->prof_stamps) {
-        xa.stamp.base = h->stamps.as<unsigned long long>() + (size_t)c.buf * h->stamp_slots() * 2 * kStampSub;
+        xa.stamp.base = h->stamp_base(c.buf, 0);
         xa.stamp.pos = pos;
         xa.stamp.stride = L * wcb_handle::kMaxSub; xa.stamp.idx = l * wcb_handle::kMaxSub + chain;
       }
@@ -1697,8 +1719,8 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
       h->xattn_bytes += xm ? launches_clips / h->H() * h->d.d_model * esize(h->d.dtype)
                                  : launches_clips * 64 * 2 * esize(h->d.dtype);
       h->xattn_flops += xm ? launches_rows * h->d.d_model * 4 : launches_rows * 64 * 4;
-      stamp_reduce(h->stamps.as<unsigned long long>() + (size_t)buf * h->stamp_slots() * 2 * kStampSub, h->stamp_slots(),
-                   h->stamp_acc.as<unsigned long long>(), D.hs);
+      for (int r = 0; r < wcb_handle::kStampRegions; ++r)
+        stamp_reduce(h->stamp_base(buf, r), h->stamp_slots(), h->stamp_acc.as<unsigned long long>() + 2 * r, D.hs);
     }
     if (nb > 1) {   // best finished sequence of every utterance; its columns = the longest of them
       beam_output(bm, D.hs);
@@ -2205,11 +2227,11 @@ int wcb_profile_enable(wcb_handle* h, int enable) {
     h->prof_e.clear();
     h->xattn_bytes = h->xattn_flops = 0;
     if (h->prof_stamps) {
-      const size_t sb = (size_t)h->nctx * h->stamp_slots() * 16 * kStampSub;   // one region per decode context
+      const size_t sb = (size_t)h->nctx * wcb_handle::kStampRegions * h->stamp_slots() * 16 * kStampSub;
       h->stamps.ensure(sb);
-      h->stamp_acc.ensure(16);
+      h->stamp_acc.ensure(16 * wcb_handle::kStampRegions);
       HIPCHK(hipMemsetAsync(h->stamps.p, 0, sb, nullptr));
-      HIPCHK(hipMemsetAsync(h->stamp_acc.p, 0, 16, nullptr));
+      HIPCHK(hipMemsetAsync(h->stamp_acc.p, 0, 16 * wcb_handle::kStampRegions, nullptr));
       HIPCHK(hipStreamSynchronize(nullptr));
     }
   });
@@ -2220,16 +2242,22 @@ int wcb_profile_read(wcb_handle* h, int n, char (*names)[32], int64_t* launches,
   const int rc = guarded(h, [&] {
     REQUIRE(h, "null handle");
     h->prof_collect();
-    if (h->prof_stamps && h->stamp_acc.p) {   // decode cross-attention: device-stamped launches
+    if (h->prof_stamps && h->stamp_acc.p) {   // decode cross-attention + lean projections: device-stamped launches
       quiesce(h);
-      unsigned long long acc[2] = {0, 0};
-      HIPCHK(hipMemcpy(acc, h->stamp_acc.p, 16, hipMemcpyDeviceToHost));
+      unsigned long long acc[2 * wcb_handle::kStampRegions] = {};
+      HIPCHK(hipMemcpy(acc, h->stamp_acc.p, sizeof(acc), hipMemcpyDeviceToHost));
       if (acc[1]) {
         const int id = h->prof_id("dec_xattn");
         h->prof_e[id].launches = (int64_t)acc[1];
         h->prof_e[id].ms = (double)acc[0] / 1e5;   // 100 MHz s_memrealtime ticks
         h->prof_e[id].bytes = h->xattn_bytes;
         h->prof_e[id].flops = h->xattn_flops;
+      }
+      for (int r = 1; r < wcb_handle::kStampRegions; ++r) {
+        if (!acc[2 * r + 1]) continue;
+        const int id = h->prof_id((std::string(kLeanStampClass[r]) + "@graph").c_str());
+        h->prof_e[id].launches = (int64_t)acc[2 * r + 1];
+        h->prof_e[id].ms = (double)acc[2 * r] / 1e5;
       }
     }
     for (size_t i = 0; i < h->prof_e.size() && (int)i < n; ++i) {
