@@ -70,7 +70,7 @@ const char* wcb_last_error(const wcb_handle* h);
  *                      launch (0); before finalize
  *   "merge_v" 0/1      greedy encoder-space cross-attention: range merge and W_v fused (1) or two launches
  *   "xq_kq" 0/1        greedy encoder-space cross-attention query (lean path): q'_h = W_k,hᵀ q_h computed inside
- *                      the LN-fused q_proj launch (1, default) or as a launch of its own (0); bit-identical
+ *                      the LN-fused q_proj launch (1) or as a launch of its own (0, default); bit-identical
  *   "lean" 0/1         decode projections of <= 64 rows (16-bit) on the lean single-tile kernel (1, default)
  *                      or the general decode GEMM (0); bit-identical. Before finalize: with it finalize keeps
  *                      fragment-major copies of the decoder projection weights and the token embedding (the

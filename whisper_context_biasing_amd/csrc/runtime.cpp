@@ -118,9 +118,10 @@ struct wcb_bias {
 };
 
 // lean decode projection classes stamped inside the replayed decode graph (stamps pass), by region
-static const char* const kLeanStampClass[] = {"dec_xattn", "dec_qkv", "dec_out", "dec_xq", "dec_xo", "dec_fc1", "dec_fc2"};
+static const char* const kLeanStampClass[] = {"dec_xattn", "dec_qkv", "dec_out", "dec_xq", "dec_xo", "dec_fc1", "dec_fc2",
+                                              "dec_kq"};
 static int lean_stamp_region(const char* cls) {
-  for (int r = 1; r < 7; ++r)
+  for (int r = 1; r < 8; ++r)
     if (!strcmp(cls, kLeanStampClass[r])) return r;
   return 0;
 }
@@ -189,9 +190,12 @@ struct wcb_handle {
   // C2 16,570 vs 16,259 audio-s/s for the two launches)
   int merge_v = 1;
   // greedy cross-attention query (<= 64 rows, encoder space, lean path): q'_h = W_k,hᵀ q_h inside the
-  // LN-fused q_proj launch (option "xq_kq"; gemm_impl.h dec_lean_kernel FZ 2; 0 = two launches,
-  // bit-identical)
-  int xq_kq = 1;
+  // LN-fused q_proj launch (option "xq_kq" 1; gemm_impl.h dec_lean_kernel FZ 2) or as a launch of its
+  // own (0, default; bit-identical). Serialised, the fused launch is the faster (6.9 vs 4.4 + 3.0 µs);
+  // inside the pipelined graph its in-launch hand-off stretches to 9.3 µs with the other chain and the
+  // encoder beside it, and the C2 bench measured 19,084 (two launches) vs 18,999 (fused), mean of five
+  // interleaved pairs
+  int xq_kq = 0;
   // decode rows > 64: 64-deep K sub-tiles per ring stage of the 64x32 / 32x32 tiles (option "ring_kt",
   // 1 or 2; C5 1,594 -> 1,644 audio-s/s)
   int ring_kt = 2;
@@ -280,7 +284,7 @@ struct wcb_handle {
   std::vector<hipEvent_t> ev_pool;
   DevBuf stamps, stamp_acc;                   // decode device stamps (graph nodes): cross-attention + the lean projections
   // stamp regions per decode context: 0 the cross-attention, 1.. the lean projection classes
-  static constexpr int kStampRegions = 7;
+  static constexpr int kStampRegions = 8;
   unsigned long long* stamp_base(int buf, int region) {
     return stamps.as<unsigned long long>() + ((size_t)buf * kStampRegions + region) * stamp_slots() * 2 * kStampSub;
   }
