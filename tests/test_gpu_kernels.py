@@ -125,6 +125,26 @@ def test_flash_attention(dt, S):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("qscale", [0.3, 1.0])
+def test_flash_attention_moving_max(dt, qscale):
+    """Key norms growing along the sequence: the row maxima keep rising tile after tile, so the online
+    softmax rescales the accumulators often and late; both encoder tilings (64 / 32 queries per wave)
+    against fp64."""
+    g = torch.Generator(device="cpu").manual_seed(int(qscale * 10))
+    B, H, S = 2, 2, 1500
+    ramp = (0.2 + 3.0 * torch.arange(S, dtype=torch.float32) / S).view(1, S, 1)
+    q = (torch.randn(B, S, H * 64, generator=g) * qscale).to(DT[dt][0]).cuda()
+    k = (torch.randn(B, S, H * 64, generator=g) * ramp).to(DT[dt][0]).cuda()
+    v = torch.randn(B, S, H * 64, generator=g).to(DT[dt][0]).cuda()
+    ref = _attn_ref(q, k, v)
+    tol = 1e-2 if dt == "bf16" else 2e-3
+    for code in (100, 1):
+        o = _attn(dt, q, k, v, code)
+        assert torch.isfinite(o.float()).all()
+        assert (o.double() - ref).abs().max().item() < tol, code
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
 @pytest.mark.parametrize("B,H,Sq,Sk", [(3, 16, 5, 1500), (2, 20, 5, 1500), (4, 6, 2, 1500), (2, 4, 8, 777),
                                        (1, 2, 16, 64), (2, 3, 17, 1500)])
 @pytest.mark.parametrize("split", [1, 4, 7, "beam", "beam8", "beam9"])
