@@ -137,11 +137,14 @@ def test_flash_attention_moving_max(dt, qscale):
     k = (torch.randn(B, S, H * 64, generator=g) * ramp).to(DT[dt][0]).cuda()
     v = torch.randn(B, S, H * 64, generator=g).to(DT[dt][0]).cuda()
     ref = _attn_ref(q, k, v)
-    tol = 1e-2 if dt == "bf16" else 2e-3
+    # peaked rows: outputs reach |v| ~ 4, so the bound is relative — the 16-bit P (2^-9 per term) and
+    # the 16-bit output (2^-9) with 4x headroom; a wrong rescale is off by O(1)
+    c = 2.0 ** -6 if dt == "bf16" else 2.0 ** -9
     for code in (100, 1):
         o = _attn(dt, q, k, v, code)
         assert torch.isfinite(o.float()).all()
-        assert (o.double() - ref).abs().max().item() < tol, code
+        err = (o.double() - ref).abs() / (ref.abs() + 0.25)
+        assert err.max().item() < c, (code, err.max().item())
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
