@@ -488,7 +488,7 @@ __global__ __launch_bounds__(256) void xenc_merge_kernel(XencArgs a, T* u, long 
 // the partials (they do not depend on them). The MFMA form replaced VALU dot products (r04 probe: 7.6k
 // cycles of the launch): 7.55 -> 7.08 us per C2 launch in the bench's serialised pass.
 template <typename T, int D, int MS, int RPW>
-__global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* wv, const float* bv, T* out, long ldo) {
+__global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* wv, const T* wfm, const float* bv, T* out, long ldo) {
   using Frag = typename DT<T>::frag;
   constexpr int KS = D / 32;
   static_assert(D <= 1024 && D % 32 == 0, "one 4-column group per thread");
@@ -499,11 +499,14 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
   __shared__ __attribute__((aligned(16))) float us[RPW][D];
   MPROBE(0);
   // W_v,h rows 16·wave + (lane & 15), k = 32·ks + 8·(lane >> 4): the A fragments of the wave's outputs
+  // (fragment-major copy when given: tile h·4 + wave, 1 KiB contiguous per wave-instruction; the same values)
   Frag wf[KS];
   {
-    const T* wr = wv + (long)(h * 64 + 16 * wave + (lane & 15)) * D + 8 * (lane >> 4);
+    const T* wr = wfm ? wfm + ((long)(h * 4 + wave) * KS * 64 + lane) * 8
+                      : wv + (long)(h * 64 + 16 * wave + (lane & 15)) * D + 8 * (lane >> 4);
+    const int kstep = wfm ? 512 : 32;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) wf[ks] = load_frag<T>(wr + ks * 32);
+    for (int ks = 0; ks < KS; ++ks) wf[ks] = load_frag<T>(wr + ks * kstep);
   }
   const int c = min(tid * 4, D - 4);
   f32x4 pv[RPW][MS];
@@ -704,23 +707,24 @@ void xenc_merge(DType t, const XencArgs& a, void* u, long ldu, hipStream_t s) {
 }
 
 template <typename T>
-static void launch_merge_v_t(const XencArgs& a, const void* wv, const float* bv, void* o, long ldo, hipStream_t s) {
+static void launch_merge_v_t(const XencArgs& a, const void* wv, const void* wfm, const float* bv, void* o, long ldo, hipStream_t s) {
   // two rows per workgroup (the head's W_v,h fragments serve both: half the weight re-reads; 4 measured
   // slower); MS: the partial loads per thread (the key-range count rounded up to 8 or 16; ranges past
   // nsplit carry weight 0)
   const dim3 grid(a.H, (a.rows + 1) / 2);
 #define WCB_XC(DD)                                                                                                    \
   case DD:                                                                                                            \
-    if (a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8, 2>), grid, dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo); \
-    else WCB_LAUNCH((xenc_merge_v_kernel<T, DD, kXencMaxSplit, 2>), grid, dim3(256), 0, s, a, (const T*)wv, bv, (T*)o, ldo);   \
+    if (a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8, 2>), grid, dim3(256), 0, s, a, (const T*)wv, (const T*)wfm, bv, (T*)o, ldo); \
+    else WCB_LAUNCH((xenc_merge_v_kernel<T, DD, kXencMaxSplit, 2>), grid, dim3(256), 0, s, a, (const T*)wv, (const T*)wfm, bv, (T*)o, ldo);   \
     break;
   switch (a.D) { WCB_XC(128) WCB_XC(256) WCB_XC(384) WCB_XC(512) WCB_XC(768) WCB_XC(1024) default: break; }
 #undef WCB_XC
 }
 
-void xenc_merge_v(DType t, const XencArgs& a, const void* wv, const float* bv, void* o, long ldo, hipStream_t s) {
-  if (t == kBF16) launch_merge_v_t<bf16_t>(a, wv, bv, o, ldo, s);
-  else if (t == kF16) launch_merge_v_t<f16_t>(a, wv, bv, o, ldo, s);
+void xenc_merge_v(DType t, const XencArgs& a, const void* wv, const float* bv, void* o, long ldo, hipStream_t s,
+                  const void* wv_fm) {
+  if (t == kBF16) launch_merge_v_t<bf16_t>(a, wv, wv_fm, bv, o, ldo, s);
+  else if (t == kF16) launch_merge_v_t<f16_t>(a, wv, wv_fm, bv, o, ldo, s);
 }
 
 }  // namespace wcb

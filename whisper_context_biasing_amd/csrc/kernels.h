@@ -202,7 +202,10 @@ void xenc_attention(DType t, const XencArgs& a, hipStream_t s);
 // u[r][h·D + c] = (Σ_s w_s part[r][s][h][c]) / L  (model dtype; ldu elements per row)
 void xenc_merge(DType t, const XencArgs& a, void* u, long ldu, hipStream_t s);
 // merge + value projection fused (D % 128 == 0): o[row][h·64 + j] = W_v,h·u_h + b_v, T
-void xenc_merge_v(DType t, const XencArgs& a, const void* wv, const float* bv, void* o, long ldo, hipStream_t s);
+// wv_fm (nullable): W_v in the fragment-major layout of frag_major(W_v, d, d, 1, d / 32) — each weight
+// wave-instruction of the merge then reads 1 KiB contiguous
+void xenc_merge_v(DType t, const XencArgs& a, const void* wv, const float* bv, void* o, long ldo, hipStream_t s,
+                  const void* wv_fm = nullptr);
 
 // log-mel front end
 void logmel_power_mel(const float* pcm, long pcm_stride, int n_samples, int B, const float* dft,

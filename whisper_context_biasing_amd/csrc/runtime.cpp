@@ -96,6 +96,7 @@ struct LayerW {
   // decoder, 16-bit: fragment-major copies for the lean decode projections (kernels.h frag_major)
   void *qkv_fm = nullptr, *o_fm = nullptr, *xq_fm = nullptr, *xkt_fm = nullptr, *xo_fm = nullptr, *fc1_fm = nullptr,
        *fc2_fm = nullptr;
+  void* xv_fm = nullptr;   // W_v for the greedy range merge (xenc_merge_v_kernel's A-fragment order)
 };
 
 struct ProfEntry {
@@ -835,6 +836,10 @@ int wcb_finalize_weights(wcb_handle* h) {
         lw.fc1_fm = fm(lw.fc1_w, F, d);
         lw.fc2_fm = fm(lw.fc2_w, d, F);
         if (lw.xkt_w) lw.xkt_fm = fm(lw.xkt_w, H * d, 64);
+        if (lw.xv_w && h->lean && h->dt != kF32 && d % 128 == 0 && d <= 1024) {   // 16 output rows per wave, all of K per wave
+          lw.xv_fm = h->own((size_t)d * d * e);
+          frag_major(h->dt, lw.xv_w, d, d, 1, d / 32, lw.xv_fm, st);
+        }
       }
     }
     h->enc_ln_w = F_("model.encoder.layer_norm.weight", d);
@@ -1295,7 +1300,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
                [&] { xenc_attention(h->dt, xa, st_); });
       if (h->merge_v && d % 128 == 0) {   // range merge + o_h = W_v,h u_h + b_v,h in one launch
         h->timed("dec_xmerge", 0, (double)M * H * d * h->xenc_split * 4.0 + (double)d * d * e, st_,
-                 [&] { xenc_merge_v(h->dt, xa, w.xv_w, w.xv_b, datt, d, st_); });
+                 [&] { xenc_merge_v(h->dt, xa, w.xv_w, w.xv_b, datt, d, st_, w.xv_fm); });
       } else {
         char* du = (char*)D.du.p + (size_t)r0 * H * d * e;
         h->timed("dec_xmerge", 0, (double)M * H * d * (h->xenc_split * 4.0 + e), st_,
