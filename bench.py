@@ -139,7 +139,70 @@ def cpu_baseline(size: str, n_tokens: int, n_phr: int, boost: float, seed: int =
                       f"{quota}); not extrapolated to the 32-clip batch"}
 
 
-def _pmc_traffic(kernel: str):
+# phase of every profiled launch class (bench `phases` keys / rocprofv3 kernel symbols via tools/check_roofline.py)
+FRONT_CLASSES = ("log_mel", "mel_to_conv_input")
+
+
+def _phase_of(cls: str) -> str:
+    if cls in FRONT_CLASSES:
+        return "front_end"
+    if cls.startswith("enc_") or cls == "layernorm":
+        return "encoder"
+    return "decode"
+
+
+def step_ideal(dims, clips: int, new_tokens: int, num_beams: int = 1, esize: int = 2,
+               peak_mfma_tflops: float = PEAK_BF16_TFLOPS, peak_hbm_gbs: float = PEAK_HBM_GBS, prompt_len: int = 1):
+    """SURVEY §8(d)'s step roofline: each phase's ideal time at its roofline, from algorithmic work alone
+    (no kernel's own accounting). front end (HBM): PCM in + mel out, f32. encoder (MFMA): conv stem + layer
+    GEMMs (2·M·N·K) + attention (4·S²·d per layer). decode (HBM), per generated token: every decoder weight
+    once (16·d² per layer + the tied V·d LM head) + the cross-attention's encoder-side bytes at the fewest
+    any formulation needs (the encoder output once per clip per layer: the encoder-space algebra; the K/V
+    form reads twice that) + the self-attention K/V cache of every row at its position (keys 1 .. t).
+    Returns {phase: ideal ms per step} and the bytes / flops behind them."""
+    d, L, S, V, nm = dims.d_model, dims.n_layers, dims.n_audio_ctx, dims.vocab, dims.n_mel
+    frames = 2 * S
+    front_bytes = clips * (480000 * 4 + nm * frames * 4)
+    enc_flops = clips * (2.0 * frames * d * 3 * nm + 2.0 * S * d * 3 * d
+                         + L * (2.0 * S * 12 * d * d + 4.0 * S * S * d))
+    rows = clips * num_beams
+    w_bytes = (L * 16 * d * d + V * d) * esize
+    x_bytes = clips * L * S * d * esize                       # per token
+    kv_bytes = sum(rows * 2 * L * (prompt_len - 1 + t) * d * esize for t in range(1, new_tokens + 1))
+    dec_bytes = new_tokens * (w_bytes + x_bytes) + kv_bytes
+    ideal = {"front_end": front_bytes / (peak_hbm_gbs * 1e9) * 1e3,
+             "encoder": enc_flops / (peak_mfma_tflops * 1e12) * 1e3,
+             "decode": dec_bytes / (peak_hbm_gbs * 1e9) * 1e3}
+    return ideal, {"front_end_bytes": front_bytes, "encoder_flops": enc_flops, "decode_bytes": dec_bytes,
+                   "decode_bytes_per_token": {"weights": w_bytes, "encoder_side": x_bytes,
+                                              "self_kv_mean": kv_bytes / max(new_tokens, 1)}}
+
+
+def step_roofline(dims, clips, new_tokens, num_beams, esize, peak_mfma, ms_per_step, phases):
+    """roofline.step: Σ(phase ideal time) ÷ the measured step time (the timed region's, pipelined), and per
+    phase its ideal time ÷ its serialised GPU time from the profiling pass (`phases`)."""
+    ideal, work = step_ideal(dims, clips, new_tokens, num_beams, esize, peak_mfma)
+    meas = {}
+    for k, v in (phases or {}).items():
+        if k.startswith("family:"):
+            continue
+        ph = _phase_of(k)
+        meas[ph] = meas.get(ph, 0.0) + v["ms_per_step"]
+    tot = sum(ideal.values())
+    per = {ph: {"ideal_ms": round(ideal[ph], 4), "bound": "mfma" if ph == "encoder" else "hbm",
+                "serialised_ms": round(meas[ph], 3) if ph in meas else None,
+                "frac": round(ideal[ph] / meas[ph], 4) if meas.get(ph) else None} for ph in ideal}
+    return {"ideal_ms": round(tot, 4), "measured_ms_per_step": round(ms_per_step, 3),
+            "frac": round(tot / ms_per_step, 4), "phases": per,
+            "serialised_gpu_ms": round(sum(meas.values()), 3) if meas else None,
+            "work": {k: (round(v, 1) if isinstance(v, float) else v) for k, v in work.items()},
+            "definition": "SURVEY §8(d): frac = Σ(phase ideal time at its roofline) ÷ measured ms_per_step; encoder "
+                          "FLOPs at the dense MFMA peak, front end and decode bytes at 8 TB/s (decode: decoder "
+                          "weights + the encoder output once per clip per layer + self-K/V, per token); phase frac = "
+                          "ideal ÷ that phase's serialised GPU time (profiling pass)"}
+
+
+def _pmc_traffic(kernel: str, grid=None):
     """HBM bytes per launch of `kernel` (symbol, every grid it runs at) from the committed rocprofv3
     PMC passes (profiles/*pmc*.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2 (gfx950
     correction) + WRITE_SIZE), or None."""
@@ -155,7 +218,9 @@ def _pmc_traffic(kernel: str):
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
-        e = d.get("symbols", {}).get(kernel)
+        # the launch shape's own figure first (one symbol runs at several grids: prefill, beams)
+        e = d.get("kernels", {}).get(f"{kernel}|{grid}") if grid else None
+        e = e or d.get("symbols", {}).get(kernel)
         if e:
             return e["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
     return None
@@ -254,6 +319,9 @@ def main():
     ap.add_argument("--reference-mode", action="store_true",
                     help="the reference's decode contract: natural EOS, max_length=225, no boost "
                          "(scripts/evaluation.py:173-179); batches serialised (the host polls EOS)")
+    ap.add_argument("--side-stream", action="store_true",
+                    help="issue the step from a non-default torch stream (CU-masked library streams, option "
+                         "cu_split, are blocking streams: work on the legacy null stream serialises them)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="serialise batches (default: batch i+1's front end + encoder overlap batch i's decode)")
     args = ap.parse_args()
@@ -288,6 +356,8 @@ def main():
     gpu = local % ndev
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
+    if args.side_stream:
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -446,7 +516,8 @@ def main():
         avg_ms = g["ms"] / g["launches"]
         per = (g["flops"] if c["bound"] == "mfma" else g["bytes"]) / g["launches"]
         ach = per / (avg_ms * 1e-3) / (1e12 if c["bound"] == "mfma" else 1e9)
-        roof = dict(c, **{"class": "+".join(sorted(g["classes"])), "achieved": round(ach, 1), "grid": None,
+        dom_grid = c["grid"] if len(g["classes"]) == 1 else None
+        roof = dict(c, **{"class": "+".join(sorted(g["classes"])), "achieved": round(ach, 1), "grid": dom_grid,
                           "frac": round(ach / c["peak"], 4), "avg_launch_ms": round(avg_ms, 5),
                           "launches_per_step": g["launches"], "bytes_per_launch": g["bytes"] / g["launches"],
                           "flops_per_launch": g["flops"] / g["launches"], "total_ms_per_step": round(g["ms"], 3),
@@ -466,7 +537,7 @@ def main():
                                    "begin/end HIP events of a serialised eager pass; rocprofv3 trace of the same "
                                    "command: profiles/ (tools/check_roofline.py compares the two)"})
         c2 = (args.model, args.batch, args.num_beams, args.dtype, args.new_tokens) == ("small", 32, 1, "bf16", 64)
-        tr = _pmc_traffic(roof["kernel"]) if c2 else None
+        tr = _pmc_traffic(roof["kernel"], dom_grid) if c2 else None
         if tr:
             roof["traffic"], roof["traffic_source"] = tr
         others = {k: v for k, v in classes.items() if k not in g["classes"]}
@@ -476,6 +547,11 @@ def main():
         fam = lambda pred: round(sum(v["ms_per_step"] for k, v in phases.items() if pred(k)), 3)
         phases["family:enc_gemm"] = {"ms_per_step": fam(lambda k: k in ENC_GEMMS)}
         phases["family:dec_proj"] = {"ms_per_step": fam(lambda k: k in DEC_PROJ)}
+    esize = {"f32": 4, "fp32": 4}.get(args.dtype, 2)
+    peak_mfma = {"bf16": PEAK_BF16_TFLOPS, "f16": PEAK_F16_TFLOPS, "fp16": PEAK_F16_TFLOPS}.get(args.dtype, PEAK_F32_TFLOPS)
+    step_roof = step_roofline(dims, B, args.new_tokens, args.num_beams, esize, peak_mfma, ms_per_step, phases)
+    if roof is not None:
+        roof["step"] = step_roof
 
     # biased-WER half of the metric (random weights: no transcript to score against): the boosted
     # decode of the benchmark batch against its lam = 0 decode, scored by the C++ host scorer with
@@ -557,7 +633,7 @@ def main():
                        "collective_backend": args.backend if world > 1 else None, "devices_used": devices_used,
                        "hipgraph_decode": use_graph, "batches_in_flight": 3 if overlap else 1},
             "rtf": round(1.0 / (value / world), 6),
-            "roofline": roof,
+            "roofline": roof if roof is not None else {"step": step_roof},
             "roofline_other": others or None,
             "phases": phases,
             # µs per launch of the lean decode projections inside the replayed decode graph (device stamps,

@@ -89,7 +89,13 @@ const char* wcb_last_error(const wcb_handle* h);
  *                      0: row-major); bit-identical
  *   "enc_gemm" v       encoder GEMM kernels: 4 (default) the ping-pong kernel, 256- or 192-wide tiles by the
  *                      fewer tile rounds; 1 the LDS-ring kernel's 256x192 tiles where 192-wide wins; 0 the
- *                      LDS-ring kernel everywhere */
+ *                      LDS-ring kernel everywhere
+ *   "cu_split" n       CU split (0..24): the decode streams on n CUs of every XCD (CU-mask bits i < 8n; the
+ *                      driver stripes mask bits over XCDs, then shader engines), the front end / encoder
+ *                      stream on the others, so the next batch's encoder runs beside the decode chains; 0:
+ *                      every stream on every CU. Re-creates the handle's streams; bit-identical
+ * While a step-wise decode is open (wcb_decode_begin .. wcb_decode_end) only decode_contexts, enc_flash,
+ * enc_gemm, enc_raster and steps_per_graph may change: the others shape the state it carries between steps. */
 int wcb_set_option(wcb_handle* h, const char* name, int value);
 
 /* replaces from_pretrained / load_state_dict: one HF state-dict tensor (host f32, C order), staged
@@ -155,11 +161,15 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
  *    running log-prob sums, scores [R]; wcb_decode_parents then gives parents [R] (int32, DEVICE): the
  *    beam (0..nb-1 of the same utterance) each running beam extends — the running sequences are the
  *    parents' sequences plus next_ids. Once every utterance is done a step changes nothing.
- *  - wcb_decode_result: out_ids [B][max_new] (int32, DEVICE; max_new = max_target_positions - prefix_len
- *    for wcb_decode_begin, max_new_tokens for wcb_decode_begin_beams) and *out_steps (host) = the columns
- *    generated: greedy, the steps taken (finished rows padded); beams, the best finished sequence of each
- *    utterance so far with *out_steps its longest length — after the steps generate() takes, exactly
- *    generate()'s output. */
+ *    Once every utterance is done (wcb_decode_info's *done) the search is frozen: a step writes parents =
+ *    identity and next_ids = pad_token_id, so a consumer that extends its hypotheses every step is unchanged.
+ *  - wcb_decode_info: *max_new = the state's column capacity (max_target_positions - prefix_len for
+ *    wcb_decode_begin, max_new_tokens for wcb_decode_begin_beams), *steps = the steps taken, *done = 1 once
+ *    every utterance (row) has finished (blocks on the decode stream for it); each pointer may be NULL.
+ *  - wcb_decode_result: out_ids [B][out_ld] (int32, DEVICE) receives the n generated columns, *out_steps
+ *    (host) = n: greedy, the steps taken (finished rows padded); beams, the best finished sequence of each
+ *    utterance so far with n its longest length — after the steps generate() takes, exactly generate()'s
+ *    output. out_ld < n is refused (WCB_ERR_ARG); out_ld = *max_new always holds the result. */
 typedef struct wcb_state wcb_state;
 int wcb_decode_begin(wcb_handle* h, const void* enc, int B, int num_beams, const int32_t* prefix, int prefix_len,
                      float bias_boost, int min_new_tokens, wcb_state** out, void* stream);
@@ -167,7 +177,8 @@ int wcb_decode_begin_beams(wcb_handle* h, const void* enc, int B, int num_beams,
                            int max_new_tokens, float bias_boost, int min_new_tokens, wcb_state** out, void* stream);
 int wcb_decode_step(wcb_handle* h, wcb_state* st, const wcb_bias* bias, int32_t* next_ids, float* scores, void* stream);
 int wcb_decode_parents(wcb_handle* h, wcb_state* st, int32_t* parents, void* stream);
-int wcb_decode_result(wcb_handle* h, wcb_state* st, int32_t* out_ids, int32_t* out_steps, void* stream);
+int wcb_decode_info(wcb_handle* h, wcb_state* st, int32_t* max_new, int32_t* steps, int32_t* done);
+int wcb_decode_result(wcb_handle* h, wcb_state* st, int32_t* out_ids, int out_ld, int32_t* out_steps, void* stream);
 int wcb_decode_end(wcb_handle* h, wcb_state* st);
 
 /* wait for every queued front-end / encoder / decode operation of the handle */

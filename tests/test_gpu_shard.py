@@ -1,4 +1,4 @@
-"""GPU, world_size 2: utterance sharding end to end on the device. Two processes
+"""GPU, world_size 2 and 8: utterance sharding end to end on the device. Two processes
 (gloo group; both ranks drive cuda:0 here — the one-GPU box) get the weights by one broadcast of the
 packed bf16 blob, decode their shard of the batch through libwcb with the bias boost, and gather the
 ids; the concatenation in rank order equals the single-process decode of the whole batch. Cases:
@@ -15,7 +15,9 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-CASES = {"tiny.en": (6, 16, 200), "small": (32, 16, 1000)}   # model: clips, tokens, bias phrases
+# name: (model, clips, tokens, bias phrases); "c4" = BASELINE config C4 at its stated shape: whisper-small,
+# 256 clips over 8 ranks (32 per rank), 64 tokens with EOS masked, the 1000-phrase boost at lambda 2
+CASES = {"tiny.en": ("tiny.en", 6, 16, 200), "small": ("small", 32, 16, 1000), "c4": ("small", 256, 64, 1000)}
 
 
 def _free_port():
@@ -41,8 +43,8 @@ def _worker(rank, world, port, outdir, name):
     from whisper_context_biasing_amd.model import WhisperCB
     from whisper_context_biasing_amd.shard import broadcast_weights, gather_shards, shard_bounds
     torch.cuda.set_device(0)
-    n_clips, tokens, n_phr = CASES[name]
-    dims = get_dims(name)
+    size, n_clips, tokens, n_phr = CASES[name]
+    dims = get_dims(size)
     sd = broadcast_weights(dims, torch.device("cpu"), seed=0)
     model = WhisperCB.from_state_dict(dims, sd, dtype="bf16")
     lo, hi = shard_bounds(n_clips, rank, world)
@@ -54,35 +56,41 @@ def _worker(rank, world, port, outdir, name):
     dist.destroy_process_group()
 
 
-def test_bench_launches_its_own_ranks():
-    """`python bench.py --gpus 2` with no torch.distributed.run: the launcher starts two ranks (gloo,
-    both on this box's GPU), each decodes its 32 clips, rank 0 prints the whole-job line."""
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_launches_its_own_ranks(world):
+    """`python bench.py --gpus N` with no torch.distributed.run: the launcher starts N ranks (gloo, all on
+    this box's GPU), each decodes its 32 clips, rank 0 prints the whole-job line. N = 8 is the command form
+    of the driver's C4 scaling run (8 x 32 = 256 clips, utterance-dp8)."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    p = subprocess.run([sys.executable, "-u", os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2",
-                        "--warmup", "1", "--no-cpu-baseline", "--no-profile", "--backend", "gloo"],
+    steps = 2 if world == 2 else 1
+    p = subprocess.run([sys.executable, "-u", os.path.join(root, "bench.py"), "--gpus", str(world), "--steps",
+                        str(steps), "--warmup", "1", "--no-cpu-baseline", "--no-profile", "--backend", "gloo"],
                        capture_output=True, text=True, timeout=900, env=env)
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [s for s in p.stdout.splitlines() if s.strip().startswith("{")]
     assert len(lines) == 1, p.stdout
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "utterance-dp2"
-    assert out["config"]["global_batch"] == 64 and out["config"]["collective_backend"] == "gloo"
-    assert out["value"] > 0 and out["steps"] == 2
+    assert out["n_gpus"] == world and out["config"]["parallelism"] == f"utterance-dp{world}"
+    assert out["config"]["global_batch"] == 32 * world and out["config"]["collective_backend"] == "gloo"
+    assert out["value"] > 0 and out["steps"] == steps
 
 
-@pytest.mark.parametrize("name", ["tiny.en", "small"])
-def test_two_rank_shards_equal_single_process(tmp_path, name):
+@pytest.mark.parametrize("name,world", [("tiny.en", 2), ("small", 2), ("c4", 8)])
+def test_rank_shards_equal_single_process(tmp_path, name, world):
+    """world ranks (gloo, all on this box's one GPU) decode their shards; the ids gathered in rank order
+    equal the single-process decode of the whole batch (generate() splits it into 64-clip calls). The
+    ("c4", 8) case is C4's shape: 8 ranks x 32 clips = 256, whisper-small bf16, 64 tokens, 1000 phrases."""
     from whisper_context_biasing_amd.config import get_dims
     from whisper_context_biasing_amd.model import WhisperCB
     from whisper_context_biasing_amd.shard import broadcast_weights
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), name), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), name), nprocs=world, join=True)
     sharded = np.load(tmp_path / "sharded.npy")
-    n_clips, tokens, n_phr = CASES[name]
-    dims = get_dims(name)
+    size, n_clips, tokens, n_phr = CASES[name]
+    dims = get_dims(size)
     model = WhisperCB.from_state_dict(dims, broadcast_weights(dims, torch.device("cpu"), seed=0), dtype="bf16")
     full = _decode(model, 0, n_clips, dims, tokens, n_phr).numpy()
     assert sharded.shape == full.shape == (n_clips, tokens)

@@ -98,8 +98,48 @@ def test_stepwise_beam5_equals_generate(dtype, boost, prompt):
         assert toks.shape == (B * 5,) and ((par >= 0) & (par < 5)).all()
         assert torch.isfinite(scores[::5]).all()
     got = dec.result(L).cpu().numpy()
+    # the length cap finished every utterance: the search is frozen — a further step gives
+    # identity parents and pad ids, and the result does not change
+    assert dec.done and dec.info()[:2] == (L, L)
+    toks, _ = dec.step()
+    assert (dec.parents().cpu().numpy() == np.tile(np.arange(5), B)).all()
+    assert (toks.cpu().numpy() == dims.pad_token_id).all()
+    assert np.array_equal(dec.result().cpu().numpy(), got)
     dec.close()
     assert np.array_equal(got, ref), (got, ref)
+
+
+def test_stepwise_greedy_result_equals_generate_and_guards():
+    """StepDecoder.result() (wcb_decode_result) for greedy decoding against generate() with the same
+    arguments; the output width comes from the library (wcb_decode_info), a caller width below the
+    generated columns is refused, and every decode option that shapes the state carried between steps
+    (lean_x, merge_v, xq_kq, ...) is refused while the decode is open."""
+    from whisper_context_biasing_amd import _lib
+    dims = get_dims("small")
+    m = WhisperCB.from_state_dict(dims, make_weights(dims, seed=0, recipe="diverse"), dtype="bf16")
+    B, n = 3, 9
+    x = torch.from_numpy(W.log_mel(synth_batch(B), dims.n_mel))
+    ref = m.generate(x, max_length=n, min_new_tokens=n).cpu().numpy()
+    dec = m.decode_begin(m.encode(x), min_new_tokens=n)
+    for opt, v in (("lean_x", 0), ("merge_v", 0), ("xq_kq", 1), ("lm_ln_split", 1), ("xvariant", 1)):
+        with pytest.raises(_lib.WcbError, match=opt):
+            m.set_option(opt, v)
+    m.set_option("enc_raster", 8)                       # encoder-side options stay free
+    for _ in range(n):
+        dec.step()
+    mx, steps, done = dec.info()
+    assert mx == dims.n_text_ctx - 1 and steps == n and not done
+    got = dec.result().cpu().numpy()
+    assert np.array_equal(got, ref), (got, ref)
+    with pytest.raises(ValueError):
+        dec.result(n - 1)
+    # the raw ABI refuses an out_ld below the generated columns instead of writing past the buffer
+    out = torch.empty(B, n - 1, dtype=torch.int32, device=m.device)
+    ns = _lib.C.c_int32(0)
+    rc = m._lib.wcb_decode_result(m._h, dec._st, out.data_ptr(), n - 1, _lib.C.byref(ns), None)
+    assert rc == -1
+    dec.close()
+    m.set_option("lean_x", 1)                            # allowed again once the state is closed
 
 
 # ---------------------------------------------------------------- forward(encoder_outputs / past_key_values)

@@ -1,7 +1,8 @@
 """Check a bench.py JSON line against rocprofv3 output of the same command: the roofline kernel must be
 the top kernel symbol by total time (rocprofv3 --stats' grouping: kernel_stats.csv, or a kernel trace
 grouped the same way), and `frac` recomputed from rocprof's average duration for it must agree
-within 5 %.
+within 5 %. With a `roofline.step`, the step fraction is recomputed from the algorithmic
+work the line states and each phase's fraction from the rocprof trace's kernel times.
 
 usage: python tools/check_roofline.py <bench.json> <kernel_stats.csv | kernel_trace.csv>
 """
@@ -37,8 +38,41 @@ def main():
                    frac_rocprof=round(ach / roof["peak"], 4),
                    rel_diff=round(abs(ach / roof["peak"] - roof["frac"]) / (ach / roof["peak"]), 4))
         out["within_5pct"] = out["rel_diff"] <= 0.05
+    step = roof.get("step")
+    if step:
+        # SURVEY §8(d) step fraction recomputed from the algorithmic work the line states (bytes / flops at
+        # the peaks) over its ms_per_step, and each phase's ideal over the rocprof trace's GPU time of the
+        # kernels of that phase (the bench's class -> kernel map: roofline + roofline_other)
+        w = step["work"]
+        peak_mfma = roof["peak"] if roof["bound"] == "mfma" else 2500.0
+        ideal = {"front_end": w["front_end_bytes"] / 8000e9 * 1e3,
+                 "encoder": w["encoder_flops"] / (peak_mfma * 1e12) * 1e3,
+                 "decode": w["decode_bytes"] / 8000e9 * 1e3}
+        frac = sum(ideal.values()) / step["measured_ms_per_step"]
+        line_all = json.loads(line)
+        cls_kernel = {c: v["kernel"] for c, v in (line_all.get("roofline_other") or {}).items()}
+        for c in roof["class"].split("+"):
+            cls_kernel[c] = roof["kernel"]
+        phase_of = lambda c: ("front_end" if c in ("log_mel", "mel_to_conv_input")
+                              else "encoder" if c.startswith("enc_") or c == "layernorm" else "decode")
+        kern_phase = {}
+        for c, k in cls_kernel.items():
+            kern_phase.setdefault(k, phase_of(c))
+        steps = max(1.0, cnt.get(roof["kernel"], 0) / max(roof["launches_per_step"], 1e-9))
+        meas = collections.defaultdict(float)
+        for k, t in tot.items():
+            if k in kern_phase:
+                meas[kern_phase[k]] += t / 1e6 / steps
+        out["step"] = {"frac_bench": step["frac"], "frac_recomputed": round(frac, 4),
+                       "rel_diff": round(abs(frac - step["frac"]) / frac, 4),
+                       "rocprof_steps": round(steps, 2),
+                       "phases_rocprof": {ph: {"ideal_ms": round(ideal[ph], 4), "rocprof_ms": round(meas[ph], 3),
+                                               "frac": round(ideal[ph] / meas[ph], 4) if meas[ph] else None}
+                                          for ph in ideal}}
+        out["step"]["within_5pct"] = out["step"]["rel_diff"] <= 0.05
     print(json.dumps(out, indent=1))
-    return 0 if out["match"] and out.get("within_5pct") else 1
+    ok = out["match"] and out.get("within_5pct") and (not step or out["step"]["within_5pct"])
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":

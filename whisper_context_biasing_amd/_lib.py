@@ -53,7 +53,8 @@ SIGNATURES = {
     "wcb_decode_begin_beams": (C.c_int, [_P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, C.c_float, C.c_int,
                                          C.POINTER(_P), _P]),
     "wcb_decode_parents": (C.c_int, [_P, _P, _P, _P]),
-    "wcb_decode_result": (C.c_int, [_P, _P, _P, C.POINTER(C.c_int32), _P]),
+    "wcb_decode_info": (C.c_int, [_P, _P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "wcb_decode_result": (C.c_int, [_P, _P, _P, C.c_int, C.POINTER(C.c_int32), _P]),
     "wcb_forward": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, _P, _P, _P]),
     "wcb_forward_enc": (C.c_int, [_P, _P, C.c_int, _P, C.c_int, _P, _P]),
     "wcb_forward_cached": (C.c_int, [_P, _P, _P, C.c_int, _P, _P]),

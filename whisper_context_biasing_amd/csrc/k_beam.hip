@@ -256,7 +256,14 @@ __global__ __launch_bounds__(NT) void beam_topk_kernel(BeamArgs a) {
 }
 
 __global__ __launch_bounds__(256) void beam_step_kernel(BeamArgs a) {
-  if (*a.all_done) return;
+  if (*a.all_done) {   // frozen search: a step changes nothing, so every beam extends itself by pad
+    if (threadIdx.x < a.nb) {
+      const int r = blockIdx.x * a.nb + threadIdx.x;
+      if (a.parent) a.parent[r] = threadIdx.x;
+      a.next_ids[r] = a.pad;
+    }
+    return;
+  }
   __shared__ float tv[kTopK], rlp[kTopK], flv[kTopK];
   __shared__ int tb[kTopK], tt[kTopK], hit[kTopK];
   __shared__ int sel[kMaxBeams], fsrc[kMaxBeams], st_old[kMaxBeams];

@@ -248,6 +248,14 @@ struct wcb_handle {
   // against the LDS-ring kernel's 256x192 tiles, tools/enc_bench.py gemm; the bench line within noise),
   // the LDS-ring kernel for those (1), or the LDS-ring kernel everywhere (0)
   int enc_gemm = 4;
+  // CU split between the encoder and the decode chains (option "cu_split" n, 0 = off): the decode streams
+  // on the CUs of CU-mask bits i < 8n, the encoder stream on the rest. The driver stripes mask bits over
+  // the XCDs (bit i → XCD i % 8) and, within an XCD, over its shader engines, so every XCD and every
+  // engine keeps the same share (tools/cumask_probe.hip): n CUs per XCD decode, 32 − n encode, and the
+  // encoder's persistent GEMM grid is its CU count (enc_cus). Disjoint CUs let the next batch's encoder
+  // run beside the decode chains instead of holding every CU while they wait for slots.
+  int cu_split = 0;
+  int enc_cus = 256;
   // decode projections on gemm_dec_kernel (K supported): the LayerNorm consumers compute their row
   // statistics from the rows they load, so the producers publish no per-16-column partial sums
   bool dec_gemm = false;
@@ -564,12 +572,22 @@ void wcb_destroy(wcb_handle* h) {
 namespace {
 void quiesce(wcb_handle* h);
 void drop_graphs(wcb_handle* h);
+void split_mask(wcb_handle* h, bool dec, std::vector<uint32_t>& m);
 }  // namespace
 
 int wcb_set_option(wcb_handle* h, const char* name, int value) {
   return guarded(h, [&] {
     REQUIRE(h && name, "bad argument");
     const std::string n = name;
+    // An open step-wise decode carries device state across wcb_decode_step calls that the decode options
+    // shaped (the next input's embedding and its fragment-major copy, the LayerNorm statistics the residual
+    // writers published, the encoder-output layout): only the encoder-side and generate()-only options may
+    // change under it (decode_contexts has its own check below).
+    static const char* const kFreeWhileStepwise[] = {"decode_contexts", "enc_flash", "enc_gemm", "enc_raster",
+                                                     "steps_per_graph", "kq_cnt_seed"};
+    bool free_opt = false;
+    for (const char* f : kFreeWhileStepwise) free_opt |= n == f;
+    REQUIRE(free_opt || !h->step_state, "option " + n + ": a step-wise decode is active (wcb_decode_end first)");
     if (n == "xmode" || n == "beam_xmode") {
       REQUIRE(!h->ready, "option " + n + " selects the weight layouts: set it before wcb_finalize_weights");
       REQUIRE(value == 0 || value == 1, "option " + n + ": 0 or 1");
@@ -588,8 +606,6 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       h->group_rows = value;
     } else if (n == "xenc_variant") {
       REQUIRE(value >= 0 && value <= 3, "option xenc_variant: 0..3");
-      // the step-wise state's copy of the encoder output was laid out for the variant at begin time
-      REQUIRE(!h->step_state, "option xenc_variant: a step-wise decode is active (wcb_decode_end first)");
       h->xenc_variant = value;
     } else if (n == "enc_flash") {
       REQUIRE(value == 2 || value == 4, "option enc_flash: 2 or 4");
@@ -613,11 +629,35 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
         std::vector<unsigned long long> v(D.kq_cnt.bytes / 8, 4ull * (unsigned long long)value);
         HIPCHK(hipMemcpy(D.kq_cnt.p, v.data(), v.size() * 8, hipMemcpyHostToDevice));
       }
+    } else if (n == "cu_split") {
+      // decode streams on n CUs of every XCD (mask bits i < 8n), the encoder stream on the others; 0: every
+      // stream on every CU (decode streams at high priority). Re-creates the library's streams.
+      REQUIRE(value >= 0 && value <= 24, "option cu_split: 0..24 (decode CUs per XCD)");
+      quiesce(h);
+      drop_graphs(h);
+      h->cu_split = value;
+      HIPCHK(hipStreamDestroy(h->he));
+      h->he = nullptr;
+      if (value) {
+        std::vector<uint32_t> m;
+        split_mask(h, false, m);
+        HIPCHK(hipExtStreamCreateWithCUMask(&h->he, (uint32_t)m.size(), m.data()));
+        int nc = 0;
+        for (uint32_t w : m) nc += __builtin_popcount(w);
+        h->enc_cus = nc;
+      } else {
+        HIPCHK(hipStreamCreateWithPriority(&h->he, hipStreamNonBlocking, 0));
+        h->enc_cus = 256;
+      }
+      for (DecCtx& D : h->dc) {   // re-created on next use with the new mask
+        if (D.hs) { HIPCHK(hipStreamDestroy(D.hs)); D.hs = nullptr; }
+        for (hipStream_t& sb : D.sub)
+          if (sb) { HIPCHK(hipStreamDestroy(sb)); sb = nullptr; }
+      }
     } else if (n == "steps_per_graph") {
       REQUIRE(value >= 1 && value <= 64, "option steps_per_graph: 1..64");
       h->steps_per_graph = value;
     } else if (n == "xenc_fm") {
-      REQUIRE(!h->step_state, "option xenc_fm: a step-wise decode is active (wcb_decode_end first)");
       h->xenc_fm = value != 0;
     } else if (n == "xq_kq") {
       h->xq_kq = value != 0;
@@ -956,6 +996,7 @@ void run_gemm(wcb_handle* h, const char* cls, const GemmArgs& g0) {
   GemmArgs g = g0;
   g.raster = h->enc_raster;
   g.pp = h->enc_gemm;
+  g.pgrid = h->enc_cus;
   h->timed(cls, 2.0 * g.M * g.N * g.K, 0.0, h->he, [&] { gemm(h->dt, g, h->he); });
 }
 
@@ -1037,15 +1078,36 @@ int prefill_chunk(int R) { return std::max(1, kPrefillRows / std::max(R, 1)); }
 // the decode streams of contexts [c0, c1), created on first use at the highest priority (the decode
 // chains are latency-bound and the next batch's encoder runs beside them: their workgroups dispatch
 // ahead of encoder tiles); row-group streams only when n_sub > 1
+// CU mask of the decode (dec = true) or encoder stream under option cu_split: bits i < 8·cu_split decode
+void split_mask(wcb_handle* h, bool dec, std::vector<uint32_t>& m) {
+  int ncu = 0;
+  HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
+  m.assign((ncu + 31) / 32, 0u);
+  for (int i = 0; i < ncu; ++i)
+    if ((i < 8 * h->cu_split) == dec) m[i / 32] |= 1u << (i % 32);
+}
+
+hipStream_t make_dec_stream(wcb_handle* h) {
+  hipStream_t s = nullptr;
+  if (h->cu_split) {
+    std::vector<uint32_t> m;
+    split_mask(h, true, m);
+    HIPCHK(hipExtStreamCreateWithCUMask(&s, (uint32_t)m.size(), m.data()));
+  } else {
+    int prio_lo = 0, prio_hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    HIPCHK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio_hi));
+  }
+  return s;
+}
+
 void ensure_ctx_streams(wcb_handle* h, int c0, int c1) {
-  int prio_lo = 0, prio_hi = 0;
   for (int ci = c0; ci < c1; ++ci) {
     DecCtx& D = h->dc[ci];
     if (D.hs && (h->n_sub <= 1 || D.sub[0])) continue;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    if (!D.hs) HIPCHK(hipStreamCreateWithPriority(&D.hs, hipStreamNonBlocking, prio_hi));
+    if (!D.hs) D.hs = make_dec_stream(h);
     for (int i = 0; i < DecCtx::kMaxSub && h->n_sub > 1; ++i)
-      if (!D.sub[i]) HIPCHK(hipStreamCreateWithPriority(&D.sub[i], hipStreamNonBlocking, prio_hi));
+      if (!D.sub[i]) D.sub[i] = make_dec_stream(h);
   }
 }
 
@@ -1744,6 +1806,7 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
       HIPCHK(hipMemcpyAsync(&olen, ints + I_UNFIN, 4, hipMemcpyDeviceToHost, D.hs));
       HIPCHK(hipEventRecord(h->ev_dec[buf], D.hs));
       HIPCHK(hipStreamSynchronize(D.hs));
+      if (h->xq_kq) check_dev_err(h);   // the in-launch hand-off's error word: outputs invalid if it is set
       *out_steps = std::min(olen, max_new);
       sync_out(h, stream, D.hs);
       return;
@@ -1751,7 +1814,12 @@ int wcb_generate(wcb_handle* h, const float* mel, int B, const wcb_gen_cfg* cfg,
     HIPCHK(hipMemcpyAsync(out_ids, D.outbuf.p, (size_t)B * out_ld * 4, hipMemcpyDeviceToDevice, D.hs));
     HIPCHK(hipEventRecord(h->ev_dec[buf], D.hs));
     *out_steps = std::min(done, max_new);
-    if (!cfg->async_out) sync_out(h, stream, D.hs);
+    if (!cfg->async_out) {
+      // blocking calls with the in-launch hand-off on (option xq_kq) validate its error word before the ids
+      // are handed out; async calls report it at wcb_synchronize
+      if (h->xq_kq) { HIPCHK(hipStreamSynchronize(D.hs)); check_dev_err(h); }
+      sync_out(h, stream, D.hs);
+    }
   });
 }
 
@@ -1775,7 +1843,7 @@ static void decode_begin_beams(wcb_handle* h, const void* enc, int B, int nb, co
                                int max_new_tokens, float bias_boost, int min_new_tokens, wcb_state** out, void* stream) {
   REQUIRE(h && enc && out && B > 0 && B <= 64, "bad argument (1 <= B <= 64, enc and out required)");
   if (!h->ready) throw WcbError(WCB_ERR_STATE, "weights not finalized");
-  REQUIRE(nb >= 2 && nb <= kMaxBeams, "num_beams must be in [1, 8]");
+  REQUIRE(nb >= 2 && nb <= kMaxBeams, "num_beams must be in [2, 8] (greedy: num_beams = 1)");
   const int R = B * nb;
   REQUIRE(R <= 64 * DecCtx::kMaxSub, "batch x num_beams > 512 rows: split the batch");
   REQUIRE(h->nctx < wcb_handle::kMaxCtx, "step-wise decoding needs a free decode context (decode_contexts <= 3)");
@@ -1812,7 +1880,8 @@ static void decode_begin_beams(wcb_handle* h, const void* enc, int B, int nb, co
   } else {
     fill_i32(ints + I_NEXT, h->d.decoder_start_token_id, R, D.hs);
   }
-  auto* st = new wcb_state;
+  // owned until the device work below succeeded (HIPCHK throws through here)
+  std::unique_ptr<wcb_state> st(new wcb_state);
   st->h = h; st->B = B; st->P = P; st->T = Tc; st->max_new = max_new; st->min_new = min_new_tokens;
   st->xmode = xm; st->lam = bias_boost; st->nb = nb;
   st->bm = beam_args(h, D, B, nb, P, Lt, Tc, max_new, min_new_tokens, bias_boost, h->empty_bias.get());
@@ -1829,8 +1898,8 @@ static void decode_begin_beams(wcb_handle* h, const void* enc, int B, int nb, co
   }
   if (prefix) gather_col(ints + I_NEXT, D.forced.as<int>(), R, P, P - 1, D.hs);
   HIPCHK(hipStreamSynchronize(D.hs));
-  h->step_state = st;
-  *out = st;
+  h->step_state = st.release();
+  *out = h->step_state;
   sync_out(h, stream, D.hs);
 }
 
@@ -1895,8 +1964,20 @@ int wcb_decode_begin(wcb_handle* h, const void* enc, int B, int num_beams, const
 int wcb_decode_step(wcb_handle* h, wcb_state* st, const wcb_bias* bias, int32_t* next_ids, float* scores, void* stream) {
   return guarded(h, [&] {
     REQUIRE(h && st && st->h == h && h->step_state == st && next_ids, "bad argument (state of this handle, next_ids)");
-    REQUIRE(st->steps < st->max_new, "max_target_positions reached");
     REQUIRE(st->fwd == 0, "wcb_decode_step on a forward cache (wcb_forward_cached state)");
+    if (st->steps >= st->max_new) {
+      // the length cap: refused, except for a finished beam search, whose steps are frozen (identity
+      // parents, pad ids; the device position stopped at the last cache slot)
+      bool frozen = false;
+      if (st->nb > 1) {
+        DecCtx& D = h->dc[wcb_handle::kMaxCtx - 1];
+        int v = 0;
+        HIPCHK(hipMemcpyAsync(&v, D.ints.as<int>() + I_DONE, 4, hipMemcpyDeviceToHost, D.hs));
+        HIPCHK(hipStreamSynchronize(D.hs));
+        frozen = v > 0;
+      }
+      REQUIRE(frozen, "max_target_positions reached");
+    }
     const wcb_bias* bs = bias ? bias : h->empty_bias.get();
     REQUIRE(bs == h->empty_bias.get() || bs->owner == h, "bias automaton was created on another handle");
     REQUIRE(bs->vocab == h->d.vocab, "bias automaton built for another vocabulary");
@@ -1949,7 +2030,22 @@ int wcb_decode_parents(wcb_handle* h, wcb_state* st, int32_t* parents, void* str
   });
 }
 
-int wcb_decode_result(wcb_handle* h, wcb_state* st, int32_t* out_ids, int32_t* out_steps, void* stream) {
+int wcb_decode_info(wcb_handle* h, wcb_state* st, int32_t* max_new, int32_t* steps, int32_t* done) {
+  return guarded(h, [&] {
+    REQUIRE(h && st && st->h == h && h->step_state == st, "bad argument (state of this handle)");
+    if (max_new) *max_new = st->max_new;
+    if (steps) *steps = st->steps;
+    if (done) {   // the device's all-finished flag (I_DONE: the step at which every utterance / row was done)
+      DecCtx& D = h->dc[wcb_handle::kMaxCtx - 1];
+      int v = 0;
+      HIPCHK(hipMemcpyAsync(&v, D.ints.as<int>() + I_DONE, 4, hipMemcpyDeviceToHost, D.hs));
+      HIPCHK(hipStreamSynchronize(D.hs));
+      *done = v > 0 ? 1 : 0;
+    }
+  });
+}
+
+int wcb_decode_result(wcb_handle* h, wcb_state* st, int32_t* out_ids, int out_ld, int32_t* out_steps, void* stream) {
   return guarded(h, [&] {
     REQUIRE(h && st && st->h == h && h->step_state == st && out_ids && out_steps, "bad argument");
     REQUIRE(st->fwd == 0, "wcb_decode_result on a forward cache (wcb_forward_cached state)");
@@ -1965,7 +2061,12 @@ int wcb_decode_result(wcb_handle* h, wcb_state* st, int32_t* out_ids, int32_t* o
       HIPCHK(hipStreamSynchronize(D.hs));
       n = std::min(olen, st->max_new);
     }
-    HIPCHK(hipMemcpyAsync(out_ids, D.outbuf.p, (size_t)st->B * st->max_new * 4, hipMemcpyDeviceToDevice, D.hs));
+    // the library's output rows are st->max_new wide; the caller's out_ld columns must hold the n generated
+    REQUIRE(out_ld >= n && out_ld >= 1, "wcb_decode_result: out_ld " + std::to_string(out_ld) + " < the " +
+                                            std::to_string(n) + " generated columns (wcb_decode_info gives the width)");
+    if (n > 0)
+      HIPCHK(hipMemcpy2DAsync(out_ids, (size_t)out_ld * 4, D.outbuf.p, (size_t)st->max_new * 4, (size_t)n * 4,
+                              st->B, hipMemcpyDeviceToDevice, D.hs));
     *out_steps = n;
     sync_out(h, stream, D.hs);
   });

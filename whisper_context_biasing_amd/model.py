@@ -113,13 +113,31 @@ class StepDecoder:
         _lib.check(m._lib.wcb_decode_parents(m._h, self._st, _ptr(par), _stream(m.device)), m._h, "wcb_decode_parents")
         return par
 
-    def result(self, max_new: int):
-        """[B, n] int64 ids as generate() returns them (Whisper-trimmed), n = the generated columns."""
+    def info(self):
+        """(max_new, steps, done): the state's column capacity, the steps taken, and whether every utterance
+        has finished (beams: the search is frozen — further steps give identity parents and pad ids)."""
         m = self.model
-        out = torch.empty(self.B, max_new, dtype=torch.int32, device=m.device)
+        mx, st, dn = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+        _lib.check(m._lib.wcb_decode_info(m._h, self._st, C.byref(mx), C.byref(st), C.byref(dn)), m._h,
+                   "wcb_decode_info")
+        return mx.value, st.value, bool(dn.value)
+
+    @property
+    def done(self) -> bool:
+        return self.info()[2]
+
+    def result(self, max_new: Optional[int] = None):
+        """[B, n] int64 ids as generate() returns them (Whisper-trimmed), n = the generated columns. The
+        output width is the library's (wcb_decode_info); `max_new` is accepted for compatibility and, when
+        given, must be at least the number of generated columns."""
+        m = self.model
+        width = self.info()[0]
+        out = torch.empty(self.B, width, dtype=torch.int32, device=m.device)
         n = C.c_int32(0)
-        _lib.check(m._lib.wcb_decode_result(m._h, self._st, _ptr(out), C.byref(n), _stream(m.device)), m._h,
+        _lib.check(m._lib.wcb_decode_result(m._h, self._st, _ptr(out), width, C.byref(n), _stream(m.device)), m._h,
                    "wcb_decode_result")
+        if max_new is not None and max_new < n.value:
+            raise ValueError(f"result(max_new={max_new}): {n.value} columns were generated")
         return m._whisper_trim(out[:, :n.value].to(torch.int64))
 
     def close(self):
