@@ -90,10 +90,6 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "enc_gemm" v       encoder GEMM kernels: 4 (default) the ping-pong kernel, 256- or 192-wide tiles by the
  *                      fewer tile rounds; 1 the LDS-ring kernel's 256x192 tiles where 192-wide wins; 0 the
  *                      LDS-ring kernel everywhere
- *   "cu_split" n       CU split (0..24): the decode streams on n CUs of every XCD (CU-mask bits i < 8n; the
- *                      driver stripes mask bits over XCDs, then shader engines), the front end / encoder
- *                      stream on the others, so the next batch's encoder runs beside the decode chains; 0:
- *                      every stream on every CU. Re-creates the handle's streams; bit-identical
  * While a step-wise decode is open (wcb_decode_begin .. wcb_decode_end) only decode_contexts, enc_flash,
  * enc_gemm, enc_raster and steps_per_graph may change: the others shape the state it carries between steps. */
 int wcb_set_option(wcb_handle* h, const char* name, int value);

@@ -313,24 +313,3 @@ def test_folded_layernorm_beam_rows_match_layernorm_launch(dtype):
     ref = generate_beam(om, mel=x[:1].numpy(), num_beams=5, max_length=10, bias=phrases, bias_boost=2.0)
     np.testing.assert_array_equal(a[:1, :ref.shape[1]], ref)
 
-
-def test_cu_split_is_bit_identical():
-    """Option cu_split (decode streams on n CUs of every XCD, the encoder on the rest; the ping-pong
-    encoder GEMM's persistent grid shrinks to the encoder's CUs) changes where work runs, never its
-    arithmetic: encoder outputs and the boosted C2-shaped decode (whisper-small bf16, 32 clips, 1000
-    phrases) are bit-identical to the unsplit handle, through pipelined non-blocking calls too."""
-    dims = get_dims("small")
-    sd = make_weights(dims, seed=1, recipe="margin")
-    x = torch.from_numpy(W.log_mel(synth_batch(32), dims.n_mel))
-    phrases = synth_bias_list(1000, eot=dims.eos_token_id)
-    kw = dict(max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0)
-    m = WhisperCB.from_state_dict(dims, sd, dtype="bf16")
-    ref_enc = m.encode(x).clone()
-    ref = m.generate(x, **kw).cpu()
-    for n in (8, 4, 0):
-        m.set_option("cu_split", n)
-        assert torch.equal(m.encode(x), ref_enc), n
-        outs = [m.generate(x, block=False, **kw) for _ in range(3)]   # batches in flight on both stream sets
-        m.synchronize()
-        for o in outs:
-            assert torch.equal(o.cpu(), ref), n

@@ -836,7 +836,7 @@ static void launch_pp_e(const GemmArgs& g, hipStream_t s) {
   }
   const int tiles = ((g.M + 255) / 256) * (g.N / BN);
   // one persistent workgroup per CU (LDS-bound); pp 3 (tools/gemm_probe): one tile per workgroup
-  const dim3 grid((unsigned)(g.pp == 3 ? tiles : std::min(tiles, g.pgrid > 0 ? g.pgrid : 256)));
+  const dim3 grid((unsigned)(g.pp == 3 ? tiles : std::min(tiles, 256)));
   WCB_LAUNCH((gemm_pp_kernel<T, EPI, BN>), grid, dim3(512), kLds, s, g);
 }
 

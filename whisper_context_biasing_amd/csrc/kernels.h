@@ -108,9 +108,6 @@ struct GemmArgs {
   int raster = 0;
   // 16-bit encoder GEMMs: the ping-pong kernel (gemm_impl.h gemm_pp_kernel) where it covers the launch
   int pp = 0;
-  // the ping-pong kernel's persistent grid: one workgroup per CU of the stream it runs on (the encoder
-  // stream's CU mask under option "cu_split"; 256 = every CU of MI355X)
-  int pgrid = 256;
   // lean LN-fused cross-attention query (EPI 0): q'_h = W_k,hᵀ q_h in the same launch (kq_w = W_kt's
   // fragment-major copy, kq_out [M][kq_ld] = [M][H·d], heads in hs_H). kq_cnt: the launch's arrival
   // counters ([row blocks][hs_H], 64-bit, zeroed once at allocation, monotonic: 2^64 arrivals never wrap);

@@ -248,14 +248,6 @@ struct wcb_handle {
   // against the LDS-ring kernel's 256x192 tiles, tools/enc_bench.py gemm; the bench line within noise),
   // the LDS-ring kernel for those (1), or the LDS-ring kernel everywhere (0)
   int enc_gemm = 4;
-  // CU split between the encoder and the decode chains (option "cu_split" n, 0 = off): the decode streams
-  // on the CUs of CU-mask bits i < 8n, the encoder stream on the rest. The driver stripes mask bits over
-  // the XCDs (bit i → XCD i % 8) and, within an XCD, over its shader engines, so every XCD and every
-  // engine keeps the same share (tools/cumask_probe.hip): n CUs per XCD decode, 32 − n encode, and the
-  // encoder's persistent GEMM grid is its CU count (enc_cus). Disjoint CUs let the next batch's encoder
-  // run beside the decode chains instead of holding every CU while they wait for slots.
-  int cu_split = 0;
-  int enc_cus = 256;
   // decode projections on gemm_dec_kernel (K supported): the LayerNorm consumers compute their row
   // statistics from the rows they load, so the producers publish no per-16-column partial sums
   bool dec_gemm = false;
@@ -572,7 +564,6 @@ void wcb_destroy(wcb_handle* h) {
 namespace {
 void quiesce(wcb_handle* h);
 void drop_graphs(wcb_handle* h);
-void split_mask(wcb_handle* h, bool dec, std::vector<uint32_t>& m);
 }  // namespace
 
 int wcb_set_option(wcb_handle* h, const char* name, int value) {
@@ -628,31 +619,6 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
         if (!D.kq_cnt.p) continue;
         std::vector<unsigned long long> v(D.kq_cnt.bytes / 8, 4ull * (unsigned long long)value);
         HIPCHK(hipMemcpy(D.kq_cnt.p, v.data(), v.size() * 8, hipMemcpyHostToDevice));
-      }
-    } else if (n == "cu_split") {
-      // decode streams on n CUs of every XCD (mask bits i < 8n), the encoder stream on the others; 0: every
-      // stream on every CU (decode streams at high priority). Re-creates the library's streams.
-      REQUIRE(value >= 0 && value <= 24, "option cu_split: 0..24 (decode CUs per XCD)");
-      quiesce(h);
-      drop_graphs(h);
-      h->cu_split = value;
-      HIPCHK(hipStreamDestroy(h->he));
-      h->he = nullptr;
-      if (value) {
-        std::vector<uint32_t> m;
-        split_mask(h, false, m);
-        HIPCHK(hipExtStreamCreateWithCUMask(&h->he, (uint32_t)m.size(), m.data()));
-        int nc = 0;
-        for (uint32_t w : m) nc += __builtin_popcount(w);
-        h->enc_cus = nc;
-      } else {
-        HIPCHK(hipStreamCreateWithPriority(&h->he, hipStreamNonBlocking, 0));
-        h->enc_cus = 256;
-      }
-      for (DecCtx& D : h->dc) {   // re-created on next use with the new mask
-        if (D.hs) { HIPCHK(hipStreamDestroy(D.hs)); D.hs = nullptr; }
-        for (hipStream_t& sb : D.sub)
-          if (sb) { HIPCHK(hipStreamDestroy(sb)); sb = nullptr; }
       }
     } else if (n == "steps_per_graph") {
       REQUIRE(value >= 1 && value <= 64, "option steps_per_graph: 1..64");
@@ -996,7 +962,6 @@ void run_gemm(wcb_handle* h, const char* cls, const GemmArgs& g0) {
   GemmArgs g = g0;
   g.raster = h->enc_raster;
   g.pp = h->enc_gemm;
-  g.pgrid = h->enc_cus;
   h->timed(cls, 2.0 * g.M * g.N * g.K, 0.0, h->he, [&] { gemm(h->dt, g, h->he); });
 }
 
@@ -1078,26 +1043,11 @@ int prefill_chunk(int R) { return std::max(1, kPrefillRows / std::max(R, 1)); }
 // the decode streams of contexts [c0, c1), created on first use at the highest priority (the decode
 // chains are latency-bound and the next batch's encoder runs beside them: their workgroups dispatch
 // ahead of encoder tiles); row-group streams only when n_sub > 1
-// CU mask of the decode (dec = true) or encoder stream under option cu_split: bits i < 8·cu_split decode
-void split_mask(wcb_handle* h, bool dec, std::vector<uint32_t>& m) {
-  int ncu = 0;
-  HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
-  m.assign((ncu + 31) / 32, 0u);
-  for (int i = 0; i < ncu; ++i)
-    if ((i < 8 * h->cu_split) == dec) m[i / 32] |= 1u << (i % 32);
-}
-
 hipStream_t make_dec_stream(wcb_handle* h) {
   hipStream_t s = nullptr;
-  if (h->cu_split) {
-    std::vector<uint32_t> m;
-    split_mask(h, true, m);
-    HIPCHK(hipExtStreamCreateWithCUMask(&s, (uint32_t)m.size(), m.data()));
-  } else {
-    int prio_lo = 0, prio_hi = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    HIPCHK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio_hi));
-  }
+  int prio_lo = 0, prio_hi = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  HIPCHK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio_hi));
   return s;
 }
 
