@@ -313,3 +313,4 @@ def test_folded_layernorm_beam_rows_match_layernorm_launch(dtype):
     ref = generate_beam(om, mel=x[:1].numpy(), num_beams=5, max_length=10, bias=phrases, bias_boost=2.0)
     np.testing.assert_array_equal(a[:1, :ref.shape[1]], ref)
 
+
