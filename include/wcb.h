@@ -69,6 +69,9 @@ const char* wcb_last_error(const wcb_handle* h);
  *                      keeps W·diag(γ) copies of QKV / cross-q / fc1, ≈ +1/4 of the decoder weights), or its own
  *                      launch (0); before finalize
  *   "merge_v" 0/1      greedy encoder-space cross-attention: range merge and W_v fused (1) or two launches
+ *   "xpart16" 0/1      greedy encoder-space cross-attention (fused merge): the key-range partials stored in the
+ *                      model dtype, each normalised by its own softmax sum, (max, sum) in f32 (1, default: half
+ *                      the partial bytes) or unnormalised f32 partials (0)
  *   "xq_kq" 0/1        greedy encoder-space cross-attention query (lean path): q'_h = W_k,hᵀ q_h computed inside
  *                      the LN-fused q_proj launch (1) or as a launch of its own (0, default); bit-identical
  *   "lean" 0/1         decode projections of <= 64 rows (16-bit) on the lean single-tile kernel (1, default)

@@ -248,7 +248,7 @@ def _xattn_enc(dt, q, enc, wk, wv, bv, nsplit, variant=1):
     return o
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "0", "3", "101"])
+@pytest.mark.parametrize("variant", ["1", "2", "0", "3", "101", "1001"])
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
 @pytest.mark.parametrize("d,B,S,nsplit", [(768, 32, 1500, 8), (768, 5, 1500, 1), (384, 3, 1500, 16), (64, 2, 1500, 3),
                                           (1024, 2, 1500, 8), (512, 4, 100, 4), (768, 3, 37, 2), (384, 1, 1, 1)])

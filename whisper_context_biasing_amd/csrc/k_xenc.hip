@@ -273,7 +273,8 @@ template <int D, int WNW = 4> struct XregCfg {
 // NR = chunks in flight per wave (register ring depth): 2 (two workgroups per CU) or 3 (one).
 // FM: the encoder output in the fragment-major chunk layout of xenc_fm_kernel (below): every load
 // wave-instruction reads 1 KiB contiguous, where the row layout touches 16 key rows x 64 B.
-template <typename T, int D, int NR, int WNW = 4, bool FM = false>
+// P16: the range partials stored in T, normalised by the range's own Σ p (XencArgs::part16)
+template <typename T, int D, int NR, int WNW = 4, bool FM = false, bool P16 = false>
 __global__ __launch_bounds__((XregCfg<D, WNW>::NW * 64), ((NR == 2 && WNW == 4) ? 2 : 1)) void attn_xenc_reg_kernel(XencArgs a) {
   using Frag = typename DT<T>::frag;
   using C = XregCfg<D, WNW>;
@@ -421,9 +422,22 @@ __global__ __launch_bounds__((XregCfg<D, WNW>::NW * 64), ((NR == 2 && WNW == 4) 
   XPROBE(10);
   if (hq < a.H) {
     const long slot = ((long)b * a.nsplit + split) * a.H + hq;
-    float* pp = a.part + slot * D + cw0 + 4 * (lane >> 4);
+    if constexpr (P16) {   // Σ_j p_j e_j / Σ_j p_j in T (a convex combination of encoder values): 8 B per lane
+      T* pp = reinterpret_cast<T*>(a.part) + slot * D + cw0 + 4 * (lane >> 4);
+      const float il = l_run > 0.f ? 1.f / l_run : 0.f;   // an empty range publishes Σ p = 0 (weight 0)
+      typedef short s4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int t = 0; t < CTW; ++t) *reinterpret_cast<f32x4*>(pp + t * 16) = acc[t];
+      for (int t = 0; t < CTW; ++t) {
+        s4 hv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hv[e] = __builtin_bit_cast(short, DT<T>::fromf(acc[t][e] * il));
+        *reinterpret_cast<s4*>(pp + t * 16) = hv;
+      }
+    } else {
+      float* pp = a.part + slot * D + cw0 + 4 * (lane >> 4);
+#pragma unroll
+      for (int t = 0; t < CTW; ++t) *reinterpret_cast<f32x4*>(pp + t * 16) = acc[t];
+    }
     if (wave == 0 && lane < 16) *reinterpret_cast<float2*>(a.ml + slot * 2) = float2{m_run, l_run};
   }
 #ifdef WCB_XENC_PROBE
@@ -487,7 +501,7 @@ __global__ __launch_bounds__(256) void xenc_merge_kernel(XencArgs a, T* u, long 
 // (u is exactly representable in T, so the B operand is u itself). Every weight load is issued before
 // the partials (they do not depend on them). The MFMA form replaced VALU dot products (r04 probe: 7.6k
 // cycles of the launch): 7.55 -> 7.08 us per C2 launch in the bench's serialised pass.
-template <typename T, int D, int MS, int RPW>
+template <typename T, int D, int MS, int RPW, bool P16 = false>
 __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* wv, const T* wfm, const float* bv, T* out, long ldo) {
   using Frag = typename DT<T>::frag;
   constexpr int KS = D / 32;
@@ -509,13 +523,20 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
     for (int ks = 0; ks < KS; ++ks) wf[ks] = load_frag<T>(wr + ks * kstep);
   }
   const int c = min(tid * 4, D - 4);
-  f32x4 pv[RPW][MS];
+  using PV = typename std::conditional<P16, uint2, f32x4>::type;   // P16: four T values, decoded after the loads
+  PV pv[RPW][MS];
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     const int b = min(blockIdx.y * RPW + r, a.rows - 1);
-    const float* pp = a.part + ((long)b * ns * a.H + h) * D;
+    if constexpr (P16) {
+      const T* pp = reinterpret_cast<const T*>(a.part) + ((long)b * ns * a.H + h) * D;
 #pragma unroll
-    for (int s = 0; s < MS; ++s) pv[r][s] = *reinterpret_cast<const f32x4*>(pp + (long)min(s, ns - 1) * a.H * D + c);
+      for (int s = 0; s < MS; ++s) pv[r][s] = *reinterpret_cast<const uint2*>(pp + (long)min(s, ns - 1) * a.H * D + c);
+    } else {
+      const float* pp = a.part + ((long)b * ns * a.H + h) * D;
+#pragma unroll
+      for (int s = 0; s < MS; ++s) pv[r][s] = *reinterpret_cast<const f32x4*>(pp + (long)min(s, ns - 1) * a.H * D + c);
+    }
     const float2 mlv = *reinterpret_cast<const float2*>(a.ml + (((long)b * ns + min(tid, ns - 1)) * a.H + h) * 2);
     if (tid < MS) sv[r][tid] = tid < ns ? mlv : float2{0.f, 0.f};
   }
@@ -541,7 +562,18 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
     const float inv = 1.f / L;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < MS; ++s) acc += w[s] * pv[r][s];
+    for (int s = 0; s < MS; ++s) {
+      if constexpr (P16) {   // normalised partials: weight w_s·Σp_s
+        const uint2 q = pv[r][s];
+        const uint32_t hw[4] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16};
+        f32x4 x;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = DT<T>::tof(__builtin_bit_cast(T, (uint16_t)hw[e]));
+        acc += (w[s] * v[s].y) * x;
+      } else {
+        acc += w[s] * pv[r][s];
+      }
+    }
     acc *= inv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc[e] = DT<T>::tof(DT<T>::fromf(acc[e]));   // u in T, as stored unfused
@@ -644,6 +676,19 @@ static void launch_xenc(const XencArgs& a, hipStream_t s) {
                               XregCfg<D>::LDS);
     attr_set = true;
   }
+  if (a.part16) {   // 16-bit normalised range partials (the register-ring variant 1)
+    static bool attr16 = false;
+    if (!attr16) {
+      (void)hipFuncSetAttribute((const void*)attn_xenc_reg_kernel<T, D, 2, 4, true, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, XregCfg<D>::LDS);
+      (void)hipFuncSetAttribute((const void*)attn_xenc_reg_kernel<T, D, 2, 4, false, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, XregCfg<D>::LDS);
+      attr16 = true;
+    }
+    if (a.fm) WCB_LAUNCH((attn_xenc_reg_kernel<T, D, 2, 4, true, true>), dim3(a.nsplit, a.rows), dim3(XregCfg<D>::NW * 64), XregCfg<D>::LDS, s, a);
+    else WCB_LAUNCH((attn_xenc_reg_kernel<T, D, 2, 4, false, true>), dim3(a.nsplit, a.rows), dim3(XregCfg<D>::NW * 64), XregCfg<D>::LDS, s, a);
+    return;
+  }
   if (a.fm) {   // the fragment-major chunk layout (register-ring variants 1 and 2 only)
     if (a.variant == 2)
       WCB_LAUNCH((attn_xenc_reg_kernel<T, D, 3, 4, true>), dim3(a.nsplit, a.rows), dim3(XregCfg<D>::NW * 64), XregCfg<D>::LDS, s, a);
@@ -714,7 +759,9 @@ static void launch_merge_v_t(const XencArgs& a, const void* wv, const void* wfm,
   const dim3 grid(a.H, (a.rows + 1) / 2);
 #define WCB_XC(DD)                                                                                                    \
   case DD:                                                                                                            \
-    if (a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8, 2>), grid, dim3(256), 0, s, a, (const T*)wv, (const T*)wfm, bv, (T*)o, ldo); \
+    if (a.part16 && a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8, 2, true>), grid, dim3(256), 0, s, a, (const T*)wv, (const T*)wfm, bv, (T*)o, ldo); \
+    else if (a.part16) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, kXencMaxSplit, 2, true>), grid, dim3(256), 0, s, a, (const T*)wv, (const T*)wfm, bv, (T*)o, ldo); \
+    else if (a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8, 2>), grid, dim3(256), 0, s, a, (const T*)wv, (const T*)wfm, bv, (T*)o, ldo); \
     else WCB_LAUNCH((xenc_merge_v_kernel<T, DD, kXencMaxSplit, 2>), grid, dim3(256), 0, s, a, (const T*)wv, (const T*)wfm, bv, (T*)o, ldo);   \
     break;
   switch (a.D) { WCB_XC(128) WCB_XC(256) WCB_XC(384) WCB_XC(512) WCB_XC(768) WCB_XC(1024) default: break; }

@@ -192,6 +192,9 @@ struct XencArgs {
   int variant = 1;                              // 1 register chunk ring, 0 LDS-DMA chunk ring
   int row0 = 0, rows_per_enc = 1;               // row b reads encoder output (row0 + b) / rows_per_enc
   int fm = 0;                                   // enc in the fragment-major chunk layout (xenc_to_fm; variants 1, 2)
+  // range partials in the model dtype, each normalised by its own Σ p (part then holds [rows][nsplit][H][D]
+  // T values: half the bytes), the (max, Σ p) pairs in f32 as before. fm variants + xenc_merge_v only
+  int part16 = 0;
 };
 bool xenc_supported(DType t, int D);
 // enc [B][S][D] → the fragment-major chunk layout of the register-ring kernel (xenc_fm_elems(B, S, D)

@@ -190,6 +190,11 @@ struct wcb_handle {
   // greedy cross-attention (encoder space): range merge and W_v in one launch (option "merge_v";
   // C2 16,570 vs 16,259 audio-s/s for the two launches)
   int merge_v = 1;
+  // greedy cross-attention: range partials in the model dtype, normalised per range (option "xpart16";
+  // half the partial bytes the attention writes and the merge reads; (max, Σp) stay f32). Measured: C2
+  // 19,607 / 19,555 vs 19,276 / 19,395 audio-s/s (interleaved, one box); the GPU suite (goldens, bf16
+  // margin gates) green with it
+  int xpart16 = 1;
   // greedy cross-attention query (<= 64 rows, encoder space, lean path): q'_h = W_k,hᵀ q_h inside the
   // LN-fused q_proj launch (option "xq_kq" 1; gemm_impl.h dec_lean_kernel FZ 2) or as a launch of its
   // own (0, default; bit-identical). Serialised, the fused launch is the faster (6.9 vs 4.4 + 3.0 µs);
@@ -639,6 +644,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       h->lean = value != 0;
     } else if (n == "lean_x") {
       h->lean_x = value != 0;
+    } else if (n == "xpart16") {
+      h->xpart16 = value != 0;
     } else if (n == "merge_v") {
       h->merge_v = value != 0;
     } else if (n == "ln_fold") {
@@ -1302,6 +1309,8 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       xa.variant = h->xenc_variant;
       xa.part = D.xpart.as<float>() + (size_t)r0 * h->xenc_split * H * d;
       xa.ml = D.xml.as<float>() + (size_t)r0 * h->xenc_split * H * 2;
+      const bool fused_merge = h->merge_v && d % 128 == 0;
+      xa.part16 = h->xpart16 && xa.fm && fused_merge;
       if (h->prof_stamps) {
         xa.stamp.base = h->stamp_base(c.buf, 0);
         xa.stamp.pos = pos;
@@ -1310,8 +1319,8 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       // algorithmic bytes: every distinct clip's encoder output once (beams of a clip share it)
       h->timed("dec_xattn", 4.0 * M * H * (double)S * d, (double)nb / c.nb * S * d * e, st_,
                [&] { xenc_attention(h->dt, xa, st_); });
-      if (h->merge_v && d % 128 == 0) {   // range merge + o_h = W_v,h u_h + b_v,h in one launch
-        h->timed("dec_xmerge", 0, (double)M * H * d * h->xenc_split * 4.0 + (double)d * d * e, st_,
+      if (fused_merge) {   // range merge + o_h = W_v,h u_h + b_v,h in one launch
+        h->timed("dec_xmerge", 0, (double)M * H * d * h->xenc_split * (xa.part16 ? e : 4.0) + (double)d * d * e, st_,
                  [&] { xenc_merge_v(h->dt, xa, w.xv_w, w.xv_b, datt, d, st_, w.xv_fm); });
       } else {
         char* du = (char*)D.du.p + (size_t)r0 * H * d * e;
@@ -2447,8 +2456,10 @@ int wcb_op_cross_attention_enc(int dtype, const void* q, const void* enc, const 
     xa.enc = enc; xa.enc_sb = (long)S * d; xa.qp = qp.p; xa.rows = B; xa.H = H; xa.D = d; xa.S = S;
     xa.nsplit = nsplit; xa.part = part.as<float>(); xa.ml = ml.as<float>();
     xa.variant = variant % 100;
+    xa.part16 = variant >= 1000 && d % 128 == 0;   // variant + 1000: 16-bit normalised range partials
+    if (xa.part16) xa.variant = 1;
     xenc_attention(DType(dtype), xa, (hipStream_t)stream);
-    if (d % 128 == 0 && variant < 100) {   // the runtime's default: merge + W_v fused
+    if (d % 128 == 0 && (variant < 100 || variant >= 1000)) {   // the runtime's default: merge + W_v fused
       xenc_merge_v(DType(dtype), xa, wv, bv, o, d, (hipStream_t)stream);
     } else {   // variant + 100: merge kernel + grouped W_v GEMM (option merge_v = 0, and d = 64)
       xenc_merge(DType(dtype), xa, u.p, (long)H * d, (hipStream_t)stream);
