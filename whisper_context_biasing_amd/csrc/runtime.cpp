@@ -225,7 +225,9 @@ struct wcb_handle {
   // beam configurations decode faster as one chain of 80-320-row launches than as 64-row chains on
   // parallel streams (measured: C3 1814 -> 2215, C5 864 -> 983 audio-s/s; profiles/r01c_sweep_grp_*)
   int group_rows = 512;
-  int xenc_split = 8;   // key ranges per row of the encoder-space kernel (rows x ranges workgroups)
+  // key ranges per row of the encoder-space kernel (rows x ranges workgroups). With 16-bit partials
+  // (xpart16) measured C2 6: 19,496 / 19,581, 8: 19,356 / 19,301, 10: 18,246, 12: 18,743, 16: 18,120
+  int xenc_split = 6;
   // the decode's copy of the encoder output in the fragment-major chunk layout (k_xenc.hip
   // xenc_fm_kernel): 1 KiB contiguous per load wave-instruction of the register-ring kernel, where the
   // row layout touches 16 rows x 64 B (option "xenc_fm"; variants 1 and 2; bit-identical)
