@@ -275,9 +275,9 @@ def test_c3_medium_bf16_64clips_beam5_1000_phrase_boost():
 def test_c3_beam5_at_the_benchmarked_length():
     """C3 as bench.py times it: 64 clips x beam 5, bf16, 1000 phrases, 64 new tokens
     with EOS masked — the key-map reorder and the self-KV cache well past the 16 positions the reference
-    beam goldens reach: clip 0 identical to the oracle's beam search over all 64 tokens, clips 62-63
-    identical to a 2-clip call."""
-    check_beam5_boost("medium", "bf16", 1000, 64, 1, max_length=64, min_new=64)
+    beam goldens reach: clips 0-1 identical to the oracle's beam search over all 64 tokens (VERDICT r05 weak
+    1: clip 0 only before), clips 62-63 identical to a 2-clip call."""
+    check_beam5_boost("medium", "bf16", 1000, 64, 2, max_length=64, min_new=64)
 
 
 # ------------------------------------------------------------------ whisper-large-v3, 32 layers (C5)
@@ -299,10 +299,10 @@ def test_c5_large_v3_f16_16clips_beam5_5000_phrase_boost():
 
 def test_c5_timed_path_pcm_to_beams():
     """C5's timed step end to end: large-v3's 128-bin front end on the device (PCM → wcb_log_mel), then
-    16 clips x beam 5, fp16, the 5000-phrase list behind the word-start gate (lambda 2), 32 new tokens with
-    EOS masked (the benchmark mode; VERDICT r04 weak 1: beyond the 12 positions of the reference goldens),
-    against the oracle's PCM → log-mel → beam search on clip 0 (high-margin recipe: identical beams), and
-    the library's mel within 1e-4 of the oracle's."""
+    16 clips x beam 5, fp16, the 5000-phrase list behind the word-start gate (lambda 2), the bench's 64 new
+    tokens with EOS masked (the benchmark mode; VERDICT r04 / r05 weak 1: beyond the 12 positions of the
+    reference goldens), against the oracle's PCM → log-mel → beam search on clips 0-1 (high-margin recipe:
+    identical beams), and the library's mel within 1e-4 of the oracle's."""
     dims = get_dims("large-v3")
     m = model("large-v3", 1, "margin", "f16")
     ws = synth_word_start(dims.eos_token_id, dims.vocab)
@@ -311,20 +311,20 @@ def test_c5_timed_path_pcm_to_beams():
     m.set_word_start(ws)
     try:
         mel_lib = m.log_mel(torch.from_numpy(pcm).cuda())
-        ids = m.generate(mel_lib, max_length=32, min_new_tokens=32, num_beams=5, bias_list=phrases,
+        ids = m.generate(mel_lib, max_length=64, min_new_tokens=64, num_beams=5, bias_list=phrases,
                          bias_boost=2.0).cpu().numpy()
     finally:
         m.set_word_start(None)
     assert ids.shape[0] == 16 and mel_lib.shape == (16, 128, 3000)
-    mel_ora = W.log_mel(pcm[:1], dims.n_mel)
-    assert np.abs(mel_lib[:1].cpu().numpy() - mel_ora).max() < 1e-4
+    mel_ora = W.log_mel(pcm[:2], dims.n_mel)
+    assert np.abs(mel_lib[:2].cpu().numpy() - mel_ora).max() < 1e-4
     om = W.OracleModel.from_dims(dims, weights("large-v3", 1, "margin"))
-    ref = generate_beam(om, mel=mel_ora, num_beams=5, max_length=32, min_new_tokens=32, bias=phrases, bias_boost=2.0,
+    ref = generate_beam(om, mel=mel_ora, num_beams=5, max_length=64, min_new_tokens=64, bias=phrases, bias_boost=2.0,
                         word_start=ws)
-    assert ref.shape[1] >= 32
+    assert ref.shape[1] >= 64
     w = max(ids.shape[1], ref.shape[1])
     pad = lambda a: np.pad(a, ((0, 0), (0, w - a.shape[1])), constant_values=dims.pad_token_id)
-    assert np.array_equal(pad(ids[:1]), pad(ref)), (ids[:1], ref)
+    assert np.array_equal(pad(ids[:2]), pad(ref)), (ids[:2], ref)
 
 
 # ------------------------------------------------------------------ prompt-conditioned decode (causal prefill)
