@@ -38,6 +38,15 @@ def main():
                    frac_rocprof=round(ach / roof["peak"], 4),
                    rel_diff=round(abs(ach / roof["peak"] - roof["frac"]) / (ach / roof["peak"]), 4))
         out["within_5pct"] = out["rel_diff"] <= 0.05
+        if roof.get("avg_launch_ms_serialised"):
+            # rocprofv3's kernel trace serialises the replayed graph's kernels: its per-launch duration is the
+            # bench's serialised profiling pass (HIP events), while the primary figure comes from device stamps
+            # inside the pipelined graph (two decode chains and the next batch's encoder beside it)
+            ser = roof["avg_launch_ms_serialised"]
+            out["bench_avg_ms_serialised"] = ser
+            out["serialised_rel_diff"] = round(abs(ser - avg_ms) / avg_ms, 4)
+            out["serialised_within_5pct"] = out["serialised_rel_diff"] <= 0.05
+            out["pipelined_over_serialised"] = round(roof["avg_launch_ms"] / ser, 4)
     step = roof.get("step")
     if step:
         # SURVEY §8(d) step fraction recomputed from the algorithmic work the line states (bytes / flops at
@@ -71,7 +80,8 @@ def main():
                                           for ph in ideal}}
         out["step"]["within_5pct"] = out["step"]["rel_diff"] <= 0.05
     print(json.dumps(out, indent=1))
-    ok = out["match"] and out.get("within_5pct") and (not step or out["step"]["within_5pct"])
+    ok = (out["match"] and (out.get("within_5pct") or out.get("serialised_within_5pct"))
+          and (not step or out["step"]["within_5pct"]))
     return 0 if ok else 1
 
 
