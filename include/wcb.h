@@ -86,6 +86,12 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "xenc_fm" 0/1      greedy encoder-space cross-attention reads the encoder output in the fragment-major chunk
  *                      layout (1, default; 1 KiB contiguous per load wave-instruction) or the row layout (0)
  *   "ring_kt" 1/2      decode rows > 64: 64-deep K sub-tiles per LDS-ring stage of the projection tiles
+ *   "beam_wide" 0/1    decode rows 65-96 (C5's beam rows): out / xo / xq / fc1 on the wide single-burst tiles
+ *                      with fragment-major weights (1, default) or the LDS-ring tiles (0); before finalize
+ *   "beam_wfm" 0/1     decode rows > 64: the LDS-ring tiles read fragment-major weight copies (0, default);
+ *                      before finalize
+ *   "beam_raster" n    decode rows > 64: ring tile order in bands of n row panels, column tiles outer (0, default:
+ *                      row panels outer)
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)
  *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave), 4 (64 queries, default)
  *   "enc_raster" n     encoder GEMM tile order: bands of n row panels, column tiles outer (8, default;
@@ -243,7 +249,11 @@ int wcb_op_gemm(int dtype, const void* A, const void* W, int M, int N, int K, co
  * and is the faster one (16-bit, N % 256 == 0, K % 64 == 0, K >= 128, M >= 256; the LDS-ring kernel's
  * 256x192 tiles where those leave fewer tile rounds), 4 = the same with the ping-pong kernel's own 192-wide
  * tiles there (option "enc_gemm"), 2 / 5 = the ping-pong kernel's 256- / 192-wide tiles for every shape they
- * cover (residual epilogue included), 0 = the LDS-ring / tile kernels */
+ * cover (residual epilogue included), 0 = the LDS-ring / tile kernels; decode-row (beam) tiles, 16-bit,
+ * M > 64: 6 = the LDS-ring tiles, 10·FM + FN (11, 12, 21, 22, 41, 42, 51, 52) = the wide single-burst
+ * tiles of 16·FM rows x 16·FN columns (K = 768, 1024 or 1280; resid, when given, must equal out; a shape
+ * the wide tiles do not cover runs on the ring tiles), 100 + that: W given fragment-major
+ * ([N / 16][K / 32][64 lanes][8]: element (n, k) at lane 16·((k % 32) / 8) + n % 16, slot k % 8) */
 int wcb_op_gemm_kernel(int dtype, const void* A, const void* W, int M, int N, int K, const float* bias, int act,
                        const float* resid, void* out, int out_f32, int kernel, void* stream);
 /* decode-step fused form: out[M][N] = act(LN(X) · W[N][K]ᵀ + bias), X f32 [M][K] (M <= 64), with the

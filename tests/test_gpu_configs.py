@@ -42,11 +42,11 @@ def weights(size, seed, recipe):
     return _W[key]
 
 
-def model(size, seed, recipe, dtype):
-    key = (size, seed, recipe, dtype)
+def model(size, seed, recipe, dtype, opts=None):
+    key = (size, seed, recipe, dtype, tuple(sorted((opts or {}).items())))
     if key not in _M:
         sd = weights(size, seed, recipe)
-        _M[key] = WhisperCB.from_state_dict(get_dims(size), sd, dtype=dtype)
+        _M[key] = WhisperCB.from_state_dict(get_dims(size), sd, dtype=dtype, options=opts)
     return _M[key]
 
 
@@ -143,7 +143,7 @@ def check_16bit_beam5(size, dtype):
     assert b.shape == g["beam5_ids"].shape and np.array_equal(b, g["beam5_ids"]), (b, g["beam5_ids"])
 
 
-def check_beam5_boost(size, dtype, n_phr, B, B_ref, tail=2, max_length=8, min_new=0):
+def check_beam5_boost(size, dtype, n_phr, B, B_ref, tail=2, max_length=8, min_new=0, opts=None):
     """Beam 5 with the n_phr-phrase boost (lambda 2) at the benchmarked batch: B clips = 5·B decoder rows
     in one call (C3: 64 clips = 320 rows on the ring-tile projections and the grouped flash
     cross-attention; C5: 16 clips = 80 rows). The first B_ref clips must equal the oracle's beam search
@@ -152,7 +152,7 @@ def check_beam5_boost(size, dtype, n_phr, B, B_ref, tail=2, max_length=8, min_ne
     the decode-GEMM path) — batch composition does not change a clip's beams. `min_new` masks EOS for that
     many tokens (the benchmark mode: every beam runs the full length, key map and self-KV cache included)."""
     dims = get_dims(size)
-    m = model(size, 1, "margin", dtype)
+    m = model(size, 1, "margin", dtype, opts)
     phrases = synth_bias_list(n_phr, eot=dims.eos_token_id)
     x = mel_of(dims, B)
     kw = dict(max_length=max_length, min_new_tokens=min_new, num_beams=5, bias_list=phrases, bias_boost=2.0)
@@ -272,6 +272,13 @@ def test_c3_medium_bf16_64clips_beam5_1000_phrase_boost():
     check_beam5_boost("medium", "bf16", 1000, 64, 2)
 
 
+@pytest.mark.parametrize("opts", [{"beam_wfm": 1}, {"beam_raster": 8}], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
+def test_c3_ring_tile_options_match_reference(opts):
+    """The 320-row ring-tile formulations (fragment-major weights, column-outer tile order) at C3's shape:
+    clips 0-1 identical to the oracle's boosted beam search, clips 62-63 to a 2-clip call."""
+    check_beam5_boost("medium", "bf16", 1000, 64, 2, opts=opts)
+
+
 def test_c3_beam5_at_the_benchmarked_length():
     """C3 as bench.py times it: 64 clips x beam 5, bf16, 1000 phrases, 64 new tokens
     with EOS masked — the key-map reorder and the self-KV cache well past the 16 positions the reference
@@ -295,6 +302,21 @@ def test_c5_large_v3_f16_16clips_beam5_5000_phrase_boost():
     rows, fp16 with the encoder clamp, 5000 phrases (lambda 2), high-margin recipe: clip 0 identical
     to the oracle, clips 14-15 identical to a 2-clip call."""
     check_beam5_boost("large-v3", "f16", 5000, 16, 1)
+
+
+def test_c5_beam_wide_tiles_match_reference():
+    """Option beam_wide: C5's 80 beam rows with out / xo / xq / fc1 on the wide single-burst tiles
+    (gemm_wide_kernel, fragment-major folded weights): clip 0 identical to the oracle's beam search with the
+    5000-phrase boost, clips 14-15 identical to a 2-clip call; and the bench's 64 tokens (EOS masked) for
+    all 16 clips identical to the ring-tile decode (high-margin recipe)."""
+    check_beam5_boost("large-v3", "f16", 5000, 16, 1, opts={"beam_wide": 1})   # (the default)
+    dims = get_dims("large-v3")
+    phrases = synth_bias_list(5000, eot=dims.eos_token_id)
+    x = mel_of(dims, 16)
+    kw = dict(max_length=64, min_new_tokens=64, num_beams=5, bias_list=phrases, bias_boost=2.0)
+    wide = model("large-v3", 1, "margin", "f16", {"beam_wide": 1}).generate(x, **kw).cpu().numpy()
+    ring = model("large-v3", 1, "margin", "f16", {"beam_wide": 0}).generate(x, **kw).cpu().numpy()
+    assert np.array_equal(wide, ring), np.argwhere(wide != ring)[:8]
 
 
 def test_c5_timed_path_pcm_to_beams():
@@ -430,7 +452,8 @@ def test_encoder_tile_raster_bit_identical(raster):
 # recipe: greedy and beam-5 ids exact in bf16, as the defaults are in check_16bit_greedy / _beam5)
 ALT_OPTIONS = [{"merge_v": 0}, {"enc_gemm": 1}, {"enc_gemm": 0}, {"xenc_split": 4}, {"xenc_split": 12}, {"xenc_variant": 0}, {"xenc_variant": 2},
                {"xenc_variant": 3}, {"decode_contexts": 1}, {"enc_flash": 2}, {"flash_split": 1},
-               {"beam_xattn": 1}, {"beam_xattn": 2}, {"ring_kt": 1}, {"lean": 0, "lean_x": 0}]
+               {"beam_xattn": 1}, {"beam_xattn": 2}, {"ring_kt": 1}, {"lean": 0, "lean_x": 0}, {"beam_wide": 0},
+               {"beam_wfm": 1}, {"beam_raster": 8}]
 
 
 @pytest.mark.parametrize("opts", ALT_OPTIONS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))

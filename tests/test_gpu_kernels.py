@@ -356,6 +356,53 @@ def test_gemm_pingpong_kernel(dt, M, N, K, act, resid, bias, f32, kernel):
     assert err0 < 2e-4, err0
 
 
+def _frag_major(W):
+    """[N][K] → [N / 16][K / 32][64 lanes][8]: element (n, k) at lane 16·((k % 32) / 8) + n % 16, slot k % 8."""
+    N, K = W.shape
+    return W.view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N, K)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("M,N,K,act,resid", [
+    (80, 1280, 1280, 0, True), (80, 5120, 1280, 1, False), (80, 3840, 1280, 0, False),   # C5's beam rows
+    (320, 1024, 1024, 0, True), (320, 4096, 1024, 1, False), (70, 768, 768, 0, False),   # C3's, ragged rows
+    (97, 512, 1024, 1, False)])
+@pytest.mark.parametrize("kernel", [6, 7, 106, 107, 12, 22, 42, 51, 112, 122, 152])
+def test_gemm_decode_row_tiles(dt, M, N, K, act, resid, kernel):
+    """Beam-row projections (decode rows > 64) through wcb_op_gemm_kernel: the LDS-ring tiles (kernel 6) and
+    the wide single-burst tiles (gemm_wide_kernel, 10·FM + FN; + 100: fragment-major W) vs fp64, bias, GELU
+    and the in-place residual epilogue, ragged row tiles, deterministic."""
+    lib = _lib.load()
+    if kernel % 100 > 10 and N % (16 * (kernel % 10)):
+        pytest.skip("N not a multiple of the tile width")
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + kernel)
+    A = torch.randn(M, K, generator=g).to(DT[dt][0]).cuda()
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(DT[dt][0]).cuda()
+    Wk = _frag_major(W) if kernel >= 100 else W
+    b = torch.randn(N, generator=g).float().cuda()
+    R = torch.randn(M, N, generator=g).float().cuda() if resid else None
+
+    def run():
+        out = torch.full((M, N), float("nan"), device="cuda", dtype=torch.float32 if resid else A.dtype)
+        if resid:
+            out.copy_(R)
+        _lib.check(lib.wcb_op_gemm_kernel(DT[dt][1], A.data_ptr(), Wk.data_ptr(), M, N, K, b.data_ptr(), act,
+                                          out.data_ptr() if resid else None, out.data_ptr(), int(resid), kernel,
+                                          _s()), None, "gemm")
+        torch.cuda.synchronize()
+        return out
+    out = run()
+    ref = A.double() @ W.double().T + b.double()
+    if act:
+        ref = torch.nn.functional.gelu(ref)
+    if resid:
+        ref = ref + R.double()
+    tol = 1e-4 if resid else (8e-3 if dt == "bf16" else 1e-3)
+    err = ((out.double() - ref).abs() - tol * ref.abs()).max().item()
+    assert err < 2e-4, err
+    assert torch.equal(run(), out)
+
+
 @pytest.mark.parametrize("dt", ["bf16", "f32"])
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("Sk,split", [(1500, 1), (1500, 4), (37, 1), (1, 3), (64, 1), (65, 1), (200, 1)])

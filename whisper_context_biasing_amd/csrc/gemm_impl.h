@@ -283,8 +283,11 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(GemmArgs g) {
 // BKB: bytes of K per LDS row of a sub-tile: 128 (64-deep) or 64 (32-deep: half the stage bytes, so
 // twice the stages in the same LDS — the encoder's 256x256 tiles keep 3 stages in flight across the
 // barrier instead of 1). The MFMA sequence over K is the same: bit-identical outputs.
+// WFM (decode rows, BKB 128): W given fragment-major (g.W_fm: [N / 16][K / 32][64 lanes][8]); each lane's
+// 16-byte piece is gathered from there into the same swizzled LDS row layout (a wave-instruction's 8 rows
+// x 64 k then read 2 KiB of contiguous weights instead of 8 rows at the K-row stride).
 template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1, int BKB = 128,
-          int PRIO = 0>
+          int PRIO = 0, bool WFM = false>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
   constexpr int NW = WM * WN, NT = NW * 64;
   static_assert(BKB == 128 || BKB == 64, "LDS row: 128 or 64 bytes");
@@ -326,12 +329,19 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
     const int m = min(m0 + r, g.M - 1);
     a_src[i] = A + a_row(g, m) + ((lane % CPR) ^ swz(r)) * CE;
   }
+  static_assert(!WFM || BKB == 128, "fragment-major W: 64-deep sub-tiles");
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
     const int r = (wave + i * NW) * RPI + lane / CPR;
     const long n = min(n0 + r, g.N - 1);
-    b_src[i] = W + n * g.ldw + ((lane % CPR) ^ swz(r)) * CE;
+    const int c = (lane % CPR) ^ swz(r);   // chunk (8 k) of the 64-deep sub-tile
+    if constexpr (WFM)   // k-step c / 4 of the sub-tile, lane 16·(c % 4) + n % 16 of that k-step's fragment
+      b_src[i] = reinterpret_cast<const T*>(g.W_fm) + ((n / 16) * (g.K / 32) + c / 4) * 512 + (16 * (c % 4) + n % 16) * 8;
+    else
+      b_src[i] = W + n * g.ldw + c * CE;
   }
+  // (fragment-major W: k advances 512 elements per 32-deep k-step, i.e. 16 per element of k)
+  constexpr int WKS = WFM ? 16 : 1;
   auto stage = [&](int st, int k0) {
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
@@ -339,7 +349,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < IA; ++i) glds16(a_src[i] + k0 + t * BK, base + (wave + i * NW) * 1024);
 #pragma unroll
-      for (int i = 0; i < IB; ++i) glds16(b_src[i] + k0 + t * BK, base + BM * BKB + (wave + i * NW) * 1024);
+      for (int i = 0; i < IB; ++i) glds16(b_src[i] + (long)(k0 + t * BK) * WKS, base + BM * BKB + (wave + i * NW) * 1024);
     }
   };
 
@@ -509,7 +519,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_ring_kernel(GemmArgs g) {
 }
 
 template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool LNF = false, int KT = 1, int BKB = 128,
-          int PRIO = 0>
+          int PRIO = 0, bool WFM = false>
 static void launch_ring_e(const GemmArgs& g, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
   constexpr int ring_bytes = NS * (BM + BN) * BKB * KT;
@@ -520,11 +530,18 @@ static void launch_ring_e(const GemmArgs& g, hipStream_t s) {
   static_assert(lds <= 160 * 1024, "LDS budget");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT, BKB, PRIO>,
+    (void)hipFuncSetAttribute((const void*)gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT, BKB, PRIO, WFM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
-  WCB_LAUNCH((gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT, BKB, PRIO>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
+  WCB_LAUNCH((gemm_ring_kernel<T, BM, BN, WM, WN, NS, EPI, LNF, KT, BKB, PRIO, WFM>), dim3(tiles), dim3(WM * WN * 64), lds, s, g);
+}
+
+// decode-row ring tiles: the weights fragment-major where the runtime hands a copy over (g.W_fm)
+template <typename T, int BM, int BN, int NS, bool LNF, int KT = 1>
+static void launch_ring_dec(const GemmArgs& g, hipStream_t s) {
+  if (g.W_fm && g.K % 32 == 0) launch_ring_e<T, BM, BN, 2, 2, NS, E_RUNTIME, LNF, KT, 128, 0, true>(g, s);
+  else launch_ring_e<T, BM, BN, 2, 2, NS, E_RUNTIME, LNF, KT>(g, s);
 }
 
 // PRIO 1: s_setprio(1) around each MFMA cluster (keeps hipcc from moving the MFMAs across the
@@ -1765,6 +1782,230 @@ static bool launch_lean(const GemmArgs& g, hipStream_t s) {
   }
 }
 
+// Beam-row projections (decode rows > 64: C3's 320 / C5's 80 beam rows), K = d_model: gemm_wide_kernel.
+// One BM x BN tile per workgroup (BM = 16·FM rows, BN = 16·FN columns), K split over the NW waves; each
+// wave issues every operand load of the launch in one burst straight into registers (FM + FN fragments
+// per 32-deep k-step, KPW k-steps; the folded-LayerNorm statistics, bias, u, residual and cache position
+// with them), multiplies, and the wave partials meet in LDS in wave order. The LDS-ring tiles
+// (gemm_ring_kernel, tile 2) keep NS - 1 K tiles in flight and pay a memory round trip per ring turn at
+// 2-8 MFMAs per wave per tile; here the workgroup's whole K extent is in flight at once.
+// Epilogue (the ring kernel's run-time forms): folded LayerNorm r·(acc − μ·u[n]) (LNF), + bias, GELU;
+// the QKV launch's k / v columns → the self-attention cache at the device-side position; residual
+// writers x += …, the 16-bit copy and the per-32-column (Σx, Σx²) partials for the next fold.
+template <typename T> struct WideArgs {
+  const T* A; const T* W; const float* bias; const float* ln_u; const float* rst_in;
+  const float* resid; void* out; T* out16; T* kv; const int* pos; float* rst_out;
+  int M, N, lda, ldw, ldc;
+  int act, out_f32, mode, n_split, kvB, kvH, kvT;
+};
+
+template <typename T, int FM, int FN, int NW, int KPW, bool LNF, bool WFM = false>
+__global__ __launch_bounds__(NW * 64) void gemm_wide_kernel(WideArgs<T> p) {
+  using Frag = typename DT<T>::frag;
+  constexpr int NT = NW * 64, BM = FM * 16, BN = FN * 16, K = NW * KPW * 32, C8 = BN / 8, LDC = BN + 4;
+  static_assert(BM * C8 <= NT, "epilogue: one 8-column item per thread");
+  constexpr int RNB = K / 32;                                   // LN statistics partials per row
+  constexpr int LPR = NT / BM >= 8 ? 8 : NT / BM >= 4 ? 4 : NT / BM >= 2 ? 2 : 1;   // lanes per row
+  constexpr int RPL = (RNB + LPR - 1) / LPR;
+  __shared__ __attribute__((aligned(16))) float red[NW][BM][LDC];
+  __shared__ float2 lnst[LNF ? BM : 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // column tile outer, row tile inner over consecutive workgroups of an XCD (the row tiles of a column
+  // tile share its weights in that XCD's L2)
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (wg % tiles_m) * BM, n0 = (wg / tiles_m) * BN;
+  const int kb = wave * (KPW * 32) + 8 * (lane >> 4);
+  // ---------------- the launch's loads, one burst
+  Frag w[FN][KPW], a[FM][KPW];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    if constexpr (WFM) {   // fragment-major weights [N / 16][K / 32][lane][8]: 1 KiB per wave-instruction
+      const T* wr = p.W + (((long)min(n0 / 16 + j, p.N / 16 - 1) * (K / 32) + wave * KPW) * 64 + lane) * 8;
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) w[j][ks] = load_frag<T>(wr + ks * 512);
+    } else {
+      const T* wr = p.W + (long)min(n0 + j * 16 + (lane & 15), p.N - 1) * p.ldw + kb;
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) w[j][ks] = load_frag<T>(wr + ks * 32);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const T* ar = p.A + (long)min(m0 + i * 16 + (lane & 15), p.M - 1) * p.lda + kb;
+#pragma unroll
+    for (int ks = 0; ks < KPW; ++ks) a[i][ks] = load_frag<T>(ar + ks * 32);
+  }
+  // epilogue operands: thread → row er, columns ec .. ec + 7
+  const int er = tid / C8, ec = n0 + (tid % C8) * 8;
+  const bool item = er < BM;
+  const int erow = min(m0 + min(er, BM - 1), p.M - 1);
+  const int ecc = min(ec, p.N - 8);
+  float b8[8], u8[8], r8[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { b8[e] = 0.f; u8[e] = 0.f; r8[e] = 0.f; }
+  if (p.bias) {
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(p.bias + ecc), hi = *reinterpret_cast<const f32x4*>(p.bias + ecc + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { b8[e] = lo[e]; b8[e + 4] = hi[e]; }
+  }
+  if constexpr (LNF) {
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(p.ln_u + ecc), hi = *reinterpret_cast<const f32x4*>(p.ln_u + ecc + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { u8[e] = lo[e]; u8[e + 4] = hi[e]; }
+  }
+  if (p.resid) {
+    const float* rr = p.resid + (long)erow * p.ldc + ecc;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(rr), hi = *reinterpret_cast<const f32x4*>(rr + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { r8[e] = lo[e]; r8[e + 4] = hi[e]; }
+  }
+  int pos = 0;
+  if (p.mode == 2) pos = *p.pos;
+  // LNF: row sr's statistics partials, lane ss of its LPR takes partials ss, ss + LPR, ...
+  const int sr = tid / LPR, ss = tid % LPR;
+  float2 st[LNF ? RPL : 1];
+  if constexpr (LNF) {
+    const float* sp = p.rst_in + (long)min(m0 + min(sr, BM - 1), p.M - 1) * RNB * 2;
+#pragma unroll
+    for (int t = 0; t < RPL; ++t) {
+      const int j = min(ss + t * LPR, RNB - 1);
+      st[t] = *reinterpret_cast<const float2*>(sp + 2 * j);
+    }
+  }
+  // ---------------- MFMA over this wave's K slice, partial tiles into LDS
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) acc = mma16(a[i][ks], w[j][ks], acc);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[wave][i * 16 + (lane >> 4) * 4 + e][j * 16 + (lane & 15)] = acc[e];
+    }
+  if constexpr (LNF) {   // (μ, r) per tile row: strided partial sums in column order, then a fixed butterfly
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < RPL; ++t)
+      if (ss + t * LPR < RNB) { s1 += st[t].x; s2 += st[t].y; }
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+    if (ss == 0 && sr < BM) {
+      const float mean = s1 / K;
+      lnst[sr] = float2{mean, rsqrtf(fmaxf(s2 / K - mean * mean, 0.f) + 1e-5f)};
+    }
+  }
+  __syncthreads();
+  // ---------------- epilogue: one row × 8 columns per thread, wave partials summed in wave order
+  const int m = m0 + er;
+  const bool ok = item && m < p.M && ec < p.N;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = 0.f;
+  if (item) {
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(&red[q][er][(tid % C8) * 8]);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(&red[q][er][(tid % C8) * 8 + 4]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[e] += lo[e]; v[e + 4] += hi[e]; }
+    }
+    float2 ls = float2{0.f, 1.f};
+    if constexpr (LNF) ls = lnst[er];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if constexpr (LNF) v[e] = ls.y * (v[e] - ls.x * u8[e]);
+      v[e] += b8[e];
+      if (p.act == 1) v[e] = gelu_t<T>(v[e]);
+    }
+  }
+  if (p.mode == 2 && ec >= p.n_split) {   // k / v of the new token → the self-attention cache
+    if (ok) {
+      const int n2 = ec - p.n_split, hh = n2 >> 6, dd = n2 & 63;
+      const int kvs = hh / p.kvH, hd = hh % p.kvH;
+      store8<T>(p.kv + ((((long)kvs * p.kvB + m) * p.kvH + hd) * p.kvT + pos) * 64 + dd, v);
+    }
+    return;
+  }
+  const long off = (long)m * p.ldc + ec;
+  if (p.resid) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += r8[e];
+  }
+  if (ok) {
+    if (p.out_f32) store8<float>(reinterpret_cast<float*>(p.out) + off, v);
+    else store8<T>(reinterpret_cast<T*>(p.out) + off, v);
+    if (p.out16) store8<T>(p.out16 + off, v);
+  }
+  if constexpr (C8 % 4 == 0) {
+    if (p.rst_out) {   // residual writer: (Σx, Σx²) of the new row per 32 columns (4 adjacent lanes)
+      float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { a1 += v[e]; a2 = fmaf(v[e], v[e], a2); }
+      a1 += __shfl_xor(a1, 1, 64); a2 += __shfl_xor(a2, 1, 64);
+      a1 += __shfl_xor(a1, 2, 64); a2 += __shfl_xor(a2, 2, 64);
+      if (ok && (tid & 3) == 0) *reinterpret_cast<float2*>(p.rst_out + ((long)m * (p.N / 32) + ec / 32) * 2) = float2{a1, a2};
+    }
+  }
+}
+
+template <typename T, int FM, int FN, int NW, int KPW>
+static void launch_wide_k(const GemmArgs& g, hipStream_t s) {
+  WideArgs<T> p;
+  p.A = reinterpret_cast<const T*>(g.A); p.W = reinterpret_cast<const T*>(g.W);
+  p.bias = g.bias; p.ln_u = g.ln_u; p.rst_in = g.rst_in;
+  p.resid = g.resid; p.out = g.out; p.out16 = reinterpret_cast<T*>(g.out16);
+  p.kv = reinterpret_cast<T*>(g.kv_out); p.pos = g.pos; p.rst_out = g.rst_out;
+  p.M = g.M; p.N = g.N; p.lda = (int)g.lda; p.ldw = (int)g.ldw; p.ldc = (int)g.ldc;
+  p.act = g.act; p.out_f32 = g.out_f32; p.mode = g.mode; p.n_split = g.n_split;
+  p.kvB = g.hs_B; p.kvH = g.hs_H; p.kvT = g.kv_T;
+  const int tiles = ((g.M + FM * 16 - 1) / (FM * 16)) * (g.N / (FN * 16));
+  if (g.W_fm) {
+    p.W = reinterpret_cast<const T*>(g.W_fm);
+    if (g.ln_u) WCB_LAUNCH((gemm_wide_kernel<T, FM, FN, NW, KPW, true, true>), dim3(tiles), dim3(NW * 64), 0, s, p);
+    else WCB_LAUNCH((gemm_wide_kernel<T, FM, FN, NW, KPW, false, true>), dim3(tiles), dim3(NW * 64), 0, s, p);
+    return;
+  }
+  if (g.ln_u) WCB_LAUNCH((gemm_wide_kernel<T, FM, FN, NW, KPW, true>), dim3(tiles), dim3(NW * 64), 0, s, p);
+  else WCB_LAUNCH((gemm_wide_kernel<T, FM, FN, NW, KPW, false>), dim3(tiles), dim3(NW * 64), 0, s, p);
+}
+
+// cfg = 10·FM + FN (FM 1..5, FN 1..2); false: the shape / epilogue is not covered (the caller keeps the
+// ring tiles). K = d_model (NW waves × KPW 32-deep k-steps).
+template <typename T>
+static bool launch_wide(const GemmArgs& g, int cfg, hipStream_t s) {
+  if constexpr (sizeof(T) != 2) {
+    return false;
+  } else {
+    const int FMr = cfg / 10, FNr = cfg % 10;
+    if (FMr < 1 || FMr > 5 || FNr < 1 || FNr > 2) return false;
+    if (g.a_Mb || g.c_Mb || g.addrow || g.st_out || g.mode == 1 || g.clamp != 0.f || g.a_grp_n) return false;
+    if (g.N % (16 * FNr) || g.ldc % 8 || g.lda % 8 || g.ldw % 8) return false;
+    if (g.ln_u && (!g.rst_in || g.rst_nb * 32 != g.K)) return false;
+    if (g.rst_out && (FNr < 2 || g.N % 32)) return false;
+    if (g.mode == 2 && (g.kv_rps > 1 || !g.kv_out || !g.pos || g.n_split % 64 || g.out_f32 || g.resid)) return false;
+    if (g.resid && g.resid != g.out) return false;
+#define WCB_WD(k, nw, kpw)                                                              \
+  if (g.K == k) {                                                                       \
+    switch (cfg) {                                                                      \
+      case 11: launch_wide_k<T, 1, 1, nw, kpw>(g, s); return true;                      \
+      case 12: launch_wide_k<T, 1, 2, nw, kpw>(g, s); return true;                      \
+      case 21: launch_wide_k<T, 2, 1, nw, kpw>(g, s); return true;                      \
+      case 22: launch_wide_k<T, 2, 2, nw, kpw>(g, s); return true;                      \
+      case 41: launch_wide_k<T, 4, 1, nw, kpw>(g, s); return true;                      \
+      case 42: launch_wide_k<T, 4, 2, nw, kpw>(g, s); return true;                      \
+      case 51: launch_wide_k<T, 5, 1, nw, kpw>(g, s); return true;                      \
+      case 52: launch_wide_k<T, 5, 2, nw, kpw>(g, s); return true;                      \
+      default: return false;                                                            \
+    }                                                                                   \
+  }
+    WCB_WD(768, 8, 3) WCB_WD(1024, 8, 4) WCB_WD(1280, 8, 5)
+#undef WCB_WD
+    return false;
+  }
+}
+
 // The LayerNorm of gemm_dec_kernel AM = 2 (the same K split over NW waves × KPW k-steps, sum order
 // and normalisation) for 16-row blocks, written as 16-bit rows: the LM head's A operand.
 template <typename T, int NW, int KPW>
@@ -1949,6 +2190,7 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
       // tile 2 (192+ rows, the d-wide and wide projections): 64-row tiles over a deep LDS-DMA ring, so
       // that even N = d_model spreads over 80-320 workgroups (C3: 320 rows = 5 row tiles); 64 columns
       // where that still fills the chip, else 32. Run-time epilogue (KV append, 16-bit residual copy).
+      if (g.tile == 2 && g.wide && launch_wide<T>(g, g.wide, s)) return;
       if (g.tile == 2 && g.K % 64 == 0 && !g.st_out && g.mode != 1 && !g.addrow &&
           (!g.ln_u || (g.K <= kLnfMaxK && g.rst_in && g.rst_nb * 32 == g.K))) {
         const int mt = (g.M + 63) / 64;
@@ -1956,18 +2198,18 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
         const bool kt2 = g.ring_kt == 2 && g.K % 128 == 0;           // 128-deep stages
         if (g.N % 64 == 0 && mt * (g.N / 64) >= 240) {
           // (128-deep stages measured slower here: C3 4,871 vs 4,946 audio-s/s with all three tiles)
-          if (lnf) launch_ring_e<T, 64, 64, 2, 2, 4, E_RUNTIME, true>(g, s);
-          else launch_ring_e<T, 64, 64, 2, 2, 4, E_RUNTIME>(g, s);
+          if (lnf) launch_ring_dec<T, 64, 64, 4, true>(g, s);
+          else launch_ring_dec<T, 64, 64, 4, false>(g, s);
         } else if (mt * ((g.N + 31) / 32) >= 240) {
-          if (lnf && kt2) launch_ring_e<T, 64, 32, 2, 2, 4, E_RUNTIME, true, 2>(g, s);
-          else if (lnf) launch_ring_e<T, 64, 32, 2, 2, 6, E_RUNTIME, true>(g, s);
-          else if (kt2) launch_ring_e<T, 64, 32, 2, 2, 4, E_RUNTIME, false, 2>(g, s);
-          else launch_ring_e<T, 64, 32, 2, 2, 6, E_RUNTIME>(g, s);
+          if (lnf && kt2) launch_ring_dec<T, 64, 32, 4, true, 2>(g, s);
+          else if (lnf) launch_ring_dec<T, 64, 32, 6, true>(g, s);
+          else if (kt2) launch_ring_dec<T, 64, 32, 4, false, 2>(g, s);
+          else launch_ring_dec<T, 64, 32, 6, false>(g, s);
         } else {
-          if (lnf && kt2) launch_ring_e<T, 32, 32, 2, 2, 4, E_RUNTIME, true, 2>(g, s);
-          else if (lnf) launch_ring_e<T, 32, 32, 2, 2, 6, E_RUNTIME, true>(g, s);
-          else if (kt2) launch_ring_e<T, 32, 32, 2, 2, 4, E_RUNTIME, false, 2>(g, s);
-          else launch_ring_e<T, 32, 32, 2, 2, 6, E_RUNTIME>(g, s);
+          if (lnf && kt2) launch_ring_dec<T, 32, 32, 4, true, 2>(g, s);
+          else if (lnf) launch_ring_dec<T, 32, 32, 6, true>(g, s);
+          else if (kt2) launch_ring_dec<T, 32, 32, 4, false, 2>(g, s);
+          else launch_ring_dec<T, 32, 32, 6, false>(g, s);
         }
         return;
       }

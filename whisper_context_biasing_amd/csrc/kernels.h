@@ -71,6 +71,7 @@ struct GemmArgs {
   int a_grp_n = 0; long a_grp_off = 0;
   int skinny = 0;                  // decode projection: the skinny kernel whatever M (row blocks over grid.y)
   int ring_kt = 1;                 // tile 2: 64-deep K sub-tiles per LDS-ring stage (1 or 2)
+  int wide = 0;                    // tile 2, K = d_model: gemm_wide_kernel tile config 10·FM + FN (0: ring tiles)
   // decode GEMM (gemm_dec_kernel): a T-typed copy of the f32 rows the epilogue writes (the
   // residual stream x → x16, read back as the LN-fused A operand of the next projection), and the
   // LN-fused A read from such a copy instead of the f32 rows (lda elements per row)
@@ -82,6 +83,7 @@ struct GemmArgs {
   const float* ln_u = nullptr;
   const float* ln_c = nullptr;     // Σ_k β_k W[n][k] + bias[n] (becomes `bias` when the fold is taken)
   const void* ln_wg = nullptr;     // W' = W·diag(γ) in the model dtype (becomes `W` when the fold is taken)
+  const void* ln_wg_fm = nullptr;  // W' fragment-major (the wide beam-row tiles; becomes `W_fm` with the fold)
   const float* rst_in = nullptr; int rst_nb = 0;
   float* rst_out = nullptr;        // ring-tile residual writers: [M][N / 32] float2 partials of the written f32 rows
   // f16 encoder layers: the layer output is clamped to ±(finfo(f16).max − 1000)

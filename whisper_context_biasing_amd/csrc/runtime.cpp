@@ -97,6 +97,7 @@ struct LayerW {
   void *qkv_fm = nullptr, *o_fm = nullptr, *xq_fm = nullptr, *xkt_fm = nullptr, *xo_fm = nullptr, *fc1_fm = nullptr,
        *fc2_fm = nullptr;
   void* xv_fm = nullptr;   // W_v for the greedy range merge (xenc_merge_v_kernel's A-fragment order)
+  void *qkv_wgfm = nullptr, *xq_wgfm = nullptr, *fc1_wgfm = nullptr;   // folded weights fragment-major (beam_wide / beam_wfm)
 };
 
 struct ProfEntry {
@@ -205,6 +206,18 @@ struct wcb_handle {
   // decode rows > 64: 64-deep K sub-tiles per ring stage of the 64x32 / 32x32 tiles (option "ring_kt",
   // 1 or 2; C5 1,594 -> 1,644 audio-s/s)
   int ring_kt = 2;
+  // decode rows 65-96 (C5's 80 beam rows), K = d_model: out / xo / xq / fc1 on the wide single-burst tiles
+  // (gemm_impl.h gemm_wide_kernel) instead of the ring tiles (option "beam_wide", set before finalize).
+  // tools/beam_gemm_bench.py (80 rows, d = 1280, cold weights): out 6.3 -> 5.3 µs (16 x 32 tiles,
+  // fragment-major W), fc1 13.5 -> 9.8 µs (32 x 32); QKV stays on the ring (7.5 vs 9.4); at C3's 320 rows
+  // the ring tiles win every shape. C5 bench 2,478 / 2,485 vs 2,446 / 2,429 audio-s/s (interleaved)
+  int beam_wide = 1;
+  // decode rows > 64, ring tiles: the weights read from fragment-major copies (option "beam_wfm", set
+  // before finalize: the folded QKV / xq / fc1 weights get such copies too) and the tile order (option
+  // "beam_raster": bands of n row panels with the column tiles outer, so the row tiles sharing a weight
+  // tile run on one XCD; 0 = row panels outer)
+  int beam_wfm = 0;
+  int beam_raster = 0;
   // greedy LM head: the final LayerNorm in a launch of its own (option "lm_ln_split" 1) or inside the
   // column walk (0, default: with the f32 copies of the A rows no longer held across the statistics
   // barrier the fused walker is 22.46 vs 22.19 µs + the LayerNorm launch, tools/dec_kernel_bench.hip)
@@ -654,6 +667,16 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       // the folded W·diag(γ) copies are built at finalize only when it is on
       REQUIRE(!h->ready, "option ln_fold selects weight layouts: set it before wcb_finalize_weights");
       h->ln_fold = value != 0;
+    } else if (n == "beam_wfm") {
+      REQUIRE(!h->ready, "option beam_wfm selects weight layouts: set it before wcb_finalize_weights");
+      h->beam_wfm = value != 0;
+    } else if (n == "beam_raster") {
+      REQUIRE(value >= 0 && value <= 64, "option beam_raster: 0..64");
+      h->beam_raster = value;
+    } else if (n == "beam_wide") {
+      // the wide tiles read fragment-major copies of the folded xq / fc1 weights, built at finalize
+      REQUIRE(!h->ready, "option beam_wide selects weight layouts: set it before wcb_finalize_weights");
+      h->beam_wide = value != 0;
     } else if (n == "beam_xattn") {
       REQUIRE(value >= 0 && value <= 3, "option beam_xattn: 0..3");
       h->beam_xattn = value;
@@ -851,6 +874,11 @@ int wcb_finalize_weights(wcb_handle* h) {
         lw.fc1_fm = fm(lw.fc1_w, F, d);
         lw.fc2_fm = fm(lw.fc2_w, d, F);
         if (lw.xkt_w) lw.xkt_fm = fm(lw.xkt_w, H * d, 64);
+        if ((h->beam_wide || h->beam_wfm) && h->ln_fold) {   // beam-row tiles: the folded weights fragment-major
+          lw.xq_wgfm = fm(lw.xq_wg, d, d);
+          lw.fc1_wgfm = fm(lw.fc1_wg, F, d);
+          if (h->beam_wfm) lw.qkv_wgfm = fm(lw.qkv_wg, 3 * d, d);
+        }
         if (lw.xv_w && h->lean && h->dt != kF32 && d % 128 == 0 && d <= 1024) {   // 16 output rows per wave, all of K per wave
           lw.xv_fm = h->own((size_t)d * d * e);
           frag_major(h->dt, lw.xv_w, d, d, 1, d / 32, lw.xv_fm, st);
@@ -1228,10 +1256,11 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     const bool ring = h->dt != kF32 && !lm && !g.st_out;
     if (tiled && !g.a_grp_n && (lm || ring || (M >= 192 && g.N >= 2048))) {
       if (g.ln_w && ring && g.ln_u && g.ln_wg && lnf_ok && lna) {   // LayerNorm folded into the ring tiles
-        g.A = lna; g.lda = d; g.W = g.ln_wg; g.ldw = g.K;
+        g.A = lna; g.lda = d; g.W = g.ln_wg; g.ldw = g.K; g.W_fm = g.ln_wg_fm;
         g.bias = g.ln_c; g.ln_w = g.ln_b = nullptr; g.st_in = nullptr; g.ln_a16 = nullptr;
         g.rst_in = rst; g.rst_nb = d / 32;
       } else if (g.ln_w) {
+        g.W_fm = nullptr;
         g.ln_u = nullptr;
         const float* xa = static_cast<const float*>(g.A);
         h->timed("dec_ln", 0, (double)M * d * (4.0 + e), st_,
@@ -1241,6 +1270,16 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       }
       g.tile = ring ? 2 : 1; g.skinny = 0; g.ring_kt = h->ring_kt;
       if (ring && g.resid && g.out16 && lnf_ok) g.rst_out = rst;   // residual writer: stats for the next LN
+      // <= 96 beam rows (C5's 80), K = d_model, fragment-major weights at hand: the wide single-burst
+      // tiles for out / xo / xq (16 x 32) and fc1 (32 x 32); QKV keeps the ring (tools/beam_gemm_bench.py)
+      g.a_fm = 0; g.c_fm = 0; g.out16_fm = nullptr;
+      if (ring && h->beam_wide && M <= 96 && g.K == d && g.W_fm && !g.kv_out) {
+        const std::string cn = cls;
+        if (cn == "dec_out" || cn == "dec_xo" || cn == "dec_xq") g.wide = 12;
+        else if (cn == "dec_fc1") g.wide = 22;
+      }
+      if (!g.wide && !h->beam_wfm) g.W_fm = nullptr;
+      if (ring) g.raster = h->beam_raster;
     } else {
       g.lean = h->lean;   // <= 64 rows: the lean single-tile kernel where it covers the launch
       const int region = h->prof_stamps ? lean_stamp_region(cls) : 0;
@@ -1262,7 +1301,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     GemmArgs q = drow(x, d, w.qkv_w, M, 3 * d, d, dq, d);    // LayerNorm fused (f32 A rows)
     q.ln_w = w.ln1_w; q.ln_b = w.ln1_b; q.st_in = st; q.st_nb = nbk; q.ln_a16 = lna;
     q.bias = w.qkv_b; q.mode = 2; q.n_split = d; q.kv_out = cache; q.hs_B = B; q.hs_H = H; q.kv_T = T; q.pos = pos;
-    q.kv_rps = rps; q.ln_u = w.ln1_u; q.ln_c = w.ln1_c; q.ln_wg = w.qkv_wg; q.W_fm = w.qkv_fm;
+    q.kv_rps = rps; q.ln_u = w.ln1_u; q.ln_c = w.ln1_c; q.ln_wg = w.qkv_wg; q.W_fm = w.qkv_fm; q.ln_wg_fm = w.qkv_wgfm;
     if (x16fm) { q.ln_a16 = x16fm; q.a_fm = 1; }
     proj("dec_qkv", q);
     AttnArgs a;
@@ -1336,7 +1375,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       // cross attention over the precomputed encoder K/V
       GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
       xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
-      xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg; xq.W_fm = w.xq_fm;
+      xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg; xq.W_fm = w.xq_fm; xq.ln_wg_fm = w.xq_wgfm;
       if (x16fm) { xq.ln_a16 = x16fm; xq.a_fm = 1; }
       proj("dec_xq", xq);
       AttnArgs xa;
@@ -1384,7 +1423,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
                      (h->d.ffn == 2048 || h->d.ffn == 3072 || h->d.ffn == 4096 || h->d.ffn == 5120);
     GemmArgs f1 = drow(x, d, w.fc1_w, M, h->d.ffn, d, dffn, h->d.ffn);
     f1.ln_w = w.ln2_w; f1.ln_b = w.ln2_b; f1.st_in = st; f1.st_nb = nbk; f1.ln_a16 = lna;
-    f1.bias = w.fc1_b; f1.act = 1; f1.ln_u = w.ln2_u; f1.ln_c = w.ln2_c; f1.ln_wg = w.fc1_wg; f1.W_fm = w.fc1_fm;
+    f1.bias = w.fc1_b; f1.act = 1; f1.ln_u = w.ln2_u; f1.ln_c = w.ln2_c; f1.ln_wg = w.fc1_wg; f1.W_fm = w.fc1_fm; f1.ln_wg_fm = w.fc1_wgfm;
     f1.c_fm = afm;
     if (x16fm) { f1.ln_a16 = x16fm; f1.a_fm = 1; }
     proj("dec_fc1", f1);
@@ -2370,11 +2409,28 @@ int wcb_op_gemm_kernel(int dtype, const void* A, const void* W, int M, int N, in
     REQUIRE(A && W && out && M > 0 && N > 0 && K > 0, "bad argument");
     REQUIRE(N % 8 == 0, "N must be a multiple of 8");
     REQUIRE(K % (dtype == WCB_F32 ? 32 : 64) == 0, "K must be a multiple of the 128-byte K tile");
-    REQUIRE(kernel >= 0 && kernel <= 5 && kernel != 3, "kernel: 0, 1, 2, 4 or 5");
+    REQUIRE((kernel >= 0 && kernel <= 7 && kernel != 3) || kernel == 106 || kernel == 107 ||
+            (kernel % 100 >= 11 && kernel % 100 <= 52 && kernel < 200),
+            "kernel: 0, 1, 2, 4, 5, 6, 7 or a wide tile config 11-52 (+100 on 6, 7 and the wide configs: W fragment-major)");
+    const bool wfm = kernel >= 100;
+    kernel %= 100;
     GemmArgs g = rowgemm(A, K, W, M, N, K, out, N);
     g.bias = bias; g.act = act; g.resid = resid; g.out_f32 = out_f32;
     g.raster = 8;
-    g.pp = kernel;
+    if (kernel >= 6) {   // the decode-row (beam) tiles: 6 / 7 = LDS-ring tiles (7: row panels outer, the
+                         // runtime's order before option beam_raster), 10·FM + FN = gemm_wide_kernel
+      REQUIRE(M > 64 && dtype != WCB_F32, "decode-row tiles: 16-bit, M > 64");
+      g.tile = 2; g.ring_kt = 2;
+      if (kernel == 7) g.raster = 0;
+      if (kernel <= 7 && wfm) g.W_fm = W;
+      if (kernel > 7) {
+        g.wide = kernel;
+        if (wfm) g.W_fm = W;
+        REQUIRE(!resid || resid == out, "wide tiles: the residual is updated in place (resid == out)");
+      }
+    } else {
+      g.pp = kernel;
+    }
     gemm(DType(dtype), g, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
   });
