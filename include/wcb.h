@@ -92,6 +92,8 @@ const char* wcb_last_error(const wcb_handle* h);
  *                      before finalize
  *   "beam_raster" n    decode rows > 64: ring tile order in bands of n row panels, column tiles outer (0, default:
  *                      row panels outer)
+ *   "beam_chunks" 0/1  beam top-K over 16 vocabulary chunks per row, one workgroup each (1) or one workgroup
+ *                      per row (0, default)
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)
  *   "enc_flash" v      encoder flash attention tiling: 2 (32 queries per wave), 4 (64 queries, default)
  *   "enc_raster" n     encoder GEMM tile order: bands of n row panels, column tiles outer (8, default;

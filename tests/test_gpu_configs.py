@@ -272,10 +272,11 @@ def test_c3_medium_bf16_64clips_beam5_1000_phrase_boost():
     check_beam5_boost("medium", "bf16", 1000, 64, 2)
 
 
-@pytest.mark.parametrize("opts", [{"beam_wfm": 1}, {"beam_raster": 8}], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
+@pytest.mark.parametrize("opts", [{"beam_wfm": 1}, {"beam_raster": 8}, {"beam_chunks": 1}], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_c3_ring_tile_options_match_reference(opts):
-    """The 320-row ring-tile formulations (fragment-major weights, column-outer tile order) at C3's shape:
-    clips 0-1 identical to the oracle's boosted beam search, clips 62-63 to a 2-clip call."""
+    """The 320-row formulations (ring tiles with fragment-major weights or column-outer tile order, the
+    chunked beam top-K) at C3's shape: clips 0-1 identical to the oracle's boosted beam search, clips 62-63
+    to a 2-clip call."""
     check_beam5_boost("medium", "bf16", 1000, 64, 2, opts=opts)
 
 
@@ -453,7 +454,7 @@ def test_encoder_tile_raster_bit_identical(raster):
 ALT_OPTIONS = [{"merge_v": 0}, {"enc_gemm": 1}, {"enc_gemm": 0}, {"xenc_split": 4}, {"xenc_split": 12}, {"xenc_variant": 0}, {"xenc_variant": 2},
                {"xenc_variant": 3}, {"decode_contexts": 1}, {"enc_flash": 2}, {"flash_split": 1},
                {"beam_xattn": 1}, {"beam_xattn": 2}, {"ring_kt": 1}, {"lean": 0, "lean_x": 0}, {"beam_wide": 0},
-               {"beam_wfm": 1}, {"beam_raster": 8}]
+               {"beam_wfm": 1}, {"beam_raster": 8}, {"beam_chunks": 1}]
 
 
 @pytest.mark.parametrize("opts", ALT_OPTIONS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))

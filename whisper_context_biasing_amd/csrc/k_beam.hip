@@ -21,6 +21,7 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <stdexcept>
 #include <type_traits>
 
 namespace wcb {
@@ -255,6 +256,172 @@ __global__ __launch_bounds__(NT) void beam_topk_kernel(BeamArgs a) {
   }
 }
 
+// Chunked top-K (nchunk > 1): each row's vocabulary split into nchunk chunks of CH4 float4 (a multiple of 8:
+// chunk token ranges are 32-aligned, whole bitmap words), one workgroup per (chunk, row) in two launches —
+// (1) the chunk's (max, Σexp); (2) the row's log-sum-exp from all chunk partials (fixed order, the same in
+// every chunk's workgroup), then the chunk's top-K by (score desc, token asc) with the same per-element
+// score as beam_topk_kernel. beam_step_kernel takes the top-K over the nb·nchunk·K candidates of an
+// utterance (the row top-K lies in the union of its chunks' top-K). 5120 workgroups at C3's 320 rows where
+// the per-row kernel ran 320 serial row scans.
+WCB_DEV int beam_ch4(const BeamArgs& a) {
+  const int n4 = (a.V + 3) >> 2;
+  return ((n4 + a.nchunk - 1) / a.nchunk + 7) & ~7;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void beam_chunk_stats_kernel(BeamArgs a) {
+  constexpr int NW = NT / 64;
+  if (*a.all_done) return;
+  __shared__ float red[NW];
+  const int c = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
+  const float* row = a.logits + (long)r * a.ld;
+  const f32x4* row4 = reinterpret_cast<const f32x4*>(row);
+  const int V4 = a.V >> 2, n4 = (a.V + 3) >> 2, ch4 = beam_ch4(a);
+  const int i_lo = c * ch4, i_hi = min(i_lo + ch4, n4);
+  float m = -INFINITY, s = 0.f;
+  for (int i = i_lo + tid; i < i_hi; i += NT) {
+    f32x4 x;
+    if (i < V4) x = row4[i];
+    else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = 4 * i + e < a.V ? row[4 * i + e] : -INFINITY;
+    }
+    const float bm = fmaxf(m, fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
+    if (bm > m) { s = m == -INFINITY ? 0.f : s * expf(m - bm); m = bm; }
+    if (m == -INFINITY) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += expf(x[e] - m);
+  }
+  const float mc = block_max<NW>(m, red);
+  s = m == -INFINITY ? 0.f : s * expf(m - mc);
+  const float sc = block_sum<NW>(s, red);
+  if (tid == 0) *reinterpret_cast<float2*>(a.chunk_stats + ((long)r * a.nchunk + c) * 2) = float2{mc, sc};
+}
+
+template <int NT, int KL>
+__global__ __launch_bounds__(NT) void beam_topk_chunk_kernel(BeamArgs a) {
+  constexpr int NW = NT / 64;
+  constexpr int kW = 4 * 1024 / 32;          // bitmap words of a chunk (<= 1024 float4 = 4096 tokens, 32-aligned)
+  if (*a.all_done) return;
+  __shared__ uint32_t bits[kW], tbits[kW];
+  __shared__ float wv[NW], row_ml[2];
+  __shared__ int wi[NW], wt[NW];
+  const int c = blockIdx.x, r = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* row = a.logits + (long)r * a.ld;
+  const f32x4* row4 = reinterpret_cast<const f32x4*>(row);
+  const int V4 = a.V >> 2, n4 = (a.V + 3) >> 2, ch4 = beam_ch4(a);
+  const int i_lo = c * ch4, i_hi = min(i_lo + ch4, n4);
+  const int v_lo = 4 * i_lo, v_hi = min(4 * i_hi, a.V), w_lo = v_lo >> 5;
+  // the row's log-sum-exp from the chunk partials (wave 0, fixed butterfly: identical in every chunk)
+  if (w == 0) {
+    float2 p = float2{-INFINITY, 0.f};
+    if (lane < a.nchunk) p = *reinterpret_cast<const float2*>(a.chunk_stats + ((long)r * a.nchunk + lane) * 2);
+    const float m = wave_max(p.x);
+    const float t = (p.x == -INFINITY || m == -INFINITY) ? 0.f : p.y * expf(p.x - m);
+    const float ssum = wave_sum(t);
+    if (lane == 0) { row_ml[0] = m; row_ml[1] = logf(ssum); }
+  }
+  const bool boost = a.lam != 0.f;
+  const int st = a.state[r];
+  int rb = 0, sd = 0, sk = 0;
+  if (boost) {
+    const int nwc = ((v_hi + 31) >> 5) - w_lo;
+    for (int k = tid; k < nwc; k += NT) { bits[k] = a.root_bits[w_lo + k]; tbits[k] = 0u; }
+    __syncthreads();
+    for (int t = a.trans_off[st] + tid; t < a.trans_off[st + 1]; t += NT) {
+      const int v = a.trans_tok[t];
+      if (v >= v_lo && v < v_hi) atomicOr(&tbits[(v >> 5) - w_lo], 1u << (v & 31));
+    }
+    sd = a.st_depth[st];
+    sk = a.st_keep[st];
+    rb = sk - sd;
+  }
+  __syncthreads();
+  const float m = row_ml[0], lsum = row_ml[1];
+  const bool mask_eos = *a.step < a.min_new;
+  const float rsc = a.run_sc[r];
+  float lv[KL];
+  int li[KL];
+#pragma unroll
+  for (int k = 0; k < KL; ++k) { lv[k] = -INFINITY; li[k] = 0x7fffffff; }
+  auto insert = [&](float x, int v) {
+    if (beam_better(x, v, lv[KL - 1], li[KL - 1])) {
+      float pv = x;
+      int pi = v;
+#pragma unroll
+      for (int k = 0; k < KL; ++k) {
+        if (beam_better(pv, pi, lv[k], li[k])) {
+          const float tv = lv[k];
+          const int ti = li[k];
+          lv[k] = pv; li[k] = pi; pv = tv; pi = ti;
+        }
+      }
+    }
+  };
+  // the chunk's scores (beam_topk_kernel's per-element arithmetic): the vocabulary pass, then trans(state)
+  for (int i = i_lo + tid; i < i_hi; i += NT) {
+    f32x4 xs;
+    if (i < V4) xs = row4[i];
+    else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xs[e] = 4 * i + e < a.V ? row[4 * i + e] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int v = 4 * i + e;
+      if (v >= a.V) continue;
+      float x = (xs[e] - m) - lsum;                                       // log_softmax
+      if (boost) {                                                        // bias boost processor
+        const int wd = (v >> 5) - w_lo;
+        if ((tbits[wd] >> (v & 31)) & 1u) continue;                       // scored below
+        x = bias_bonus(x, a.lam, rb + (int)((bits[wd] >> (v & 31)) & 1u));
+      }
+      if (mask_eos && v == a.eos) x = -INFINITY;                          // MinNewTokens processor
+      insert(x + rsc, v);                                                 // + running beam score
+    }
+  }
+  if (boost) {   // trans(state) tokens of this chunk: the exact n(s, v) = d' - d + min(k, d + 1 - d')
+    for (int t = a.trans_off[st] + tid; t < a.trans_off[st + 1]; t += NT) {
+      const int v = a.trans_tok[t];
+      if (v < v_lo || v >= v_hi) continue;
+      const int d2 = a.st_depth[a.trans_dst[t]];
+      float x = bias_bonus((row[v] - m) - lsum, a.lam, d2 - sd + min(sk, sd + 1 - d2));
+      if (mask_eos && v == a.eos) x = -INFINITY;
+      insert(x + rsc, v);
+    }
+  }
+  int head = 0;
+  for (int k = 0; k < a.K; ++k) {   // K rounds: block argmax over the threads' list heads
+    float hv = -INFINITY;
+    int hi = 0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < KL; ++q)
+      if (q == head) { hv = lv[q]; hi = li[q]; }
+    int ht = tid;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(hv, o, 64);
+      const int oi = __shfl_xor(hi, o, 64), ot = __shfl_xor(ht, o, 64);
+      if (beam_better(ov, oi, hv, hi)) { hv = ov; hi = oi; ht = ot; }
+    }
+    if (lane == 0) { wv[w] = hv; wi[w] = hi; wt[w] = ht; }
+    __syncthreads();
+    float bv = wv[0];
+    int bi = wi[0], bt = wt[0];
+#pragma unroll
+    for (int q = 1; q < NW; ++q)
+      if (beam_better(wv[q], wi[q], bv, bi)) { bv = wv[q]; bi = wi[q]; bt = wt[q]; }
+    if (tid == bt) ++head;
+    // fewer than K elements (or an all-NaN chunk): the index stays inside the vocabulary
+    if (tid == 0) {
+      const long o = ((long)r * a.nchunk + c) * a.K + k;
+      a.cand_val[o] = bv;
+      a.cand_tok[o] = bi >= 0 && bi < a.V ? bi : a.eos;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void beam_step_kernel(BeamArgs a) {
   if (*a.all_done) {   // frozen search: a step changes nothing, so every beam extends itself by pad
     if (threadIdx.x < a.nb) {
@@ -278,33 +445,39 @@ __global__ __launch_bounds__(256) void beam_step_kernel(BeamArgs a) {
   const int cur = a.P + step;                 // tokens in every running sequence before this one
   const int Lg = a.Lt - a.P;
   const int unsat_old = a.flags[2 * b];
-  // ---- phase 1 (wave 0): top-K of the nb·K candidates by (score desc, beam·V + token asc)
+  // ---- phase 1 (wave 0): top-K of the nb·nchunk·K candidates by (score desc, beam·V + token asc);
+  // candidate j of the utterance at lane j % 64, slot j / 64 (kCandPL slots: nb·nchunk·K <= 64·kCandPL)
   if (tid < 64) {
-    const int nc = nb * K;   // <= 128: two per lane
-    float v0 = -INFINITY, v1 = -INFINITY;
-    int f0 = 0x7fffffff, f1 = 0x7fffffff;
-    if (lane < nc) {
-      const int rr = lane / K, k = lane % K;
-      v0 = a.cand_val[(long)(R0 + rr) * K + k];
-      f0 = rr * a.V + a.cand_tok[(long)(R0 + rr) * K + k];
-    }
-    if (lane + 64 < nc) {
-      const int rr = (lane + 64) / K, k = (lane + 64) % K;
-      v1 = a.cand_val[(long)(R0 + rr) * K + k];
-      f1 = rr * a.V + a.cand_tok[(long)(R0 + rr) * K + k];
+    constexpr int kCandPL = 2 * kBeamChunks;
+    const int per_row = a.nchunk * K, nc = nb * per_row;
+    float cv[kCandPL];
+    int cf[kCandPL];
+#pragma unroll
+    for (int q = 0; q < kCandPL; ++q) {
+      const int j = q * 64 + lane;
+      cv[q] = -INFINITY; cf[q] = 0x7fffffff;
+      if (j < nc) {
+        const int rr = j / per_row;
+        cv[q] = a.cand_val[(long)R0 * per_row + j];
+        cf[q] = rr * a.V + a.cand_tok[(long)R0 * per_row + j];
+      }
     }
     for (int k = 0; k < K; ++k) {
-      float bv = v0;
-      int bf = f0;
-      if (beam_better(v1, f1, bv, bf)) { bv = v1; bf = f1; }
+      float bv = cv[0];
+      int bf = cf[0];
+#pragma unroll
+      for (int q = 1; q < kCandPL; ++q)
+        if (beam_better(cv[q], cf[q], bv, bf)) { bv = cv[q]; bf = cf[q]; }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
         const float ov = __shfl_xor(bv, o, 64);
         const int of = __shfl_xor(bf, o, 64);
         if (beam_better(ov, of, bv, bf)) { bv = ov; bf = of; }
       }
-      if (f0 == bf) { v0 = -INFINITY; f0 = 0x7fffffff; }
-      else if (f1 == bf) { v1 = -INFINITY; f1 = 0x7fffffff; }
+      bool gone = false;   // the winner leaves its lane (the first slot holding it)
+#pragma unroll
+      for (int q = 0; q < kCandPL; ++q)
+        if (!gone && cf[q] == bf && cv[q] == bv) { cv[q] = -INFINITY; cf[q] = 0x7fffffff; gone = true; }
       if (lane == 0) { tv[k] = bv; tb[k] = bf / a.V; tt[k] = bf % a.V; }
     }
   }
@@ -439,8 +612,25 @@ void beam_init(const BeamArgs& a, hipStream_t s) {
   WCB_LAUNCH(beam_init_kernel, dim3(a.B * a.nb), dim3(256), 0, s, a);
 }
 void beam_select(const BeamArgs& a, hipStream_t s) {
-  // 16 waves per row while the rows fit one per CU (C5: 80 rows), 8 up to two per CU (C3: 320)
   const int rows = a.B * a.nb;
+  if (a.nchunk > 1) {   // chunked: (max, Σexp) per chunk, then the chunk top-K lists
+    if (a.nchunk > kBeamChunks || a.nb * a.K > 2 * 64 || a.nb * a.nchunk * a.K > 64 * 2 * kBeamChunks)
+      throw std::runtime_error("internal error: chunked beam top-K beyond its candidate budget");
+    if ((((a.V + 3) / 4 + a.nchunk - 1) / a.nchunk + 7) / 8 * 8 > 1024)
+      throw std::runtime_error("internal error: chunked beam top-K: vocabulary chunk above 4096 tokens");
+    WCB_LAUNCH((beam_chunk_stats_kernel<256>), dim3(a.nchunk, rows), dim3(256), 0, s, a);
+    auto chunk = [&](auto kl) {
+      constexpr int KL = decltype(kl)::value;
+      WCB_LAUNCH((beam_topk_chunk_kernel<256, KL>), dim3(a.nchunk, rows), dim3(256), 0, s, a);
+    };
+    if (a.K <= 4) chunk(std::integral_constant<int, 4>{});
+    else if (a.K <= 8) chunk(std::integral_constant<int, 8>{});
+    else if (a.K <= 12) chunk(std::integral_constant<int, 12>{});
+    else chunk(std::integral_constant<int, 16>{});
+    WCB_LAUNCH(beam_step_kernel, dim3(a.B), dim3(256), 0, s, a);
+    return;
+  }
+  // 16 waves per row while the rows fit one per CU (C5: 80 rows), 8 up to two per CU (C3: 320)
   auto topk = [&](auto kl) {
     constexpr int KL = decltype(kl)::value;
     if (rows <= 256) WCB_LAUNCH((beam_topk_kernel<1024, KL>), dim3(rows), dim3(1024), 0, s, a);

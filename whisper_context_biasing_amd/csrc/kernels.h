@@ -255,6 +255,7 @@ void gather_col(int* dst, const int* src, int M, int ld, int col, hipStream_t s)
 constexpr int kMaxBeams = 8;
 constexpr int kBeamMaxLen = 448;       // max_target_positions of every Whisper size
 constexpr int kBeamMaxVocab = 53248;   // LDS boost bitmap
+constexpr int kBeamChunks = 16;        // vocabulary chunks per row of the chunked beam top-K
 struct BeamArgs {
   const float* logits = nullptr; long ld = 0; int V = 0;
   int B = 0, nb = 0, K = 0;            // utterances, beams, candidates kept per step (2·nb)
@@ -268,7 +269,9 @@ struct BeamArgs {
   int* next_ids = nullptr; int* state = nullptr;        // [R]
   float* run_sc = nullptr; int* run_seq = nullptr;      // [R], [R][Lt-P]
   int* phys = nullptr;                                  // [R][T] cache row of every key position
-  float* cand_val = nullptr; int* cand_tok = nullptr;   // [R][K] per-row top-K
+  float* cand_val = nullptr; int* cand_tok = nullptr;   // [R][nchunk][K] top-K per (row, vocabulary chunk)
+  int nchunk = 1;                                       // vocabulary chunks per row (k_beam.hip beam_select)
+  float* chunk_stats = nullptr;                         // [R][nchunk] (max, Σexp) of each chunk (nchunk > 1)
   float* fin_sc = nullptr; int* fin_done = nullptr; int* fin_len = nullptr; int* fin_seq = nullptr;  // [B·nb](·(Lt-P))
   int* flags = nullptr;                                 // [B][2]: heuristic unsatisfied, all K hit
   int* out_ids = nullptr; int out_ld = 0; int* out_len = nullptr;

@@ -217,6 +217,11 @@ struct wcb_handle {
   // "beam_raster": bands of n row panels with the column tiles outer, so the row tiles sharing a weight
   // tile run on one XCD; 0 = row panels outer)
   int beam_wfm = 0;
+  // beam top-K: each row's vocabulary in kBeamChunks chunks, one workgroup per (chunk, row) (option
+  // "beam_chunks" 1) or one workgroup per row (0, default; k_beam.hip beam_select). Measured: C3 6,160 vs
+  // 6,228, C5 2,517 vs 2,518 audio-s/s — the per-row kernel's 320 (80) long workgroups already run beside
+  // the other decode context's launches, so spreading the scan over the chip only adds contention
+  int beam_chunks = 0;
   int beam_raster = 0;
   // greedy LM head: the final LayerNorm in a launch of its own (option "lm_ln_split" 1) or inside the
   // column walk (0, default: with the f32 copies of the A rows no longer held across the statistics
@@ -667,6 +672,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       // the folded W·diag(γ) copies are built at finalize only when it is on
       REQUIRE(!h->ready, "option ln_fold selects weight layouts: set it before wcb_finalize_weights");
       h->ln_fold = value != 0;
+    } else if (n == "beam_chunks") {
+      h->beam_chunks = value != 0;
     } else if (n == "beam_wfm") {
       REQUIRE(!h->ready, "option beam_wfm selects weight layouts: set it before wcb_finalize_weights");
       h->beam_wfm = value != 0;
@@ -1566,10 +1573,11 @@ void prefill_step(wcb_handle* h, StepCfg c, int np, const int* src, int ld) {
 // into [R] running / finished scores, finished flags and lengths, [R][Lg] running and finished
 // sequences, [R][Tc] key map, [R][K] per-row candidates, [B][2] utterance flags, [R] parent beams.
 // ensure_beam_buf sizes it (draining the streams first when it grows); beam_args carves it.
-constexpr int kBeamBufs = 11;
+constexpr int kBeamBufs = 12;
 void beam_words(int B, int nb, int Lg, int Tc, size_t* w) {
   const size_t R = (size_t)B * nb, K = 2 * (size_t)nb;
-  const size_t v[kBeamBufs] = {R, R, R, R, R * Lg, R * Lg, R * Tc, R * K, R * K, (size_t)B * 2, R};
+  const size_t C = kBeamChunks;   // candidate lists per (row, vocabulary chunk); chunk (max, Σexp)
+  const size_t v[kBeamBufs] = {R, R, R, R, R * Lg, R * Lg, R * Tc, R * C * K, R * C * K, (size_t)B * 2, R, R * C * 2};
   std::copy(v, v + kBeamBufs, w);
 }
 void ensure_beam_buf(wcb_handle* h, DecCtx& D, int B, int nb, int Lg, int Tc) {
@@ -1596,6 +1604,8 @@ BeamArgs beam_args(wcb_handle* h, DecCtx& D, int B, int nb, int P, int Lt, int T
   bm.run_sc = (float*)take(0); bm.fin_sc = (float*)take(1); bm.fin_done = (int*)take(2); bm.fin_len = (int*)take(3);
   bm.run_seq = (int*)take(4); bm.fin_seq = (int*)take(5); bm.phys = (int*)take(6);
   bm.cand_val = (float*)take(7); bm.cand_tok = (int*)take(8); bm.flags = (int*)take(9); bm.parent = (int*)take(10);
+  bm.chunk_stats = (float*)take(11);
+  bm.nchunk = h->beam_chunks ? kBeamChunks : 1;
   bm.logits = D.logits.as<float>(); bm.ld = h->vocab_pad; bm.V = h->d.vocab;
   bm.B = B; bm.nb = nb; bm.K = 2 * nb; bm.P = P; bm.Lt = Lt; bm.T = Tc;
   bm.eos = h->d.eos_token_id; bm.pad = h->d.pad_token_id; bm.min_new = min_new;
