@@ -92,6 +92,9 @@ const char* wcb_last_error(const wcb_handle* h);
  *                      before finalize
  *   "beam_raster" n    decode rows > 64: ring tile order in bands of n row panels, column tiles outer (0, default:
  *                      row panels outer)
+ *   "lean_fold" 0/1    <= 64 rows: the LayerNorm-fused projections (QKV, cross-q, fc1) with the LayerNorm folded
+ *                      into fragment-major W·diag(γ) copies (1, default) or normalised in the kernel (0); before
+ *                      finalize
  *   "beam_chunks" 0/1  beam top-K over 16 vocabulary chunks per row, one workgroup each (1) or one workgroup
  *                      per row (0, default)
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)

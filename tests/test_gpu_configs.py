@@ -214,6 +214,26 @@ def test_c2_small_b32_1000_phrase_boost(recipe, seed, dtype):
             assert n >= 0.75 * ref.size, (n, ref.size)
 
 
+@pytest.mark.parametrize("recipe,seed", [("margin", 1), ("diverse", 0)])
+def test_c2_lean_unfolded_matches_reference(recipe, seed):
+    """Option lean_fold 0 (the greedy LN-fused projections normalising their rows in the kernel instead of
+    the default folded weights) on C2's decode: whisper-small bf16, 32 clips, 64 tokens EOS masked, 1000
+    phrases, lambda 2 — rows 0-3 against the oracle, margin-gated with every checkable token checked."""
+    dims = get_dims("small")
+    m = model("small", seed, recipe, "bf16", {"lean_fold": 0})
+    phrases = synth_bias_list(1000, eot=dims.eos_token_id)
+    x = mel_of(dims, 32)
+    ids = m.generate(x, max_length=64, min_new_tokens=64, bias_list=phrases, bias_boost=2.0).cpu().numpy()
+    om = W.OracleModel.from_dims(dims, weights("small", seed, recipe))
+    ref, margin = om.generate(x[:4].numpy(), max_length=64, min_new_tokens=64, bias=phrases, bias_boost=2.0,
+                              return_margins=True, trim=False)
+    checkable = sum(int(np.argmax(mg < TAU)) if (mg < TAU).any() else mg.size for mg in margin)
+    n = gated_equal(ids[:4], ref, margin, name=f"c2-lean-unfolded-{recipe}")
+    assert n == checkable
+    if recipe == "margin":
+        assert n >= 0.75 * ref.size, (n, ref.size)
+
+
 @pytest.mark.parametrize("recipe,seed,dtype", [("margin", 1, "bf16"), ("margin", 1, "f32"), ("diverse", 0, "bf16")])
 def test_c2_timed_path_pcm_to_ids(recipe, seed, dtype):
     """The bench's timed step end to end (bench.py step(): 32 synthetic clips of PCM resident on the
@@ -272,7 +292,8 @@ def test_c3_medium_bf16_64clips_beam5_1000_phrase_boost():
     check_beam5_boost("medium", "bf16", 1000, 64, 2)
 
 
-@pytest.mark.parametrize("opts", [{"beam_wfm": 1}, {"beam_raster": 8}, {"beam_chunks": 1}], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
+@pytest.mark.parametrize("opts", [{"beam_wfm": 1}, {"beam_raster": 8}, {"beam_chunks": 1},
+               {"lean_fold": 0}], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
 def test_c3_ring_tile_options_match_reference(opts):
     """The 320-row formulations (ring tiles with fragment-major weights or column-outer tile order, the
     chunked beam top-K) at C3's shape: clips 0-1 identical to the oracle's boosted beam search, clips 62-63
@@ -398,18 +419,22 @@ def test_lean_decode_projections_bit_identical(size, dtype, B):
     """dec_lean_kernel (option "lean", default) against gemm_dec_kernel on the same greedy decode with the
     1000-phrase boost: every decode projection of <= 64 rows (QKV with the KV append, out / xo / fc2
     residual writers, LN-fused xq / fc1, grouped W_k,hᵀ) has the same K split and sum order, so the ids
-    must be identical (d = 768 / 1024 / 1280 tables)."""
+    must be identical (d = 768 / 1024 / 1280 tables). The folded-LayerNorm form (option lean_fold, default)
+    has its own arithmetic (the oracle tests pin it): there the row-layout and fragment-major residual copies
+    must agree bit for bit."""
     dims = get_dims(size)
     sd = weights(size, 0, "diverse")
     x = mel_of(dims, B)
     phrases = synth_bias_list(1000, eot=dims.eos_token_id)
-    out = []
-    for opts in ({"lean": 1}, {"lean": 1, "lean_x": 0}, {"lean": 0}):
-        m = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options=opts)
-        out.append(m.generate(x, max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0).cpu().numpy())
-        del m
-    for o in out[1:]:
-        assert np.array_equal(out[0], o), np.argwhere(out[0] != o)[:8]
+    for group in ([{"lean": 1, "lean_fold": 0}, {"lean": 1, "lean_x": 0, "lean_fold": 0}, {"lean": 0, "lean_fold": 0}],
+                  [{"lean": 1, "lean_fold": 1}, {"lean": 1, "lean_x": 0, "lean_fold": 1}]):
+        out = []
+        for opts in group:
+            m = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options=opts)
+            out.append(m.generate(x, max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0).cpu().numpy())
+            del m
+        for o in out[1:]:
+            assert np.array_equal(out[0], o), (group, np.argwhere(out[0] != o)[:8])
 
 
 @pytest.mark.parametrize("B,group_rows", [(24, 16), (40, 16), (5, 512)])
@@ -454,7 +479,8 @@ def test_encoder_tile_raster_bit_identical(raster):
 ALT_OPTIONS = [{"merge_v": 0}, {"enc_gemm": 1}, {"enc_gemm": 0}, {"xenc_split": 4}, {"xenc_split": 12}, {"xenc_variant": 0}, {"xenc_variant": 2},
                {"xenc_variant": 3}, {"decode_contexts": 1}, {"enc_flash": 2}, {"flash_split": 1},
                {"beam_xattn": 1}, {"beam_xattn": 2}, {"ring_kt": 1}, {"lean": 0, "lean_x": 0}, {"beam_wide": 0},
-               {"beam_wfm": 1}, {"beam_raster": 8}, {"beam_chunks": 1}]
+               {"beam_wfm": 1}, {"beam_raster": 8}, {"beam_chunks": 1},
+               {"lean_fold": 0}]
 
 
 @pytest.mark.parametrize("opts", ALT_OPTIONS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))

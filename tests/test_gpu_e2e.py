@@ -255,8 +255,8 @@ def test_fused_lean_launches_are_bit_identical(dtype):
     dims = get_dims("small")
     sd = make_weights(dims, seed=0, recipe="diverse")
     phrases = synth_bias_list(1000, eot=dims.eos_token_id)
-    models = [WhisperCB.from_state_dict(dims, sd, dtype=dtype, options=o)
-              for o in ({"xq_kq": 1}, {"xq_kq": 0})]
+    models = [WhisperCB.from_state_dict(dims, sd, dtype=dtype, options=o)   # (the q_proj LayerNorm unfolded in both)
+              for o in ({"xq_kq": 1, "lean_fold": 0}, {"xq_kq": 0, "lean_fold": 0})]
     kw = dict(max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0)
     for B in (32, 13, 40):
         x = torch.from_numpy(W.log_mel(synth_batch(B, start=3), dims.n_mel))

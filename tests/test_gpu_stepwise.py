@@ -48,13 +48,13 @@ def test_stepwise_scores_lm_head_layernorm_split_bit_identical(size, dtype, B):
     """The lean LM head with the final LayerNorm inside its column walk (default), in a launch of its own
     (option lm_ln_split: gemm_impl.h ln_rows_kernel, the same K split, sum order and normalisation), and
     the general decode kernel's fused form (option lean = 0): the chosen tokens' boosted logits returned
-    per step must be equal bit for bit."""
+    per step must be equal bit for bit (the projections' LayerNorm unfolded: lean_fold 0 in all three)."""
     dims = get_dims(size)
     sd = make_weights(dims, seed=1, recipe="diverse")
     x = torch.from_numpy(W.log_mel(synth_batch(B), dims.n_mel))
     phrases = synth_bias_list(200, eot=dims.eos_token_id)
     out = []
-    for opts in ({"lean": 1}, {"lean": 1, "lm_ln_split": 1}, {"lean": 0}):
+    for opts in ({"lean": 1, "lean_fold": 0}, {"lean": 1, "lm_ln_split": 1, "lean_fold": 0}, {"lean": 0, "lean_fold": 0}):
         m = WhisperCB.from_state_dict(dims, sd, dtype=dtype, options=opts)
         dec = m.decode_begin(m.encode(x), bias_list=phrases, bias_boost=2.0, min_new_tokens=6)
         steps = [dec.step() for _ in range(6)]

@@ -1454,22 +1454,29 @@ template <typename T> struct DecLean {
   T* att = nullptr; int ld_att = 0; unsigned long long* cnt = nullptr; int* err = nullptr;
   const T* kq_w = nullptr;
   Stamp lst;                             // stamps pass: launch start / end inside the decode graph
+  const float* ln_u = nullptr;           // FOLD: u[n] = Σ_k W'[n][k] (bias = c[n])
 };
 
 //   FZ 2 (EPI 0, LN: the cross-attention query q_h = LN(x) W_q,hᵀ + b_q): the 4 column tiles of a head store
 //   q_h write-through, meet at the head's counter, and each then computes a quarter of q'_h = W_k,hᵀ q_h
 //   (the grouped K = 64 product of the kq launch it replaces: the same two 32-deep MFMA halves summed in
 //   the same order, weights prefetched with the launch's first loads) — bit-identical to the two launches.
+//   FOLD (LN): the LayerNorm folded into the weights (the beam ring tiles' LNF algebra): W = W·diag(γ)
+//   (fragment-major), bias = c[n] = Σ_k β_k W[n][k] + b[n], ln_u = u[n] = Σ_k W'[n][k]; the MFMAs start on the
+//   raw 16-bit rows as soon as they land, the row statistics ride the partial-tile barrier, and the epilogue
+//   applies r·(acc − μ·u[n]) + c[n] — no γ / β loads, no statistics barrier, no per-element normalisation.
 template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP, bool WFM = false, bool AFM = false,
-          int FZ = 0>
+          int FZ = 0, bool FOLD = false>
 __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   constexpr bool KQ = FZ == 2 && EPI == 0 && LN && !GELU && !GRP;
+  static_assert(!FOLD || (LN && !KQ), "folded LayerNorm: LN-fused launches without the cross-query hand-off");
+  constexpr bool LNN = LN && !FOLD;   // normalise the A rows in the kernel
   using Frag = typename DT<T>::frag;
   constexpr int NT = NW * 64, K = NW * KPW * 32, R = MF * 16;
   static_assert(R * 4 <= NT, "epilogue: 4 columns per thread");
   __shared__ __attribute__((aligned(16))) float red[NW][R][17];
   __shared__ float2 rst[LN ? NW : 1][LN ? R : 1];
-  __shared__ __attribute__((aligned(16))) float lnp[LN ? 2 * K : 4];   // γ [K], β [K]
+  __shared__ __attribute__((aligned(16))) float lnp[LNN ? 2 * K : 4];   // γ [K], β [K]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ct = blockIdx.x, mb = blockIdx.y * R, n0 = ct * 16;
   const int kb = wave * (KPW * 32) + 8 * (lane >> 4);
@@ -1505,7 +1512,7 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   // LayerNorm γ / β: into LDS by LDS-DMA with the burst (one 16-byte piece per lane, K / 4 lanes each), read
   // per k-step after the statistics barrier (held in registers they took 2·KPW·8 floats per lane and kept
   // the LN-fused instances at one workgroup per CU)
-  if constexpr (LN) {
+  if constexpr (LNN) {
     for (int c = wave * 64; c < K / 4; c += NT) {   // (K / 4 is a multiple of 64: wave-uniform)
       glds16(p.gam + 4 * (c + lane), lnp + 4 * c);
       glds16(p.bet + 4 * (c + lane), lnp + K + 4 * c);
@@ -1515,8 +1522,9 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   const int er = tid >> 2, ec = n0 + (tid & 3) * 4;
   const int erow = min(mb + min(er, R - 1), p.M - 1);
   const int ecc = min(ec, p.N - 4);
-  f32x4 bias4 = f32x4{0.f, 0.f, 0.f, 0.f}, res4 = bias4;
+  f32x4 bias4 = f32x4{0.f, 0.f, 0.f, 0.f}, res4 = bias4, u4 = bias4;
   if constexpr (!GRP) bias4 = *reinterpret_cast<const f32x4*>(p.bias + ecc);
+  if constexpr (FOLD) u4 = *reinterpret_cast<const f32x4*>(p.ln_u + ecc);
   if constexpr (EPI == 1) res4 = *reinterpret_cast<const f32x4*>(p.x + (long)erow * p.ldo + ecc);
   int pos = 0;
   if constexpr (EPI == 2) pos = __builtin_nontemporal_load(p.pos);
@@ -1539,13 +1547,12 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   unsigned long long t1 = 0, t2 = 0;
   if (p.stamp) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); t1 = stamp_now(); }
   // ---------------- LayerNorm of the A rows (gemm_dec_kernel AM = 2 arithmetic)
-  if constexpr (LN) {
-    // (the f32 value of an element is re-derived from its 16-bit bits where needed: exact, no copy kept)
-    auto xf = [&](int i, int ks, int e) -> float {
-      if constexpr (__is_same(T, bf16_t)) return bf16_to_f((bf16_t)a[i][ks][e]);
-      else return float(a[i][ks][e]);
-    };
-    float mean[MF], rstd[MF];
+  // (the f32 value of an element is re-derived from its 16-bit bits where needed: exact, no copy kept)
+  auto xf = [&](int i, int ks, int e) -> float {
+    if constexpr (__is_same(T, bf16_t)) return bf16_to_f((bf16_t)a[i][ks][e]);
+    else return float(a[i][ks][e]);
+  };
+  if constexpr (LN) {   // row statistics partials of this wave's K slice (FOLD: read after the tile barrier)
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
       float s1 = 0.f, s2 = 0.f;
@@ -1562,6 +1569,9 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
       s1 = xor32_add(s1); s2 = xor32_add(s2);
       if (lane < 16) rst[wave][i * 16 + lane] = float2{s1, s2};
     }
+  }
+  if constexpr (LNN) {
+    float mean[MF], rstd[MF];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's γ / β pieces landed (LDS-DMA)
     __syncthreads();
 #pragma unroll
@@ -1605,12 +1615,21 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
   const bool live = er < R && row < p.M && ec < p.N;
   if (!KQ && !live) return;   // (KQ: every thread reaches the hand-off below)
   if (live) {
+  float fm_mean = 0.f, fm_rstd = 1.f;
+  if constexpr (FOLD) {   // the row's (μ, r) from the waves' partials, the LN path's order and formula
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) { const float2 t = rst[q][er]; s1 += t.x; s2 += t.y; }
+    fm_mean = s1 / K;
+    fm_rstd = rsqrtf(fmaxf(s2 / K - fm_mean * fm_mean, 0.f) + 1e-5f);
+  }
   float v[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < NW; ++q) s += red[q][er][(tid & 3) * 4 + e];
+    if constexpr (FOLD) s = fm_rstd * (s - fm_mean * u4[e]);
     v[e] = s + bias4[e];
     if constexpr (GELU) v[e] = gelu_t<T>(v[e]);
   }
@@ -1695,9 +1714,26 @@ __global__ __launch_bounds__(NW * 64) void dec_lean_kernel(DecLean<T> p) {
 
 inline thread_local unsigned long long* g_lean_stamp = nullptr;   // tools/dec_kernel_bench only
 
-template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP>
+template <typename T, int MF, int NW, int KPW, bool LN, int EPI, bool GELU, bool GRP, bool FOLD = false>
 static void launch_lean_k(const GemmArgs& g, hipStream_t s) {
   DecLean<T> p;
+  if constexpr (FOLD) {   // folded LayerNorm: W' fragment-major, c[n] as the bias, u[n]; A = the raw 16-bit rows
+    if (!g.ln_wg_fm || !g.ln_u || !g.ln_c) throw std::runtime_error("internal error: folded lean launch without its folded weights");
+    p.stamp = g_lean_stamp;
+    if (g.lstamp) p.lst = *g.lstamp;
+    p.W = reinterpret_cast<const T*>(g.ln_wg_fm);
+    p.A = reinterpret_cast<const T*>(g.ln_a16);
+    p.bias = g.ln_c; p.ln_u = g.ln_u;
+    p.out = reinterpret_cast<T*>(g.out);
+    p.kv = reinterpret_cast<T*>(g.kv_out); p.pos = g.pos;
+    p.M = g.M; p.N = g.N; p.lda = (int)g.lda; p.ldo = (int)g.ldc;
+    p.n_split = g.n_split; p.kvB = g.hs_B; p.kvH = g.hs_H; p.kvT = g.kv_T;
+    if (g.c_fm) lean_cfg(g.N, p.cfm_nw, p.cfm_kpw);
+    const dim3 grid((g.N + 15) / 16, (g.M + MF * 16 - 1) / (MF * 16));
+    if (g.a_fm) WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, true, 0, true>), grid, dim3(NW * 64), 0, s, p);
+    else WCB_LAUNCH((dec_lean_kernel<T, MF, NW, KPW, LN, EPI, GELU, GRP, true, false, 0, true>), grid, dim3(NW * 64), 0, s, p);
+    return;
+  }
   p.stamp = g_lean_stamp;
   if (g.lstamp) p.lst = *g.lstamp;
   p.W = reinterpret_cast<const T*>(g.W_fm ? g.W_fm : g.W);
@@ -1761,6 +1797,14 @@ static bool launch_lean(const GemmArgs& g, hipStream_t s) {
 #define WCB_LN(k, nw, kpw)                                                                          \
   if (g.K == k) {                                                                                   \
     const bool mf2 = g.N >= 2048 && g.M > 16;                                                       \
+    if (fold) {                                                                                     \
+      if (g.mode == 2 && mf2) launch_lean_k<T, 2, nw, kpw, true, 2, false, false, true>(g, s);      \
+      else if (g.mode == 2) launch_lean_k<T, 1, nw, kpw, true, 2, false, false, true>(g, s);        \
+      else if (g.act && mf2) launch_lean_k<T, 2, nw, kpw, true, 0, true, false, true>(g, s);        \
+      else if (g.act) launch_lean_k<T, 1, nw, kpw, true, 0, true, false, true>(g, s);               \
+      else launch_lean_k<T, 1, nw, kpw, true, 0, false, false, true>(g, s);                         \
+      return true;                                                                                  \
+    }                                                                                               \
     if (g.mode == 2 && mf2) launch_lean_k<T, 2, nw, kpw, true, 2, false, false>(g, s);              \
     else if (g.mode == 2) launch_lean_k<T, 1, nw, kpw, true, 2, false, false>(g, s);                \
     else if (g.act && mf2) launch_lean_k<T, 2, nw, kpw, true, 0, true, false>(g, s);                \
@@ -1768,6 +1812,9 @@ static bool launch_lean(const GemmArgs& g, hipStream_t s) {
     else launch_lean_k<T, 1, nw, kpw, true, 0, false, false>(g, s);                                 \
     return true;                                                                                    \
   }
+      // folded LayerNorm (runtime option lean_fold): the folded weights' fragment-major copy at hand, and not
+      // the cross-query hand-off launch
+      const bool fold = g.lean_fold && g.ln_wg_fm && g.ln_u && g.ln_c && !g.kq_w;
       WCB_LN(512, 4, 4) WCB_LN(768, 4, 6) WCB_LN(1024, 4, 8) WCB_LN(1280, 8, 5)
 #undef WCB_LN
       return false;

@@ -217,6 +217,12 @@ struct wcb_handle {
   // "beam_raster": bands of n row panels with the column tiles outer, so the row tiles sharing a weight
   // tile run on one XCD; 0 = row panels outer)
   int beam_wfm = 0;
+  // <= 64 rows (greedy), the LN-fused lean projections (QKV, xq, fc1): the LayerNorm folded into the weights
+  // (W·diag(γ) fragment-major, c, u: the beam tiles' algebra) instead of normalising the A rows in the kernel
+  // (option "lean_fold", set before finalize). C2 bench 19,777 / 20,001 / 19,974 vs 19,527 / 19,553 / 19,692
+  // audio-s/s (interleaved): the MFMAs start as soon as the rows land, the statistics ride the partial-tile
+  // barrier — the in-kernel LayerNorm cost its launches ~1.1 µs each (xq 3.89 vs out 2.78 µs in-graph)
+  int lean_fold = 1;
   // beam top-K: each row's vocabulary in kBeamChunks chunks, one workgroup per (chunk, row) (option
   // "beam_chunks" 1) or one workgroup per row (0, default; k_beam.hip beam_select). Measured: C3 6,160 vs
   // 6,228, C5 2,517 vs 2,518 audio-s/s — the per-row kernel's 320 (80) long workgroups already run beside
@@ -672,6 +678,9 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       // the folded W·diag(γ) copies are built at finalize only when it is on
       REQUIRE(!h->ready, "option ln_fold selects weight layouts: set it before wcb_finalize_weights");
       h->ln_fold = value != 0;
+    } else if (n == "lean_fold") {
+      REQUIRE(!h->ready, "option lean_fold selects weight layouts: set it before wcb_finalize_weights");
+      h->lean_fold = value != 0;
     } else if (n == "beam_chunks") {
       h->beam_chunks = value != 0;
     } else if (n == "beam_wfm") {
@@ -881,10 +890,10 @@ int wcb_finalize_weights(wcb_handle* h) {
         lw.fc1_fm = fm(lw.fc1_w, F, d);
         lw.fc2_fm = fm(lw.fc2_w, d, F);
         if (lw.xkt_w) lw.xkt_fm = fm(lw.xkt_w, H * d, 64);
-        if ((h->beam_wide || h->beam_wfm) && h->ln_fold) {   // beam-row tiles: the folded weights fragment-major
+        if ((h->beam_wide || h->beam_wfm || h->lean_fold) && h->ln_fold) {   // the folded weights fragment-major
           lw.xq_wgfm = fm(lw.xq_wg, d, d);
           lw.fc1_wgfm = fm(lw.fc1_wg, F, d);
-          if (h->beam_wfm) lw.qkv_wgfm = fm(lw.qkv_wg, 3 * d, d);
+          if (h->beam_wfm || h->lean_fold) lw.qkv_wgfm = fm(lw.qkv_wg, 3 * d, d);
         }
         if (lw.xv_w && h->lean && h->dt != kF32 && d % 128 == 0 && d <= 1024) {   // 16 output rows per wave, all of K per wave
           lw.xv_fm = h->own((size_t)d * d * e);
@@ -1289,6 +1298,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       if (ring) g.raster = h->beam_raster;
     } else {
       g.lean = h->lean;   // <= 64 rows: the lean single-tile kernel where it covers the launch
+      g.lean_fold = h->lean_fold && g.ln_w && g.ln_wg_fm && g.ln_u && g.ln_c;
       const int region = h->prof_stamps ? lean_stamp_region(cls) : 0;
       if (region) {   // stamps pass: this launch's start / end inside the replayed graph
         lst.base = h->stamp_base(c.buf, region);
