@@ -95,6 +95,9 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "lean_fold" 0/1    <= 64 rows: the LayerNorm-fused projections (QKV, cross-q, fc1) with the LayerNorm folded
  *                      into fragment-major W·diag(γ) copies (1, default) or normalised in the kernel (0); before
  *                      finalize
+ *   "xqk" 0/1          greedy cross query (encoder space, lean, folded): q_h and q'_h = W_k,hᵀ q_h in one launch
+ *                      with no hand-off, each workgroup recomputing its head's q_h (1, default) or the xq → kq
+ *                      launches (0)
  *   "beam_chunks" 0/1  beam top-K over 16 vocabulary chunks per row, one workgroup each (1) or one workgroup
  *                      per row (0, default)
  *   "xenc_split" n     key ranges per row of the greedy encoder-space cross-attention (1..16, before finalize)

@@ -273,6 +273,23 @@ def test_fused_lean_launches_are_bit_identical(dtype):
         fused.synchronize()
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_fused_cross_query_is_bit_identical(dtype):
+    """Option xqk (gemm_impl.h dec_xqk_kernel): each workgroup recomputes its head's q_h with the folded lean
+    q_proj's K split, MFMA and sum order, then its chunk of q'_h = W_k,hᵀ q_h in the kq launch's order — the
+    same arithmetic as the xq → kq launches, so identical ids even on the diverse recipe's near-ties: 32 rows,
+    13 and 40 rows (ragged 16-row blocks), 1000-phrase boost."""
+    dims = get_dims("small")
+    sd = make_weights(dims, seed=0, recipe="diverse")
+    phrases = synth_bias_list(1000, eot=dims.eos_token_id)
+    models = [WhisperCB.from_state_dict(dims, sd, dtype=dtype, options=o) for o in ({"xqk": 1}, {"xqk": 0})]
+    kw = dict(max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0)
+    for B in (32, 13, 40):
+        x = torch.from_numpy(W.log_mel(synth_batch(B, start=3), dims.n_mel))
+        out = [m.generate(x, **kw).cpu().numpy() for m in models]
+        np.testing.assert_array_equal(out[0], out[1])
+
+
 def test_bias_from_another_handle_is_rejected():
     """A bias automaton belongs to the handle that built it (its decode graphs are keyed on it): passing
     it to another handle is an argument error, not a silently wrong boost."""

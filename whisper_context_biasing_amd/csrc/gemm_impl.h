@@ -14,6 +14,7 @@
 //   partials reduced through LDS.
 #pragma once
 #include <stdexcept>
+#include <string>
 #include "common.h"
 #include "kernels.h"
 
@@ -1768,6 +1769,156 @@ static void launch_lean_k(const GemmArgs& g, hipStream_t s) {
   }
 }
 
+// Greedy cross-attention query and its encoder-space form in ONE launch without a hand-off
+// (dec_xqk_kernel): workgroup (head h, q' column chunk c, 16·MF-row block) computes the head's whole
+// q_h = LN(x) W_q,hᵀ + b_q,h for its rows (the folded LayerNorm, the lean q_proj launch's K split, MFMA and
+// wave-sum order and epilogue: bit-identical q_h), keeps it in LDS, and multiplies it by its chunk of
+// W_k,hᵀ (the kq launch's two 32-deep halves summed in that launch's order: bit-identical q'_h). Each of a
+// head's NCH chunk workgroups recomputes q_h (W_q,h re-read from L2 NCH times): no cross-workgroup
+// dependency, one launch boundary less per layer than xq → kq.
+template <typename T> struct XqkArgs {
+  const T* A; const T* Wq; const float* u; const float* c; const T* Wk; T* qp;
+  int M, H, D;   // rows, heads, d_model (K of the q projection; q'_h has D columns)
+};
+template <typename T, int MF, int NW, int KPW, int NCH, bool AFM>
+__global__ __launch_bounds__(NW * 64) void dec_xqk_kernel(XqkArgs<T> p) {
+  using Frag = typename DT<T>::frag;
+  constexpr int NT = NW * 64, K = NW * KPW * 32, R = MF * 16;
+  constexpr int CW = K / NCH, NT16 = CW / 16, TPW = (NT16 + NW - 1) / NW;   // q' columns per chunk, tiles
+  static_assert(CW % 16 == 0 && R * 16 <= NT, "chunk of whole tiles; one 4-column item per thread");
+  __shared__ __attribute__((aligned(16))) float red[NW][R][65];
+  __shared__ float2 rst[NW][R];
+  __shared__ __attribute__((aligned(16))) T qa[R][72];     // q_h (16-bit), rows padded against bank conflicts
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);          // a head's chunks run on one XCD (W_q,h in its L2)
+  const int h = wg / NCH, ch = wg % NCH, mb = blockIdx.y * R;
+  const int kb = wave * (KPW * 32) + 8 * (lane >> 4);
+  // ---------------- the launch's loads, one burst: W_q,h's 4 column tiles, the A rows, this chunk's W_k,hᵀ
+  Frag w[4][KPW], a[MF][KPW], wk[TPW][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const T* wr = p.Wq + ((((long)(h * 4 + j) * NW + wave) * KPW * 64) + lane) * 8;
+#pragma unroll
+    for (int ks = 0; ks < KPW; ++ks) w[j][ks] = __builtin_nontemporal_load(reinterpret_cast<const Frag*>(wr + ks * 512));
+  }
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    if constexpr (AFM) {
+      const T* ar = p.A + ((((long)(mb / 16 + i) * NW + wave) * KPW * 64) + lane) * 8;
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) a[i][ks] = load_frag<T>(ar + ks * 512);
+    } else {
+      const T* ar = p.A + (long)min(mb + i * 16 + (lane & 15), p.M - 1) * K + kb;
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) a[i][ks] = load_frag<T>(ar + ks * 32);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int tt = min(wave + t * NW, NT16 - 1);
+    const long ct = (long)h * (K / 16) + ch * NT16 + tt;   // W_kt fragment-major tile (K = 64: two k-steps)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) wk[t][kh] = __builtin_nontemporal_load(reinterpret_cast<const Frag*>(p.Wk + ((ct * 2 + kh) * 64 + lane) * 8));
+  }
+  // epilogue item of the q_h phase: row er, columns cq .. cq + 3 of the head
+  const int er = tid >> 4, cq = (tid & 15) * 4;
+  const bool item = er < R;
+  const f32x4 u4 = *reinterpret_cast<const f32x4*>(p.u + h * 64 + cq);
+  const f32x4 c4 = *reinterpret_cast<const f32x4*>(p.c + h * 64 + cq);
+  __builtin_amdgcn_sched_barrier(0);
+  // ---------------- row statistics partials (the lean LN arithmetic) and the q_h MFMAs
+#pragma unroll
+  for (int i = 0; i < MF; ++i) {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KPW; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v;
+        if constexpr (__is_same(T, bf16_t)) v = bf16_to_f((bf16_t)a[i][ks][e]);
+        else v = float(a[i][ks][e]);
+        s1 += v;
+        s2 = fmaf(v, v, s2);
+      }
+    s1 = xor16_add(s1); s2 = xor16_add(s2);
+    s1 = xor32_add(s1); s2 = xor32_add(s2);
+    if (lane < 16) rst[wave][i * 16 + lane] = float2{s1, s2};
+  }
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KPW; ++ks) acc = mma16(a[i][ks], w[j][ks], acc);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[wave][i * 16 + (lane >> 4) * 4 + e][j * 16 + (lane & 15)] = acc[e];
+    }
+  __syncthreads();
+  // ---------------- q_h = r·(acc − μ·u) + c (the folded lean epilogue), 16-bit, into LDS
+  if (item) {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) { const float2 t = rst[q][er]; s1 += t.x; s2 += t.y; }
+    const float mean = s1 / K, rstd = rsqrtf(fmaxf(s2 / K - mean * mean, 0.f) + 1e-5f);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float sum = 0.f;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) sum += red[q][er][cq + e];
+      sum = rstd * (sum - mean * u4[e]);
+      qa[er][cq + e] = DT<T>::fromf(sum + c4[e]);
+    }
+  }
+  __syncthreads();
+  // ---------------- q'_h = W_k,hᵀ q_h for this chunk's columns: the kq launch's two halves, its sum order
+  Frag qf[2];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) qf[kh] = *reinterpret_cast<const Frag*>(&qa[lane & 15][kh * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int tt = wave + t * NW;
+    if (tt < NT16) {
+      const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 a0 = mma16(qf[0], wk[t][0], z), a1 = mma16(qf[1], wk[t][1], z);
+      const int col = h * K + ch * CW + tt * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rr = mb + 4 * (lane >> 4) + e;
+        float sum = 0.f;
+        sum += a0[e];
+        sum += a1[e];
+        const float v = sum + 0.f;
+        if (rr < p.M) p.qp[(long)rr * ((long)p.H * K) + col] = DT<T>::fromf(v);
+      }
+    }
+  }
+}
+
+// the fused cross query where it applies (16-bit, <= 64 rows, 64-wide heads, the lean LN table's widths,
+// the folded q_proj weights and W_kt fragment-major); false: the caller keeps xq → kq
+template <typename T>
+static bool launch_xqk(const void* A, bool a_fm, const void* Wq_fm, const float* u, const float* c, const void* Wk_fm,
+                       void* qp, int M, int H, int D, hipStream_t s) {
+  if constexpr (sizeof(T) != 2) {
+    return false;
+  } else {
+    if (M > 64 || H * 64 != D || !A || !Wq_fm || !u || !c || !Wk_fm || !qp) return false;
+    XqkArgs<T> p{reinterpret_cast<const T*>(A), reinterpret_cast<const T*>(Wq_fm), u, c,
+                 reinterpret_cast<const T*>(Wk_fm), reinterpret_cast<T*>(qp), M, H, D};
+    const dim3 grid(H * 8, (M + 15) / 16);
+#define WCB_XQK(k, nw, kpw)                                                                                \
+  if (D == k) {                                                                                            \
+    if (a_fm) WCB_LAUNCH((dec_xqk_kernel<T, 1, nw, kpw, 8, true>), grid, dim3(nw * 64), 0, s, p);          \
+    else WCB_LAUNCH((dec_xqk_kernel<T, 1, nw, kpw, 8, false>), grid, dim3(nw * 64), 0, s, p);              \
+    return true;                                                                                           \
+  }
+    WCB_XQK(512, 4, 4) WCB_XQK(768, 4, 6) WCB_XQK(1024, 4, 8) WCB_XQK(1280, 8, 5)
+#undef WCB_XQK
+    return false;
+  }
+}
+
 // the lean form where it applies (16-bit, <= 64 rows, single-tile decode projections); false: the
 // caller takes gemm_dec_kernel. Same (waves, k-steps) table as launch_dec_mf: bit-identical outputs.
 template <typename T>
@@ -2269,6 +2420,13 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
     // decode GEMM (K in its table; else the older skinny kernel below): 16-row workgroups up to 64
     // rows (measured C2: 1.074 vs 1.147 ms/token with 32-row workgroups); the LM head walks the
     // vocabulary persistently with 32-row workgroups, reading every weight tile once
+    if (g.xqk_wk) {   // the fused cross query: the runtime sets it only where dec_xqk_kernel covers the launch
+      if (launch_xqk<T>(g.ln_a16, g.a_fm != 0, g.ln_wg_fm, g.ln_u, g.ln_c, g.xqk_wk, g.xqk_out, g.M, g.hs_H, g.K, s)) return;
+      throw std::runtime_error("internal error: fused cross query on a launch dec_xqk_kernel does not cover (M " +
+                               std::to_string(g.M) + ", H " + std::to_string(g.hs_H) + ", K " + std::to_string(g.K) +
+                               ", operands " + std::to_string(!!g.ln_a16) + std::to_string(!!g.ln_wg_fm) +
+                               std::to_string(!!g.ln_u) + std::to_string(!!g.ln_c) + std::to_string(!!g.xqk_out) + ")");
+    }
     if (g.lean && launch_lean<T>(g, s)) return;
     if (g.kq_w) throw std::runtime_error("internal error: fused cross-query on a launch the lean kernel does not cover");
     if (g.a_fm || g.c_fm || g.out16_fm)   // the runtime pairs fragment-major operands only where the lean path takes both

@@ -223,6 +223,10 @@ struct wcb_handle {
   // audio-s/s (interleaved): the MFMAs start as soon as the rows land, the statistics ride the partial-tile
   // barrier — the in-kernel LayerNorm cost its launches ~1.1 µs each (xq 3.89 vs out 2.78 µs in-graph)
   int lean_fold = 1;
+  // greedy cross query: the q projection and q'_h = W_k,hᵀ q_h in one launch, each workgroup recomputing its
+  // head's q_h (gemm_impl.h dec_xqk_kernel; option "xqk"; needs lean_fold) instead of xq → kq: one launch
+  // boundary less per layer, no hand-off. C2 20,423 / 20,431 / 20,382 vs 20,243 / 20,295 / 20,097 (interleaved)
+  int xqk = 1;
   // beam top-K: each row's vocabulary in kBeamChunks chunks, one workgroup per (chunk, row) (option
   // "beam_chunks" 1) or one workgroup per row (0, default; k_beam.hip beam_select). Measured: C3 6,160 vs
   // 6,228, C5 2,517 vs 2,518 audio-s/s — the per-row kernel's 320 (80) long workgroups already run beside
@@ -678,6 +682,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       // the folded W·diag(γ) copies are built at finalize only when it is on
       REQUIRE(!h->ready, "option ln_fold selects weight layouts: set it before wcb_finalize_weights");
       h->ln_fold = value != 0;
+    } else if (n == "xqk") {
+      h->xqk = value != 0;
     } else if (n == "lean_fold") {
       REQUIRE(!h->ready, "option lean_fold selects weight layouts: set it before wcb_finalize_weights");
       h->lean_fold = value != 0;
@@ -1344,7 +1350,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       char* dqp = (char*)D.dqp.p + (size_t)r0 * H * d * e;
       GemmArgs xq = drow(x, d, w.xq_w, M, d, d, dq, d);
       xq.ln_w = w.lnx_w; xq.ln_b = w.lnx_b; xq.st_in = st; xq.st_nb = nbk; xq.ln_a16 = lna;
-      xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg; xq.W_fm = w.xq_fm;
+      xq.bias = w.xq_b; xq.ln_u = w.lnx_u; xq.ln_c = w.lnx_c; xq.ln_wg = w.xq_wg; xq.W_fm = w.xq_fm; xq.ln_wg_fm = w.xq_wgfm;
       if (x16fm) { xq.ln_a16 = x16fm; xq.a_fm = 1; }
       // q'_h = W_k,hᵀ q_h in the q_proj launch: the lean LN table's widths, both fragment-major copies
       const bool kqf = h->xq_kq && h->lean && fm_ok && w.xq_fm && w.xkt_fm && (d == 512 || d == 768 || d == 1024 || d == 1280);
@@ -1353,8 +1359,12 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
         xq.kq_cnt = D.kq_cnt.as<unsigned long long>() + ((size_t)l * DecCtx::kMaxSub + chain) * 4 * H;
         xq.kq_err = h->dev_err.as<int>();
       }
+      // q_h and q'_h in one launch without a hand-off (option xqk; the folded q_proj weights)
+      const bool xqk = !kqf && h->xqk && h->lean && fm_ok && h->lean_fold && w.xq_wgfm && w.xkt_fm && w.lnx_u &&
+                       H * 64 == d && (d == 512 || d == 768 || d == 1024 || d == 1280);
+      if (xqk) { xq.xqk_wk = w.xkt_fm; xq.xqk_out = dqp; xq.hs_H = H; }
       proj("dec_xq", xq);
-      if (!kqf) {
+      if (!kqf && !xqk) {
         GemmArgs kq = drow(dq, d, w.xkt_w, M, H * d, 64, dqp, (long)H * d);
         kq.a_grp_n = d; kq.a_grp_off = 64; kq.W_fm = w.xkt_fm;
         proj("dec_kq", kq);
