@@ -290,6 +290,21 @@ def test_fused_cross_query_is_bit_identical(dtype):
         np.testing.assert_array_equal(out[0], out[1])
 
 
+def test_merge_output_split_is_bit_identical():
+    """Option merge_os 2 (xenc_merge_v_kernel OS: a head's 64 W_v outputs over two workgroups of 4 rows) runs
+    the same range merge and MFMA sequence per output as merge_os 1: identical ids on the diverse recipe,
+    32 and 13 rows, 1000-phrase boost."""
+    dims = get_dims("small")
+    sd = make_weights(dims, seed=0, recipe="diverse")
+    phrases = synth_bias_list(1000, eot=dims.eos_token_id)
+    models = [WhisperCB.from_state_dict(dims, sd, dtype="bf16", options=o) for o in ({"merge_os": 2}, {"merge_os": 1})]
+    kw = dict(max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0)
+    for B in (32, 13):
+        x = torch.from_numpy(W.log_mel(synth_batch(B, start=5), dims.n_mel))
+        out = [m.generate(x, **kw).cpu().numpy() for m in models]
+        np.testing.assert_array_equal(out[0], out[1])
+
+
 def test_bias_from_another_handle_is_rejected():
     """A bias automaton belongs to the handle that built it (its decode graphs are keyed on it): passing
     it to another handle is an argument error, not a silently wrong boost."""

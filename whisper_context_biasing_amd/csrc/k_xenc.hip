@@ -501,23 +501,29 @@ __global__ __launch_bounds__(256) void xenc_merge_kernel(XencArgs a, T* u, long 
 // (u is exactly representable in T, so the B operand is u itself). Every weight load is issued before
 // the partials (they do not depend on them). The MFMA form replaced VALU dot products (r04 probe: 7.6k
 // cycles of the launch): 7.55 -> 7.08 us per C2 launch in the bench's serialised pass.
-template <typename T, int D, int MS, int RPW, bool P16 = false>
+// OS (output splits): the head's 64 outputs over OS workgroups (OS = 2: waves 0-1 own the 32 outputs of
+// this workgroup, waves 2-3 help with the range merge only): each workgroup reads W_v,h / OS, so twice the
+// rows (RPW) per workgroup keep the grid while the weight bytes per workgroup halve. Same arithmetic per output.
+template <typename T, int D, int MS, int RPW, bool P16 = false, int OS = 1>
 __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* wv, const T* wfm, const float* bv, T* out, long ldo) {
   using Frag = typename DT<T>::frag;
   constexpr int KS = D / 32;
   static_assert(D <= 1024 && D % 32 == 0, "one 4-column group per thread");
   static_assert(RPW <= 16, "the rows are the B columns of one MFMA");
-  const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  static_assert(OS == 1 || OS == 2, "output splits");
+  const int h = blockIdx.x / OS, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int otile = (blockIdx.x % OS) * (4 / OS) + wave;   // this wave's 16-output tile of the head
+  const bool owner = wave < 4 / OS;
   const int ns = a.nsplit;
   __shared__ float2 sv[RPW][MS];
   __shared__ __attribute__((aligned(16))) float us[RPW][D];
   MPROBE(0);
-  // W_v,h rows 16·wave + (lane & 15), k = 32·ks + 8·(lane >> 4): the A fragments of the wave's outputs
-  // (fragment-major copy when given: tile h·4 + wave, 1 KiB contiguous per wave-instruction; the same values)
+  // W_v,h rows 16·otile + (lane & 15), k = 32·ks + 8·(lane >> 4): the A fragments of the wave's outputs
+  // (fragment-major copy when given: tile h·4 + otile, 1 KiB contiguous per wave-instruction; the same values)
   Frag wf[KS];
-  {
-    const T* wr = wfm ? wfm + ((long)(h * 4 + wave) * KS * 64 + lane) * 8
-                      : wv + (long)(h * 64 + 16 * wave + (lane & 15)) * D + 8 * (lane >> 4);
+  if (owner) {
+    const T* wr = wfm ? wfm + ((long)(h * 4 + otile) * KS * 64 + lane) * 8
+                      : wv + (long)(h * 64 + 16 * otile + (lane & 15)) * D + 8 * (lane >> 4);
     const int kstep = wfm ? 512 : 32;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) wf[ks] = load_frag<T>(wr + ks * kstep);
@@ -581,6 +587,7 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
   }
   __syncthreads();
   MPROBE(3);
+  if (!owner) return;
   // B: column lane & 15 = row r of this workgroup (zero past RPW), k = 32·ks + 8·(lane >> 4)
   const int r = lane & 15;
   f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -598,10 +605,10 @@ __global__ __launch_bounds__(256) void xenc_merge_v_kernel(XencArgs a, const T* 
     }
     o = mma16(wf[ks], uf, o);
   }
-  // C: lane holds outputs 16·wave + 4·(lane >> 4) + e of row lane & 15
+  // C: lane holds outputs 16·otile + 4·(lane >> 4) + e of row lane & 15
   const int b = blockIdx.y * RPW + r;
   if (r < RPW && b < a.rows) {
-    const int n = h * 64 + 16 * wave + 4 * (lane >> 4);
+    const int n = h * 64 + 16 * otile + 4 * (lane >> 4);
     const f32x4 b4 = *reinterpret_cast<const f32x4*>(bv + n);
     typedef short s4 __attribute__((ext_vector_type(4)));
     s4 hv;
@@ -757,9 +764,11 @@ static void launch_merge_v_t(const XencArgs& a, const void* wv, const void* wfm,
   // slower); MS: the partial loads per thread (the key-range count rounded up to 8 or 16; ranges past
   // nsplit carry weight 0)
   const dim3 grid(a.H, (a.rows + 1) / 2);
+  const dim3 grid2(a.H * 2, (a.rows + 3) / 4);   // merge_os 2: the head's outputs over two workgroups, 4 rows each
 #define WCB_XC(DD)                                                                                                    \
   case DD:                                                                                                            \
-    if (a.part16 && a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8, 2, true>), grid, dim3(256), 0, s, a, (const T*)wv, (const T*)wfm, bv, (T*)o, ldo); \
+    if (a.merge_os == 2 && a.part16 && a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8, 4, true, 2>), grid2, dim3(256), 0, s, a, (const T*)wv, (const T*)wfm, bv, (T*)o, ldo); \
+    else if (a.part16 && a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8, 2, true>), grid, dim3(256), 0, s, a, (const T*)wv, (const T*)wfm, bv, (T*)o, ldo); \
     else if (a.part16) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, kXencMaxSplit, 2, true>), grid, dim3(256), 0, s, a, (const T*)wv, (const T*)wfm, bv, (T*)o, ldo); \
     else if (a.nsplit <= 8) WCB_LAUNCH((xenc_merge_v_kernel<T, DD, 8, 2>), grid, dim3(256), 0, s, a, (const T*)wv, (const T*)wfm, bv, (T*)o, ldo); \
     else WCB_LAUNCH((xenc_merge_v_kernel<T, DD, kXencMaxSplit, 2>), grid, dim3(256), 0, s, a, (const T*)wv, (const T*)wfm, bv, (T*)o, ldo);   \

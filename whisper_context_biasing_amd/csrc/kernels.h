@@ -201,6 +201,7 @@ struct XencArgs {
   // range partials in the model dtype, each normalised by its own Σ p (part then holds [rows][nsplit][H][D]
   // T values: half the bytes), the (max, Σ p) pairs in f32 as before. fm variants + xenc_merge_v only
   int part16 = 0;
+  int merge_os = 1;          // xenc_merge_v_kernel: a head's 64 outputs over merge_os workgroups (1 or 2)
 };
 bool xenc_supported(DType t, int D);
 // enc [B][S][D] → the fragment-major chunk layout of the register-ring kernel (xenc_fm_elems(B, S, D)

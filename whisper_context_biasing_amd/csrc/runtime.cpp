@@ -227,6 +227,9 @@ struct wcb_handle {
   // head's q_h (gemm_impl.h dec_xqk_kernel; option "xqk"; needs lean_fold) instead of xq → kq: one launch
   // boundary less per layer, no hand-off. C2 20,423 / 20,431 / 20,382 vs 20,243 / 20,295 / 20,097 (interleaved)
   int xqk = 1;
+  // greedy range merge + W_v (16-bit partials): a head's 64 outputs over 1 or 2 workgroups (option "merge_os";
+  // 2 measured slower: C2 20,114 / 20,074 / 20,080 vs 20,325 / 20,343 / 20,300, interleaved)
+  int merge_os = 1;
   // beam top-K: each row's vocabulary in kBeamChunks chunks, one workgroup per (chunk, row) (option
   // "beam_chunks" 1) or one workgroup per row (0, default; k_beam.hip beam_select). Measured: C3 6,160 vs
   // 6,228, C5 2,517 vs 2,518 audio-s/s — the per-row kernel's 320 (80) long workgroups already run beside
@@ -682,6 +685,9 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       // the folded W·diag(γ) copies are built at finalize only when it is on
       REQUIRE(!h->ready, "option ln_fold selects weight layouts: set it before wcb_finalize_weights");
       h->ln_fold = value != 0;
+    } else if (n == "merge_os") {
+      REQUIRE(value == 1 || value == 2, "option merge_os: 1 or 2");
+      h->merge_os = value;
     } else if (n == "xqk") {
       h->xqk = value != 0;
     } else if (n == "lean_fold") {
@@ -1379,6 +1385,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       xa.ml = D.xml.as<float>() + (size_t)r0 * h->xenc_split * H * 2;
       const bool fused_merge = h->merge_v && d % 128 == 0;
       xa.part16 = h->xpart16 && xa.fm && fused_merge;
+      xa.merge_os = h->merge_os;
       if (h->prof_stamps) {
         xa.stamp.base = h->stamp_base(c.buf, 0);
         xa.stamp.pos = pos;
