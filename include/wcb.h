@@ -98,6 +98,8 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "xqk" 0/1          greedy cross query (encoder space, lean, folded): q_h and q'_h = W_k,hᵀ q_h in one launch
  *                      with no hand-off, each workgroup recomputing its head's q_h (1, default) or the xq → kq
  *                      launches (0)
+ *   "lm_walkers" n     greedy LM head: column walkers per row block = argmax partials per row (128, 192, 256
+ *                      (default), 384, 512, 1024; before finalize); the selected ids do not depend on it
  *   "merge_os" 1/2     greedy range merge + W_v: a head's 64 outputs in one workgroup of 2 rows (1, default) or
  *                      over two workgroups of 4 rows (2); bit-identical
  *   "beam_chunks" 0/1  beam top-K over 16 vocabulary chunks per row, one workgroup each (1) or one workgroup

@@ -480,7 +480,7 @@ ALT_OPTIONS = [{"merge_v": 0}, {"enc_gemm": 1}, {"enc_gemm": 0}, {"xenc_split": 
                {"xenc_variant": 3}, {"decode_contexts": 1}, {"enc_flash": 2}, {"flash_split": 1},
                {"beam_xattn": 1}, {"beam_xattn": 2}, {"ring_kt": 1}, {"lean": 0, "lean_x": 0}, {"beam_wide": 0},
                {"beam_wfm": 1}, {"beam_raster": 8}, {"beam_chunks": 1},
-               {"lean_fold": 0}, {"xqk": 0}]
+               {"lean_fold": 0}, {"xqk": 0}, {"lm_walkers": 512}]
 
 
 @pytest.mark.parametrize("opts", ALT_OPTIONS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))

@@ -2269,7 +2269,7 @@ static void launch_dec_k(const GemmArgs& g, hipStream_t s) {
   if (!g.sel_val && (AM == 3 || ntile * gy <= 1024)) {
     WCB_LAUNCH((gemm_dec_kernel<T, MF, NW, KPW, AM, false>), dim3(ntile, gy), dim3(NW * 64), 0, s, g);
   } else {   // the LM head: kDecWalkers column walkers per row block (= argmax partials per row)
-    const int gx = std::min(ntile, kDecWalkers);
+    const int gx = std::min(ntile, g.walkers > 0 ? g.walkers : kDecWalkers);
     int nw = 0, kpw = 0;
     if constexpr (sizeof(T) == 2 && AM != 3) {
       // the copy's split matches; it covers whole 16-column tiles (the LM head's rows are padded with zeros)

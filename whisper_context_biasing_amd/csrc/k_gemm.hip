@@ -13,8 +13,8 @@ bool gemm_dec_supported(DType t, int K) {
   return K == 64 || K == 128 || K == 256 || K == 384 || K == 512 || K == 768 || K == 1024 || K == 1280;
 }
 
-int lm_head_partials(DType t, int K, int vocab) {
-  return gemm_dec_supported(t, K) ? std::min((vocab + 15) / 16, kDecWalkers) : (vocab + 63) / 64;
+int lm_head_partials(DType t, int K, int vocab, int walkers) {
+  return gemm_dec_supported(t, K) ? std::min((vocab + 15) / 16, walkers) : (vocab + 63) / 64;
 }
 
 void gemm(DType t, const GemmArgs& g, hipStream_t s) {

@@ -72,6 +72,7 @@ struct GemmArgs {
   int skinny = 0;                  // decode projection: the skinny kernel whatever M (row blocks over grid.y)
   int ring_kt = 1;                 // tile 2: 64-deep K sub-tiles per LDS-ring stage (1 or 2)
   int wide = 0;                    // tile 2, K = d_model: gemm_wide_kernel tile config 10·FM + FN (0: ring tiles)
+  int walkers = 0;                 // LM head column walkers per row block (0: kDecWalkers)
   // decode GEMM (gemm_dec_kernel): a T-typed copy of the f32 rows the epilogue writes (the
   // residual stream x → x16, read back as the LN-fused A operand of the next projection), and the
   // LN-fused A read from such a copy instead of the f32 rows (lda elements per row)
@@ -147,7 +148,7 @@ void add_i32(int* p, int v, hipStream_t s);   // *p += v (one thread)
 // per row block and writes one partial per walker; the older skinny kernel one per 64 columns.
 constexpr int kDecWalkers = 512;
 bool gemm_dec_supported(DType t, int K);
-int lm_head_partials(DType t, int K, int vocab);
+int lm_head_partials(DType t, int K, int vocab, int walkers = kDecWalkers);
 
 // Attention over heads of 64. q row for (b, i): q + (b·q_Sb + i)·ldq + h·64.
 // key j of (b, h): k + b·k_sb + h·k_sh + j·k_sk (same strides for v).

@@ -230,6 +230,11 @@ struct wcb_handle {
   // greedy range merge + W_v (16-bit partials): a head's 64 outputs over 1 or 2 workgroups (option "merge_os";
   // 2 measured slower: C2 20,114 / 20,074 / 20,080 vs 20,325 / 20,343 / 20,300, interleaved)
   int merge_os = 1;
+  // greedy LM head: column walkers per row block (option "lm_walkers", before finalize; = the argmax
+  // partials per row select_finalize reduces). C2 (interleaved pairs): 256 walkers 20,464-20,644 vs 512
+  // 20,353-20,395 audio-s/s; 128 and 1024 no better than 512, 384 equal to 256 — fewer walkers re-read and
+  // re-normalise the rows fewer times, and the walk of ~13 tiles each still hides its weight stream
+  int lm_walkers = 256;
   // beam top-K: each row's vocabulary in kBeamChunks chunks, one workgroup per (chunk, row) (option
   // "beam_chunks" 1) or one workgroup per row (0, default; k_beam.hip beam_select). Measured: C3 6,160 vs
   // 6,228, C5 2,517 vs 2,518 audio-s/s — the per-row kernel's 320 (80) long workgroups already run beside
@@ -685,6 +690,11 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       // the folded W·diag(γ) copies are built at finalize only when it is on
       REQUIRE(!h->ready, "option ln_fold selects weight layouts: set it before wcb_finalize_weights");
       h->ln_fold = value != 0;
+    } else if (n == "lm_walkers") {
+      REQUIRE(!h->ready, "option lm_walkers sizes the argmax partials: set it before wcb_finalize_weights");
+      REQUIRE(value == 128 || value == 192 || value == 256 || value == 384 || value == 512 || value == 1024,
+              "option lm_walkers: 128, 192, 256, 384, 512 or 1024");
+      h->lm_walkers = value;
     } else if (n == "merge_os") {
       REQUIRE(value == 1 || value == 2, "option merge_os: 1 or 2");
       h->merge_os = value;
@@ -1166,7 +1176,7 @@ void ensure_dec_ws(wcb_handle* h, int clips, int B, int T, int out_ld, int xmode
     D.kq_cnt.ensure((size_t)L * DecCtx::kMaxSub * 4 * h->H() * 8);   // zeroed on allocation, monotonic
     D.pids.ensure((size_t)rows * 4);
     D.logits.ensure((size_t)B * h->vocab_pad * 4);
-    D.nchunk = lm_head_partials(h->dt, (int)d, h->d.vocab);   // argmax partials per row of the LM head
+    D.nchunk = lm_head_partials(h->dt, (int)d, h->d.vocab, h->lm_walkers);   // argmax partials per row of the LM head
     D.part_val.ensure((size_t)B * D.nchunk * 4);
     D.part_idx.ensure((size_t)B * D.nchunk * 4);
     D.ints.ensure(need[5]);
@@ -1478,6 +1488,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     if (h->lean && !tiled && rps == 1 && h->lm_ln_split) lm.ln_scratch = dh;   // the final LayerNorm in a launch of its own
     lm.out_f32 = 1;
     if (c.select && !c.beam) {   // argmax partials with the root boost + EOS mask fused into the LM head
+      lm.walkers = h->lm_walkers;
       lm.sel_val = D.part_val.as<float>() + (size_t)b0 * D.nchunk;
       lm.sel_idx = D.part_idx.as<int>() + (size_t)b0 * D.nchunk;
       lm.sel_root_bits = c.bias->root_bits.as<uint32_t>(); lm.sel_lam = c.lam;
