@@ -110,7 +110,8 @@ const char* wcb_last_error(const wcb_handle* h);
  *                      0: row-major); bit-identical
  *   "enc_gemm" v       encoder GEMM kernels: 4 (default) the ping-pong kernel, 256- or 192-wide tiles by the
  *                      fewer tile rounds; 1 the LDS-ring kernel's 256x192 tiles where 192-wide wins; 0 the
- *                      LDS-ring kernel everywhere
+ *                      LDS-ring kernel everywhere; 5 the ping-pong kernel's 192-wide tiles wherever N allows
+ *                      (162 VGPRs: room on a CU for a decode workgroup beside it; measured 1 % slower)
  * While a step-wise decode is open (wcb_decode_begin .. wcb_decode_end) only decode_contexts, enc_flash,
  * enc_gemm, enc_raster and steps_per_graph may change: the others shape the state it carries between steps. */
 int wcb_set_option(wcb_handle* h, const char* name, int value);

@@ -671,7 +671,7 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "xq_kq") {
       h->xq_kq = value != 0;
     } else if (n == "enc_gemm") {
-      REQUIRE(value == 0 || value == 1 || value == 4, "option enc_gemm: 0, 1 or 4");
+      REQUIRE(value == 0 || value == 1 || value == 4 || value == 5, "option enc_gemm: 0, 1, 4 or 5");
       h->enc_gemm = value;
     } else if (n == "enc_raster") {
       REQUIRE(value >= 0 && value <= 64, "option enc_raster: 0..64");
