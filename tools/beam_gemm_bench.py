@@ -16,8 +16,10 @@ from whisper_context_biasing_amd import _lib  # noqa: E402
 lib = _lib.load()
 
 SHAPES = {
-    "c3": [("qkv", 320, 3072, 1024, 0, False), ("out", 320, 1024, 1024, 0, True), ("fc1", 320, 4096, 1024, 1, False)],
-    "c5": [("qkv", 80, 3840, 1280, 0, False), ("out", 80, 1280, 1280, 0, True), ("fc1", 80, 5120, 1280, 1, False)],
+    "c3": [("qkv", 320, 3072, 1024, 0, False), ("out", 320, 1024, 1024, 0, True), ("fc1", 320, 4096, 1024, 1, False),
+           ("fc2", 320, 1024, 4096, 0, True)],
+    "c5": [("qkv", 80, 3840, 1280, 0, False), ("out", 80, 1280, 1280, 0, True), ("fc1", 80, 5120, 1280, 1, False),
+           ("fc2", 80, 1280, 5120, 0, True)],
 }
 
 
@@ -89,10 +91,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="7,6,107,106,112,122")
     ap.add_argument("--shapes", default="c3,c5")
+    ap.add_argument("--only", default="", help="comma-separated projection names (default: all)")
     args = ap.parse_args()
     cfgs = [int(c) for c in args.configs.split(",")]
     for sh in args.shapes.split(","):
         for name, M, N, K, act, resid in SHAPES[sh]:
+            if args.only and name not in args.only.split(","):
+                continue
             copies = max(8, int(1.2e9 / (N * K * 2)))   # > 1 GB of weights per replay
             line = f"{sh} {name:4s} M={M:4d} N={N:5d} K={K:5d}:"
             for c in cfgs:
