@@ -431,18 +431,20 @@ def test_decode_attention_variants(dt, variant, Sk, split):
         assert torch.equal(o, o6)
 
 
+@pytest.mark.parametrize("mel_split", [0, 1])
 @pytest.mark.parametrize("n_mel", [80, 128])
-def test_log_mel_matches_reference_golden(n_mel):
+def test_log_mel_matches_reference_golden(n_mel, mel_split):
     """The GPU front end against the reference's own feature extractor outputs (tests/golden/mel_golden.npz,
     WhisperFeatureExtractor run by make_golden.py): the same bar the numpy oracle meets (2e-5 on the
-    golden slices; HF quotes 1e-5 between its CPU and GPU paths), plus the global statistics."""
+    golden slices; HF quotes 1e-5 between its CPU and GPU paths), plus the global statistics — for the f32
+    MFMA DFT and the split-bf16 one (option mel_split)."""
     import os
     MEL_COLS = [slice(0, 48), slice(1476, 1524), slice(2952, 3000)]   # as tests/test_oracle_golden.py
     from whisper_context_biasing_amd.config import get_dims
     from whisper_context_biasing_amd.model import WhisperCB
     from whisper_context_biasing_amd.synth import synth_clip
     gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "mel_golden.npz"))
-    m = WhisperCB(get_dims("large-v3" if n_mel == 128 else "micro"), dtype="f32")
+    m = WhisperCB(get_dims("large-v3" if n_mel == 128 else "micro"), dtype="f32", options={"mel_split": mel_split})
     for clip in range(4):
         pcm = synth_clip(clip, n_samples=5 * 16000) if clip == 2 else synth_clip(clip)
         if clip == 3:

@@ -28,8 +28,14 @@ WCB_DEV unsigned ord_enc(float f) {
 }
 WCB_DEV float ord_dec(unsigned u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u); }
 
+// SPLIT: the DFT products as bf16 MFMAs of 3-part splits of both operands (x = xh + xm + xl, t = th + tm +
+// tl, each part the RNE bf16 of the remainder): x·t = xh·th + xh·tm + xm·th + xh·tl + xl·th + xm·tm + O(2^-24)
+// (the six 16x16x32 bf16 MFMAs of a 32-deep k-step cost ~1/5 of the eight 16x16x4 f32 ones); not
+// bit-identical to the f32 form, ~f32 accurate.
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void logmel_power_mel_kernel(const float* __restrict__ pcm, long pcm_stride, int n_valid,
-                                                               const float* __restrict__ dft, const int* __restrict__ mel_lo,
+                                                               const float* __restrict__ dft, const uint16_t* __restrict__ dft3,
+                                                               const int* __restrict__ mel_lo,
                                                                const int* __restrict__ mel_hi, const float* __restrict__ mel_w,
                                                                int n_mel, float* __restrict__ out, unsigned* __restrict__ clip_max) {
   constexpr int kPowLd = kBins + 3;
@@ -62,6 +68,45 @@ __global__ __launch_bounds__(256) void logmel_power_mel_kernel(const float* __re
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < kCW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (SPLIT) {
+    constexpr long kPart = (long)kNCol * kNCol;
+    const uint16_t* brow = dft3 + (long)(cf0 * 16 + (lane & 15)) * kNCol + 8 * (lane >> 4);
+    for (int kb = 0; kb < kNCol; kb += 32) {
+      s16x8 ah[4], am[4], al[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float* arow = lds + (i * 16 + (lane & 15)) * kHop + 8 * (lane >> 4) + kb;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = arow[e];
+          const bf16_t h = f_to_bf16(v);
+          const float r1 = v - bf16_to_f(h);
+          const bf16_t m = f_to_bf16(r1);
+          const bf16_t l = f_to_bf16(r1 - bf16_to_f(m));
+          ah[i][e] = (short)h; am[i][e] = (short)m; al[i][e] = (short)l;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kCW; ++j) {
+        if (j < ncf) {
+          const uint16_t* bp = brow + (long)j * 16 * kNCol + kb;
+          const s16x8 bh = *reinterpret_cast<const s16x8*>(bp);
+          const s16x8 bm = *reinterpret_cast<const s16x8*>(bp + kPart);
+          const s16x8 bl = *reinterpret_cast<const s16x8*>(bp + 2 * kPart);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {   // small terms first
+            f32x4 c = acc[i][j];
+            c = mma16(am[i], bm, c);
+            c = mma16(al[i], bh, c);
+            c = mma16(ah[i], bl, c);
+            c = mma16(am[i], bh, c);
+            c = mma16(ah[i], bm, c);
+            acc[i][j] = mma16(ah[i], bh, c);
+          }
+        }
+      }
+    }
+  } else {
   const float* brow = dft + (long)(cf0 * 16 + (lane & 15)) * kNCol + 8 * (lane >> 4);
   for (int kb = 0; kb < kNCol; kb += 32) {
     f32x8 a[4];
@@ -79,6 +124,7 @@ __global__ __launch_bounds__(256) void logmel_power_mel_kernel(const float* __re
         for (int i = 0; i < 4; ++i) acc[i][j] = mma16(a[i], bf, acc[i][j]);
       }
     }
+  }
   }
   __syncthreads();   // samples no longer needed: reuse LDS for the power spectrum
   // acc[i][j][e]: frame row 16i + (lane>>4)*4 + e, column 16(cf0 + j) + (lane&15): even = re, odd = im
@@ -120,12 +166,17 @@ __global__ void logmel_normalize_kernel(float* mel, const unsigned* clip_max, in
   }
 }
 
-void logmel_power_mel(const float* pcm, long pcm_stride, int n_samples, int B, const float* dft, const int* mel_lo,
-                      const int* mel_hi, const float* mel_w, int n_mel, float* mel_out, unsigned* clip_max,
-                      hipStream_t s) {
+void logmel_power_mel(const float* pcm, long pcm_stride, int n_samples, int B, const float* dft, const void* dft3,
+                      const int* mel_lo, const int* mel_hi, const float* mel_w, int n_mel, float* mel_out,
+                      unsigned* clip_max, hipStream_t s) {
   (void)hipMemsetAsync(clip_max, 0, sizeof(unsigned) * B, s);
-  WCB_LAUNCH(logmel_power_mel_kernel, dim3((kFrames + kFPB - 1) / kFPB, B), dim3(256), 0, s, pcm, pcm_stride,
-                     n_samples, dft, mel_lo, mel_hi, mel_w, n_mel, mel_out, clip_max);
+  const dim3 grid((kFrames + kFPB - 1) / kFPB, B);
+  if (dft3)
+    WCB_LAUNCH(logmel_power_mel_kernel<true>, grid, dim3(256), 0, s, pcm, pcm_stride, n_samples, dft,
+               reinterpret_cast<const uint16_t*>(dft3), mel_lo, mel_hi, mel_w, n_mel, mel_out, clip_max);
+  else
+    WCB_LAUNCH(logmel_power_mel_kernel<false>, grid, dim3(256), 0, s, pcm, pcm_stride, n_samples, dft,
+               nullptr, mel_lo, mel_hi, mel_w, n_mel, mel_out, clip_max);
 }
 
 void logmel_normalize(float* mel, const unsigned* clip_max, int B, int n_mel, hipStream_t s) {

@@ -219,7 +219,8 @@ void xenc_merge_v(DType t, const XencArgs& a, const void* wv, const float* bv, v
                   const void* wv_fm = nullptr);
 
 // log-mel front end
-void logmel_power_mel(const float* pcm, long pcm_stride, int n_samples, int B, const float* dft,
+// dft3 (nullable): the table as three bf16 parts [3][416][416] — the DFT as split-bf16 MFMAs instead of f32
+void logmel_power_mel(const float* pcm, long pcm_stride, int n_samples, int B, const float* dft, const void* dft3,
                       const int* mel_lo, const int* mel_hi, const float* mel_w, int n_mel,
                       float* mel_out, unsigned* clip_max, hipStream_t s);
 void logmel_normalize(float* mel, const unsigned* clip_max, int B, int n_mel, hipStream_t s);

@@ -235,6 +235,9 @@ struct wcb_handle {
   // 20,353-20,395 audio-s/s; 128 and 1024 no better than 512, 384 equal to 256 — fewer walkers re-read and
   // re-normalise the rows fewer times, and the walk of ~13 tiles each still hides its weight stream
   int lm_walkers = 256;
+  // log-mel DFT: the f32 products as six bf16 MFMA products of 3-part splits (hi, mid, lo; the dropped terms
+  // below 2^-24 relative) instead of f32 MFMAs (option "mel_split")
+  int mel_split = 0;
   // beam top-K: each row's vocabulary in kBeamChunks chunks, one workgroup per (chunk, row) (option
   // "beam_chunks" 1) or one workgroup per row (0, default; k_beam.hip beam_select). Measured: C3 6,160 vs
   // 6,228, C5 2,517 vs 2,518 audio-s/s — the per-row kernel's 320 (80) long workgroups already run beside
@@ -308,7 +311,7 @@ struct wcb_handle {
   void *tok_emb = nullptr, *dec_pos = nullptr;
   void* tok_emb_fm = nullptr;   // 16-bit: fragment-major copy of tok_emb for the greedy LM head
   // mel tables
-  DevBuf dft, mel_lo, mel_hi, mel_w, clip_max;
+  DevBuf dft, dft3, mel_lo, mel_hi, mel_w, clip_max;
   // encoder workspace
   int enc_B = 0;
   DevBuf xt, hbuf, x, h, qkv, att, ffn, encout;
@@ -527,6 +530,36 @@ int wcb_create(const wcb_model_desc* desc, int device, wcb_handle** out) {
     }
     h->dft.ensure(dft.size() * 4);
     HIPCHK(hipMemcpy(h->dft.p, dft.data(), dft.size() * 4, hipMemcpyHostToDevice));
+    {   // the same table as three bf16 parts (hi, mid, lo: each the RNE bf16 of the remainder of the double
+        // value): the split-bf16 DFT (k_logmel.hip SPLIT) multiplies with these
+      auto bf = [](double v, double& back) -> uint16_t {
+        const float f = (float)v;
+        uint32_t u;
+        std::memcpy(&u, &f, 4);
+        u += 0x7fffu + ((u >> 16) & 1u);   // round to nearest even (finite values only)
+        const uint16_t hbits = (uint16_t)(u >> 16);
+        const uint32_t w = (uint32_t)hbits << 16;
+        float g;
+        std::memcpy(&g, &w, 4);
+        back = g;
+        return hbits;
+      };
+      std::vector<uint16_t> t3((size_t)3 * kNCol * kNCol, 0);
+      for (int c = 0; c < 402; ++c) {
+        const int bin = c >> 1;
+        for (int k = 0; k < 400; ++k) {
+          const double win = 0.5 - 0.5 * std::cos(2.0 * M_PI * k / 400.0);
+          const double ang = 2.0 * M_PI * (double)((long)bin * k % 400) / 400.0;
+          double r = win * ((c & 1) ? -std::sin(ang) : std::cos(ang)), back;
+          for (int part = 0; part < 3; ++part) {
+            t3[(size_t)part * kNCol * kNCol + (size_t)c * kNCol + k] = bf(r, back);
+            r -= back;
+          }
+        }
+      }
+      h->dft3.ensure(t3.size() * 2);
+      HIPCHK(hipMemcpy(h->dft3.p, t3.data(), t3.size() * 2, hipMemcpyHostToDevice));
+    }
     const auto fb = mel_filters(desc->n_mel);
     std::vector<int> lo(desc->n_mel), hi(desc->n_mel);
     std::vector<float> w((size_t)desc->n_mel * 32, 0.f);
@@ -589,7 +622,7 @@ void wcb_destroy(wcb_handle* h) {
     if (D.hs) (void)hipStreamDestroy(D.hs);
   }
   for (auto& b : h->owned) b.release();
-  for (DevBuf* b : {&h->dft, &h->mel_lo, &h->mel_hi, &h->mel_w, &h->clip_max, &h->xt, &h->hbuf, &h->x, &h->h,
+  for (DevBuf* b : {&h->dft, &h->dft3, &h->mel_lo, &h->mel_hi, &h->mel_w, &h->clip_max, &h->xt, &h->hbuf, &h->x, &h->h,
                     &h->qkv, &h->att, &h->ffn, &h->encout, &h->stamps, &h->stamp_acc, &h->dev_err})
     b->release();
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
@@ -690,6 +723,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       // the folded W·diag(γ) copies are built at finalize only when it is on
       REQUIRE(!h->ready, "option ln_fold selects weight layouts: set it before wcb_finalize_weights");
       h->ln_fold = value != 0;
+    } else if (n == "mel_split") {
+      h->mel_split = value != 0;
     } else if (n == "lm_walkers") {
       REQUIRE(!h->ready, "option lm_walkers sizes the argmax partials: set it before wcb_finalize_weights");
       REQUIRE(value == 128 || value == 192 || value == 256 || value == 384 || value == 512 || value == 1024,
@@ -1666,7 +1701,8 @@ int wcb_log_mel(wcb_handle* h, const float* pcm, int B, int n_samples, int64_t p
     if ((size_t)B * 4 > h->clip_max.bytes) { quiesce(h); h->clip_max.ensure((size_t)std::max(B, h->enc_B) * 4); }
     sync_in(h, stream, h->he);
     h->timed("log_mel", 0, (double)B * (std::min(n_samples, kNSamp) * 4.0 + h->d.n_mel * kFrames * 4.0 * 3), h->he, [&] {
-      logmel_power_mel(pcm, (long)pcm_stride, n_samples, B, h->dft.as<float>(), h->mel_lo.as<int>(), h->mel_hi.as<int>(),
+      logmel_power_mel(pcm, (long)pcm_stride, n_samples, B, h->dft.as<float>(), h->mel_split ? h->dft3.p : nullptr,
+                       h->mel_lo.as<int>(), h->mel_hi.as<int>(),
                        h->mel_w.as<float>(), h->d.n_mel, mel_out, h->clip_max.as<unsigned>(), h->he);
       logmel_normalize(mel_out, h->clip_max.as<unsigned>(), B, h->d.n_mel, h->he);
     });
