@@ -61,6 +61,7 @@ __global__ __launch_bounds__(256) void logmel_power_mel_kernel(const float* __re
   // split, 16 frames x all 26 column fragments per wave, re-read the 692 KB table 4x as often). The K
   // order of every output element is unchanged: bit-identical.
   constexpr int kCF = 26, kCW = 7;                       // column fragments, per wave (at most)
+  static_assert(kCF == 2 * kCW + 2 * (kCW - 1) && kCF * 16 == kNCol, "the waves' column shares cover the table");
   const int cf0 = wave < 2 ? wave * kCW : 2 * kCW + (wave - 2) * (kCW - 1);
   const int ncf = wave < 2 ? kCW : kCW - 1;
   f32x4 acc[4][kCW];
