@@ -305,6 +305,20 @@ def test_merge_output_split_is_bit_identical():
         np.testing.assert_array_equal(out[0], out[1])
 
 
+def test_lean_32_row_workgroups_are_bit_identical():
+    """Option lean_mf2 (every lean projection on 32-row workgroups where the chain has > 16 rows) keeps each
+    row's K split, MFMA and sum order: identical ids to the default 16-row residual writers, 32 and 40 rows."""
+    dims = get_dims("small")
+    sd = make_weights(dims, seed=0, recipe="diverse")
+    phrases = synth_bias_list(1000, eot=dims.eos_token_id)
+    models = [WhisperCB.from_state_dict(dims, sd, dtype="bf16", options=o) for o in ({"lean_mf2": 1}, {"lean_mf2": 0})]
+    kw = dict(max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0)
+    for B in (32, 40):
+        x = torch.from_numpy(W.log_mel(synth_batch(B, start=7), dims.n_mel))
+        out = [m.generate(x, **kw).cpu().numpy() for m in models]
+        np.testing.assert_array_equal(out[0], out[1])
+
+
 def test_bias_from_another_handle_is_rejected():
     """A bias automaton belongs to the handle that built it (its decode graphs are keyed on it): passing
     it to another handle is an argument error, not a silently wrong boost."""

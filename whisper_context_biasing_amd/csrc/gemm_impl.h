@@ -1947,7 +1947,7 @@ static bool launch_lean(const GemmArgs& g, hipStream_t s) {
 // arithmetic
 #define WCB_LN(k, nw, kpw)                                                                          \
   if (g.K == k) {                                                                                   \
-    const bool mf2 = g.N >= 2048 && g.M > 16;                                                       \
+    const bool mf2 = (g.N >= 2048 || g.lean_mf2) && g.M > 16;                                       \
     if (fold) {                                                                                     \
       if (g.mode == 2 && mf2) launch_lean_k<T, 2, nw, kpw, true, 2, false, false, true>(g, s);      \
       else if (g.mode == 2) launch_lean_k<T, 1, nw, kpw, true, 2, false, false, true>(g, s);        \
@@ -1973,9 +1973,17 @@ static bool launch_lean(const GemmArgs& g, hipStream_t s) {
     // residual writers: x (f32, in place) += A·Wᵀ + b, and its 16-bit copy
     if (g.mode || g.act || !g.resid || g.resid != g.out || !g.out_f32 || !g.out16) return false;
 #define WCB_RS(k, nw, kpw) if (g.K == k) { launch_lean_k<T, 1, nw, kpw, false, 1, false, false>(g, s); return true; }
-    WCB_RS(512, 4, 4) WCB_RS(768, 4, 6) WCB_RS(1024, 4, 8) WCB_RS(1280, 8, 5) WCB_RS(2048, 8, 8) WCB_RS(3072, 8, 12)
+    // option lean_mf2: 32-row workgroups (each weight tile read once for 32 rows; same per-row arithmetic)
+#define WCB_RS2(k, nw, kpw)                                                                               \
+  if (g.K == k) {                                                                                         \
+    if (g.lean_mf2 && g.M > 16) launch_lean_k<T, 2, nw, kpw, false, 1, false, false>(g, s);               \
+    else launch_lean_k<T, 1, nw, kpw, false, 1, false, false>(g, s);                                      \
+    return true;                                                                                          \
+  }
+    WCB_RS2(512, 4, 4) WCB_RS2(768, 4, 6) WCB_RS2(1024, 4, 8) WCB_RS2(1280, 8, 5) WCB_RS2(2048, 8, 8) WCB_RS2(3072, 8, 12)
     WCB_RS(4096, 16, 8) WCB_RS(5120, 16, 10)
 #undef WCB_RS
+#undef WCB_RS2
     return false;
   }
 }

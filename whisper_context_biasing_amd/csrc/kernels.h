@@ -86,6 +86,7 @@ struct GemmArgs {
   const void* ln_wg = nullptr;     // W' = W·diag(γ) in the model dtype (becomes `W` when the fold is taken)
   const void* ln_wg_fm = nullptr;  // W' fragment-major (the wide beam-row tiles; becomes `W_fm` with the fold)
   int lean_fold = 0;               // lean LN-fused projections: the folded form (W' fragment-major, c, u)
+  int lean_mf2 = 0;                // lean projections: 32-row workgroups wherever M > 16 (default: N >= 2048 LN-fused)
   // greedy cross query (folded, lean): q'_h = W_k,hᵀ q_h in the same launch without a hand-off
   // (gemm_impl.h dec_xqk_kernel): W_kt fragment-major, q' rows [M][hs_H·K] (the q rows are not written)
   const void* xqk_wk = nullptr; void* xqk_out = nullptr;

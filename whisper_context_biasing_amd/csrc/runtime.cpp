@@ -238,6 +238,9 @@ struct wcb_handle {
   // log-mel DFT: the f32 products as six bf16 MFMA products of 3-part splits (hi, mid, lo; the dropped terms
   // below 2^-24 relative) instead of f32 MFMAs (option "mel_split")
   int mel_split = 0;
+  // lean projections on 32-row workgroups wherever the chain has > 16 rows (option "lean_mf2"; default:
+  // only the LN-fused N >= 2048 ones). Measured 2.7 % slower at C2 (19,803-19,948 vs 20,424-20,521)
+  int lean_mf2 = 0;
   // beam top-K: each row's vocabulary in kBeamChunks chunks, one workgroup per (chunk, row) (option
   // "beam_chunks" 1) or one workgroup per row (0, default; k_beam.hip beam_select). Measured: C3 6,160 vs
   // 6,228, C5 2,517 vs 2,518 audio-s/s — the per-row kernel's 320 (80) long workgroups already run beside
@@ -723,6 +726,8 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
       // the folded W·diag(γ) copies are built at finalize only when it is on
       REQUIRE(!h->ready, "option ln_fold selects weight layouts: set it before wcb_finalize_weights");
       h->ln_fold = value != 0;
+    } else if (n == "lean_mf2") {
+      h->lean_mf2 = value != 0;
     } else if (n == "mel_split") {
       h->mel_split = value != 0;
     } else if (n == "lm_walkers") {
@@ -1356,6 +1361,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
     } else {
       g.lean = h->lean;   // <= 64 rows: the lean single-tile kernel where it covers the launch
       g.lean_fold = h->lean_fold && g.ln_w && g.ln_wg_fm && g.ln_u && g.ln_c;
+      g.lean_mf2 = h->lean_mf2;
       const int region = h->prof_stamps ? lean_stamp_region(cls) : 0;
       if (region) {   // stamps pass: this launch's start / end inside the replayed graph
         lst.base = h->stamp_base(c.buf, region);
