@@ -98,6 +98,8 @@ const char* wcb_last_error(const wcb_handle* h);
  *   "xqk" 0/1          greedy cross query (encoder space, lean, folded): q_h and q'_h = W_k,hᵀ q_h in one launch
  *                      with no hand-off, each workgroup recomputing its head's q_h (1, default) or the xq → kq
  *                      launches (0)
+ *   "xqk_chunks" n     fused cross query: q' column chunks per head, each chunk's workgroup recomputing q_h (2, 4,
+ *                      8 (default), 16); bit-identical
  *   "lean_mf2" 0/1     <= 64 rows: every lean projection on 32-row workgroups where the chain has > 16 rows (1) or
  *                      only the LN-fused N >= 2048 ones (0, default); bit-identical
  *   "mel_split" 0/1    log-mel DFT as split-bf16 MFMAs (1) or exact-f32 MFMAs (0, default); both within 2e-5 of

@@ -282,12 +282,14 @@ def test_fused_cross_query_is_bit_identical(dtype):
     dims = get_dims("small")
     sd = make_weights(dims, seed=0, recipe="diverse")
     phrases = synth_bias_list(1000, eot=dims.eos_token_id)
-    models = [WhisperCB.from_state_dict(dims, sd, dtype=dtype, options=o) for o in ({"xqk": 1}, {"xqk": 0})]
+    models = [WhisperCB.from_state_dict(dims, sd, dtype=dtype, options=o)
+              for o in ({"xqk": 1}, {"xqk": 0}, {"xqk": 1, "xqk_chunks": 2}, {"xqk": 1, "xqk_chunks": 16})]
     kw = dict(max_length=24, min_new_tokens=24, bias_list=phrases, bias_boost=2.0)
     for B in (32, 13, 40):
         x = torch.from_numpy(W.log_mel(synth_batch(B, start=3), dims.n_mel))
         out = [m.generate(x, **kw).cpu().numpy() for m in models]
-        np.testing.assert_array_equal(out[0], out[1])
+        for o in out[1:]:
+            np.testing.assert_array_equal(out[0], o)
 
 
 def test_merge_output_split_is_bit_identical():

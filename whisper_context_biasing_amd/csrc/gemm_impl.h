@@ -1899,22 +1899,30 @@ __global__ __launch_bounds__(NW * 64) void dec_xqk_kernel(XqkArgs<T> p) {
 // the folded q_proj weights and W_kt fragment-major); false: the caller keeps xq → kq
 template <typename T>
 static bool launch_xqk(const void* A, bool a_fm, const void* Wq_fm, const float* u, const float* c, const void* Wk_fm,
-                       void* qp, int M, int H, int D, hipStream_t s) {
+                       void* qp, int M, int H, int D, hipStream_t s, int nch = 8) {
   if constexpr (sizeof(T) != 2) {
     return false;
   } else {
     if (M > 64 || H * 64 != D || !A || !Wq_fm || !u || !c || !Wk_fm || !qp) return false;
+    if (nch != 2 && nch != 4 && nch != 8 && nch != 16) return false;
     XqkArgs<T> p{reinterpret_cast<const T*>(A), reinterpret_cast<const T*>(Wq_fm), u, c,
                  reinterpret_cast<const T*>(Wk_fm), reinterpret_cast<T*>(qp), M, H, D};
-    const dim3 grid(H * 8, (M + 15) / 16);
+    const dim3 grid(H * nch, (M + 15) / 16);
+    // NCH: q' column chunks per head (each chunk's workgroup recomputes q_h): 4 / 8 (default) / 16
+#define WCB_XQKN(nw, kpw, NC)                                                                              \
+  if (nch == NC) {                                                                                         \
+    if (a_fm) WCB_LAUNCH((dec_xqk_kernel<T, 1, nw, kpw, NC, true>), grid, dim3(nw * 64), 0, s, p);         \
+    else WCB_LAUNCH((dec_xqk_kernel<T, 1, nw, kpw, NC, false>), grid, dim3(nw * 64), 0, s, p);             \
+    return true;                                                                                           \
+  }
 #define WCB_XQK(k, nw, kpw)                                                                                \
   if (D == k) {                                                                                            \
-    if (a_fm) WCB_LAUNCH((dec_xqk_kernel<T, 1, nw, kpw, 8, true>), grid, dim3(nw * 64), 0, s, p);          \
-    else WCB_LAUNCH((dec_xqk_kernel<T, 1, nw, kpw, 8, false>), grid, dim3(nw * 64), 0, s, p);              \
-    return true;                                                                                           \
+    WCB_XQKN(nw, kpw, 8) WCB_XQKN(nw, kpw, 4) WCB_XQKN(nw, kpw, 2) WCB_XQKN(nw, kpw, 16)                    \
+    return false;                                                                                          \
   }
     WCB_XQK(512, 4, 4) WCB_XQK(768, 4, 6) WCB_XQK(1024, 4, 8) WCB_XQK(1280, 8, 5)
 #undef WCB_XQK
+#undef WCB_XQKN
     return false;
   }
 }
@@ -2429,7 +2437,8 @@ static void gemm_t(const GemmArgs& g, hipStream_t s) {
     // rows (measured C2: 1.074 vs 1.147 ms/token with 32-row workgroups); the LM head walks the
     // vocabulary persistently with 32-row workgroups, reading every weight tile once
     if (g.xqk_wk) {   // the fused cross query: the runtime sets it only where dec_xqk_kernel covers the launch
-      if (launch_xqk<T>(g.ln_a16, g.a_fm != 0, g.ln_wg_fm, g.ln_u, g.ln_c, g.xqk_wk, g.xqk_out, g.M, g.hs_H, g.K, s)) return;
+      if (launch_xqk<T>(g.ln_a16, g.a_fm != 0, g.ln_wg_fm, g.ln_u, g.ln_c, g.xqk_wk, g.xqk_out, g.M, g.hs_H, g.K, s,
+                        g.xqk_nch > 0 ? g.xqk_nch : 8)) return;
       throw std::runtime_error("internal error: fused cross query on a launch dec_xqk_kernel does not cover (M " +
                                std::to_string(g.M) + ", H " + std::to_string(g.hs_H) + ", K " + std::to_string(g.K) +
                                ", operands " + std::to_string(!!g.ln_a16) + std::to_string(!!g.ln_wg_fm) +

@@ -89,7 +89,7 @@ struct GemmArgs {
   int lean_mf2 = 0;                // lean projections: 32-row workgroups wherever M > 16 (default: N >= 2048 LN-fused)
   // greedy cross query (folded, lean): q'_h = W_k,hᵀ q_h in the same launch without a hand-off
   // (gemm_impl.h dec_xqk_kernel): W_kt fragment-major, q' rows [M][hs_H·K] (the q rows are not written)
-  const void* xqk_wk = nullptr; void* xqk_out = nullptr;
+  const void* xqk_wk = nullptr; void* xqk_out = nullptr; int xqk_nch = 0;   // (q' column chunks per head; 0: 8)
   const float* rst_in = nullptr; int rst_nb = 0;
   float* rst_out = nullptr;        // ring-tile residual writers: [M][N / 32] float2 partials of the written f32 rows
   // f16 encoder layers: the layer output is clamped to ±(finfo(f16).max − 1000)

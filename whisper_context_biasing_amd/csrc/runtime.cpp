@@ -227,6 +227,9 @@ struct wcb_handle {
   // head's q_h (gemm_impl.h dec_xqk_kernel; option "xqk"; needs lean_fold) instead of xq → kq: one launch
   // boundary less per layer, no hand-off. C2 20,423 / 20,431 / 20,382 vs 20,243 / 20,295 / 20,097 (interleaved)
   int xqk = 1;
+  // q' column chunks per head of the fused cross query (option "xqk_chunks": 2, 4, 8, 16; C2: 4 within noise of
+  // 8, 2 and 16 slower)
+  int xqk_nch = 8;
   // greedy range merge + W_v (16-bit partials): a head's 64 outputs over 1 or 2 workgroups (option "merge_os";
   // 2 measured slower: C2 20,114 / 20,074 / 20,080 vs 20,325 / 20,343 / 20,300, interleaved)
   int merge_os = 1;
@@ -738,6 +741,9 @@ int wcb_set_option(wcb_handle* h, const char* name, int value) {
     } else if (n == "merge_os") {
       REQUIRE(value == 1 || value == 2, "option merge_os: 1 or 2");
       h->merge_os = value;
+    } else if (n == "xqk_chunks") {
+      REQUIRE(value == 2 || value == 4 || value == 8 || value == 16, "option xqk_chunks: 2, 4, 8 or 16");
+      h->xqk_nch = value;
     } else if (n == "xqk") {
       h->xqk = value != 0;
     } else if (n == "lean_fold") {
@@ -1419,7 +1425,7 @@ void decode_rows(wcb_handle* h, const StepCfg& c, int b0, int nb, int chain, hip
       // q_h and q'_h in one launch without a hand-off (option xqk; the folded q_proj weights)
       const bool xqk = !kqf && h->xqk && h->lean && fm_ok && h->lean_fold && w.xq_wgfm && w.xkt_fm && w.lnx_u &&
                        H * 64 == d && (d == 512 || d == 768 || d == 1024 || d == 1280);
-      if (xqk) { xq.xqk_wk = w.xkt_fm; xq.xqk_out = dqp; xq.hs_H = H; }
+      if (xqk) { xq.xqk_wk = w.xkt_fm; xq.xqk_out = dqp; xq.hs_H = H; xq.xqk_nch = h->xqk_nch; }
       proj("dec_xq", xq);
       if (!kqf && !xqk) {
         GemmArgs kq = drow(dq, d, w.xkt_w, M, H * d, 64, dqp, (long)H * d);
